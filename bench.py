@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""bench.py -- AES-256 GiB/s on a device-resident packet batch (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): 1 M x 1 KiB random payloads, AES-256
+package mode, one connection key/IV.  One step = encrypt the whole batch (K2,
+one lane per packet chain) + decrypt it back (K1, one lane per 16-byte block),
+inputs resident in HBM before timing starts.
+
+value = payload bytes processed by all ranks (P*L encrypted + P*L decrypted per
+rank per step) / wall time of K steps (barrier + synchronize on both sides, max over
+ranks), in GiB/s -- i.e. the per-direction payload rate of the whole job.
+
+Multi-GPU: one process per GPU (torchrun); rank r encrypts/decrypts packets
+[r*P, (r+1)*P) of one global synthetic batch (weak scaling, no data-path collective;
+torch.distributed only for the barrier and the max-time reduction).
+
+Also reported: "roofline" for the dominant kernel (algorithmic bytes per launch /
+its mean HIP-event duration vs the 8 TB/s HBM peak) and "cpu_baseline" (the
+reference's own Encryptor compiled into oracle/_ref, timed on this host's cores).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import workloads as W  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=W.C2["packets"])
+    ap.add_argument("--length", type=int, default=W.C2["length"])
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--pcie", action="store_true", help="also time pinned H2D + kernels + D2H (for DESIGN.md)")
+    ap.add_argument("--only", choices=["encrypt", "decrypt"], default=None,
+                    help="profiling aid: run one direction only (not a bench line)")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_*.json), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(plain_host: np.ndarray, P: int, L: int, key: bytes, iv: bytes, target_s: float, gpu_cipher):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle, ref_available
+    kind = "reference" if ref_available() else "port"
+    o = Oracle(kind)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a small sample, then size the sample to ~target_s of wall time
+    n = min(P, 8192)
+    tmp = np.empty(n * L, np.uint8)
+    out = np.empty(n * L, np.uint8)
+    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, 1)
+    n = int(min(P, max(n, n * target_s / max(t, 1e-6))))
+    tmp = np.empty(n * L, np.uint8)
+    out = np.empty(n * L, np.uint8)
+    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, 1)
+    ok = bool(np.array_equal(tmp, gpu_cipher[:n * L])) and bool(np.array_equal(out, plain_host[:n * L]))
+    gib = 2.0 * n * L / t / 2**30
+    src = "oracle/_ref: reference base/rijndael.c + core/Encryptor.cpp (-O2)" if kind == "reference" \
+        else "oracle/aes_oracle.c restatement (-O2)"
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} x {L} B packets (first {n} of the C2 batch), PackageEncryptor::encrypt then "
+                      f"::decrypt per packet, {threads} threads; {src}; {t:.2f} s wall; matches GPU output: {ok}",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pcie_rate(eng, ks, P, L, steps=3):
+    """Pinned host buffers -> H2D -> encrypt -> D2H (and the reverse for decrypt)."""
+    n = P * L
+    h_in = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    eng.fill_synthetic(d_in, 2)
+    h_in.copy_(d_in)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        d_in.copy_(h_in, non_blocking=True)
+        eng.package_encrypt(d_in, d_out, P, ks, stride=L, uniform_len=L)
+        h_out.copy_(d_out, non_blocking=True)
+        d_in.copy_(h_out, non_blocking=True)
+        eng.package_decrypt(d_in, d_out, P, ks, stride=L, uniform_len=L)
+        h_out.copy_(d_out, non_blocking=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ok = torch.equal(h_out, h_in)
+    return {"value": round(2.0 * n * steps / dt / 2**30, 3), "unit": "GiB/s",
+            "note": "host pinned -> H2D -> kernel -> D2H per direction, serialized on one stream", "roundtrip_ok": ok}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import fpnn_amd
+
+    P, L = args.packets, args.length
+    cfg = W.C2
+    key, iv = W.single_key(cfg)
+    eng = fpnn_amd.Engine(local)  # queues on torch's current stream of this device
+    ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+    nbytes = P * L
+    plain = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    eng.fill_synthetic(plain, cfg["payload_seed"], byte_offset=rank * nbytes)  # this rank's shard
+    cipher = torch.empty_like(plain)
+    back = torch.empty_like(plain)
+
+    def step():
+        if args.only != "decrypt":
+            eng.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L)
+        if args.only != "encrypt":
+            eng.package_decrypt(cipher, back, P, ks, stride=L, uniform_len=L)
+
+    if args.only == "decrypt":
+        eng.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    eng.reset_stats()
+    eng.set_timing(True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    elapsed = max_over_ranks(elapsed, world)
+    n_enc, ms_enc = eng.kernel_stats(fpnn_amd.K_ENCRYPT)
+    n_dec, ms_dec = eng.kernel_stats(fpnn_amd.K_DECRYPT)
+
+    verify = {}
+    if not args.no_verify:
+        if args.only is None:
+            verify["roundtrip_ok"] = bool(torch.equal(back, plain))
+        if rank == 0 and P == cfg["packets"] and L == cfg["length"]:
+            with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+                gold = json.load(f)["C2"]
+            verify["cipher_sha256_matches_reference"] = \
+                hashlib.sha256(cipher.cpu().numpy()).hexdigest() == gold["cipher_sha256"]
+
+    directions = 2 if args.only is None else 1
+    payload = float(directions) * nbytes * world * args.steps
+    value = payload / elapsed / 2**30
+
+    # roofline for the dominant kernel: algorithmic bytes per launch
+    alg_bytes = 2.0 * nbytes + 28.0 * P + 244.0 * 1
+    kernels = {}
+    for name, n, ms in (("cfb_encrypt_chains", n_enc, ms_enc), ("cfb_decrypt_blocks", n_dec, ms_dec)):
+        if n:
+            avg_s = ms / n / 1e3
+            ach = alg_bytes / avg_s / 1e9
+            kernels[name] = {"launches": n, "avg_ms": round(ms / n, 4), "achieved_GBs": round(ach, 1),
+                             "payload_GiBs": round(nbytes / avg_s / 2**30, 2)}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+    ach = kernels[dom]["achieved_GBs"]
+    traffic = load_traffic(dom)
+    roofline = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "alg_bytes_per_launch": int(alg_bytes), "kernels": kernels}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host_plain = plain.cpu().numpy()
+        cpu = cpu_baseline(host_plain, P, L, key, iv, args.cpu_seconds, cipher.cpu().numpy())
+
+    extra = {}
+    if args.pcie and rank == 0:
+        extra["pcie_inclusive"] = pcie_rate(eng, ks, P, L)
+
+    if rank == 0:
+        line = {
+            "metric": "AES-256 GiB/s on device-resident packet batch",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter splitmix64 payload, seed 2; key/IV from seed 1002)",
+            "config": {"workload": "C2: 1M x 1 KiB AES-256 package-mode CFB encrypt+decrypt per GPU",
+                       "packets_per_gpu": P, "payload_bytes": L, "key_bits": 256, "mode": "package",
+                       "global_packets": P * world, "parallelism": f"packet-shard x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "verify": verify,
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

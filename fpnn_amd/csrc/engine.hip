@@ -1,0 +1,594 @@
+// engine.hip -- implementation of the C-ABI declared in include/fpnn_aes.h.
+//
+// Host-side responsibilities only: argument checking, key-set management, scratch
+// sizing, choosing the kernel variant (uniform vs general layout, uniform vs
+// per-packet keys, package vs stream, in-place) and queuing it on the engine's
+// HIP stream.  There is no CPU cipher in this library: every byte of payload is
+// transformed by the HIP kernels in kernels.hip.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fpnn_aes.h"
+#include "aes_common.hpp"
+#include "kernels.hpp"
+
+using namespace fpnn_aes;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t err, const char *what) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(err), (int)err);
+    g_last_error = buf;
+    return FPNN_AES_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                          \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);      \
+    } while (0)
+
+struct EventPair {
+    hipEvent_t beg, end;
+};
+
+}  // namespace
+
+struct fpnn_aes_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 256;
+    uint8_t *d_tables = nullptr;  // t0le[256] (1 KiB) then sbox[256]
+    // general-layout scratch
+    uint64_t *d_bstart = nullptr;
+    uint64_t cap_bstart = 0;
+    uint64_t *d_wgsums = nullptr;
+    uint64_t cap_wgsums = 0;
+    uint64_t *d_tile = nullptr;
+    uint64_t cap_tile = 0;
+    uint4 *d_boundary = nullptr;
+    uint64_t cap_boundary = 0;
+    uint64_t *d_total = nullptr;
+    uint64_t *h_total = nullptr;  // pinned
+    // host staging for fpnn_aes_cfb_host
+    uint8_t *h_stage = nullptr;
+    uint8_t *d_stage = nullptr;
+    uint64_t cap_stage = 0;
+    // instrumentation
+    bool timing = false;
+    std::vector<EventPair> ev[2];
+    size_t ev_used[2] = {0, 0};
+};
+
+struct fpnn_aes_keyset {
+    fpnn_aes_engine *e = nullptr;
+    DevKey *d_keys = nullptr;
+    uint32_t count = 0;
+    int nrounds = 0;
+    uint32_t keylen = 0;
+};
+
+namespace {
+
+const uint32_t *t0le_of(const fpnn_aes_engine *e) { return reinterpret_cast<const uint32_t *>(e->d_tables); }
+const uint8_t *sbox_of(const fpnn_aes_engine *e) { return e->d_tables + 1024; }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <class T>
+int grow(T *&ptr, uint64_t &cap, uint64_t need) {
+    if (need <= cap) return FPNN_AES_OK;
+    uint64_t n = cap ? cap : 1024;
+    while (n < need) n *= 2;
+    if (ptr) HIP_TRY(hipFree(ptr));
+    ptr = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ptr), n * sizeof(T)));
+    cap = n;
+    return FPNN_AES_OK;
+}
+
+int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
+    *pair = nullptr;
+    if (!e->timing) return FPNN_AES_OK;
+    auto &v = e->ev[which];
+    if (e->ev_used[which] == v.size()) {
+        EventPair p;
+        HIP_TRY(hipEventCreate(&p.beg));
+        HIP_TRY(hipEventCreate(&p.end));
+        v.push_back(p);
+    }
+    *pair = &v[e->ev_used[which]++];
+    HIP_TRY(hipEventRecord((*pair)->beg, e->stream));
+    return FPNN_AES_OK;
+}
+
+int timing_end(fpnn_aes_engine *e, EventPair *pair) {
+    if (pair) HIP_TRY(hipEventRecord(pair->end, e->stream));
+    return FPNN_AES_OK;
+}
+
+// ceil(2^64 / d) for 1 <= d < 2^32
+uint64_t magic_for(uint32_t d) {
+    if (d == 1) return 0;  // unused: fast path divides by 1 via umulhi(g, 0) -> wrong, handled below
+    const unsigned __int128 one = (unsigned __int128)1 << 64;
+    return (uint64_t)((one + d - 1) / d);
+}
+
+int check_batch(const fpnn_aes_engine *e, const fpnn_aes_batch *b) {
+    if (!e || !b || !b->keys) return FPNN_AES_ERR_ARG;
+    if (b->count && (!b->in || !b->out)) return FPNN_AES_ERR_ARG;
+    if (b->keys->e && b->keys->e->device != e->device) return FPNN_AES_ERR_ARG;
+    if (b->keys->count == 0) return FPNN_AES_ERR_ARG;
+    return FPNN_AES_OK;
+}
+
+KBatch make_kbatch(const fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state) {
+    KBatch k;
+    memset(&k, 0, sizeof k);
+    k.in = b->in;
+    k.out = b->out;
+    k.count = b->count;
+    k.stride = b->stride;
+    k.uniform_len = b->uniform_len;
+    k.flags = b->flags;
+    k.in_off = b->in_off;
+    k.out_off = b->out_off;
+    k.len = b->len;
+    k.key_slot = b->key_slot;
+    k.keys = b->keys->d_keys;
+    k.iv_state = iv_state;
+    k.pos_state = pos_state;
+    k.t0le = t0le_of(e);
+    return k;
+}
+
+bool is_uniform_layout(const fpnn_aes_batch *b) {
+    return !b->in_off && !b->out_off && !b->len && !b->key_slot;
+}
+
+int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
+    int rc = check_batch(e, b);
+    if (rc) return rc;
+    if (stream && b->count && (!iv_state || !pos_state || ((uintptr_t)iv_state & 15))) return FPNN_AES_ERR_ARG;
+    if (!stream && (b->flags & FPNN_AES_F_WIRE_PREFIX) && (b->out_off == nullptr && b->in == b->out))
+        return FPNN_AES_ERR_ARG;  // the 4-byte prefix needs a distinct output layout
+    if (!b->count) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    KBatch k = make_kbatch(e, b, iv_state, pos_state);
+    const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
+    const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
+    const uint64_t want = (b->count + kThreads - 1) / kThreads;
+    const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+    EventPair *ev;
+    if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, e->stream));
+    return timing_end(e, ev);
+}
+
+int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
+    int rc = check_batch(e, b);
+    if (rc) return rc;
+    if (stream && b->count && (!iv_state || !pos_state || ((uintptr_t)iv_state & 15))) return FPNN_AES_ERR_ARG;
+    if (b->flags & FPNN_AES_F_WIRE_PREFIX) return FPNN_AES_ERR_ARG;
+    if (!b->count) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    KBatch k = make_kbatch(e, b, iv_state, pos_state);
+    const bool inplace = b->in == b->out && b->out_off == nullptr;
+    const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
+    // Uniform layout: every segment has the same block count, known on the host.
+    // (Stream mode only when there is a single segment, whose position the caller
+    // supplies through the host path; otherwise positions differ per stream.)
+    Layout layout = LAYOUT_GENERAL;
+    if (is_uniform_layout(b) && !stream) {
+        const uint64_t nb = ((uint64_t)b->uniform_len + 15) >> 4;
+        const uint64_t total = nb * b->count;
+        if (nb > 0 && total < (1ull << 32) && nb > 1) {
+            layout = LAYOUT_UNIFORM;
+            k.total_blocks = total;
+            k.nb_uniform = (uint32_t)nb;
+            k.magic = magic_for((uint32_t)nb);
+        }
+    }
+    if (layout == LAYOUT_GENERAL) {
+        const uint64_t nwg = (b->count + 1023) / 1024;
+        if ((rc = grow(e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
+        if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
+        HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        const uint64_t total = *e->h_total;
+        if (!total) return FPNN_AES_OK;
+        const uint64_t nchunks = (total + 63) >> 6;
+        if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
+        HIP_TRY(launch_tile_map(k, stream, e->d_bstart, e->d_tile, nchunks, e->stream));
+        k.total_blocks = total;
+        k.bstart = e->d_bstart;
+        k.tile_first = e->d_tile;
+    }
+    const uint64_t nchunks = (k.total_blocks + 63) >> 6;
+    if (inplace) {
+        if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks))) return rc;
+        HIP_TRY(launch_boundary_save(k, layout, stream, e->d_boundary, nchunks, e->stream));
+        k.boundary = e->d_boundary;
+    }
+    const uint64_t want = (nchunks + 15) / 16;  // 16 waves per workgroup
+    const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+    EventPair *ev;
+    if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, layout, km, stream, inplace, grid, e->stream));
+    return timing_end(e, ev);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+
+extern "C" {
+
+const char *fpnn_aes_strerror(int status) {
+    switch (status) {
+        case FPNN_AES_OK: return "ok";
+        case FPNN_AES_ERR_KEYLEN: return "key length must be 16, 24 or 32 bytes";
+        case FPNN_AES_ERR_ARG: return "invalid argument";
+        case FPNN_AES_ERR_RANGE: return "batch too large";
+        case FPNN_AES_ERR_HIP: return "HIP runtime error";
+        case FPNN_AES_ERR_NODEV: return "no usable gfx950 device";
+        default: return "unknown status";
+    }
+}
+
+const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
+
+const char *fpnn_aes_version(void) {
+    return "fpnn_aes 0.1 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
+           "K1 lane-per-block decrypt, K2 lane-per-chain encrypt)";
+}
+
+int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen) {
+    if (!ctx || !key) return FPNN_AES_ERR_ARG;
+    const int nr = expand_key_be(ctx->rk, key, keylen);
+    ctx->nrounds = nr;
+    return nr ? FPNN_AES_OK : FPNN_AES_ERR_KEYLEN;
+}
+
+int fpnn_aes_device_count(int *count) {
+    if (!count) return FPNN_AES_ERR_ARG;
+    int n = 0;
+    hipError_t err = hipGetDeviceCount(&n);
+    if (err != hipSuccess) {
+        *count = 0;
+        hip_fail(err, "hipGetDeviceCount");
+        return FPNN_AES_ERR_NODEV;
+    }
+    *count = n;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) {
+    if (!out) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        g_last_error = "no HIP device with that index";
+        return FPNN_AES_ERR_NODEV;
+    }
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_last_error = std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950";
+        return FPNN_AES_ERR_NODEV;
+    }
+    DeviceGuard g(device);
+    fpnn_aes_engine *e = new fpnn_aes_engine();
+    e->device = device;
+    e->num_cus = prop.multiProcessorCount;
+    int rc = FPNN_AES_OK;
+    do {
+        if (hip_stream != FPNN_AES_OWN_STREAM) {
+            e->stream = (hipStream_t)hip_stream;  // NULL: the null stream
+        } else {
+            hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+            if (err != hipSuccess) { rc = hip_fail(err, "hipStreamCreate"); break; }
+            e->own_stream = true;
+        }
+        hipError_t err = hipMalloc(reinterpret_cast<void **>(&e->d_tables), 1024 + 256);
+        if (err != hipSuccess) { rc = hip_fail(err, "hipMalloc(tables)"); break; }
+        err = hipMemcpy(e->d_tables, kTables.t0le, 1024, hipMemcpyHostToDevice);
+        if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1024, kTables.sbox, 256, hipMemcpyHostToDevice);
+        if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
+        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), sizeof(uint64_t));
+        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), sizeof(uint64_t), 0);
+        if (err != hipSuccess) { rc = hip_fail(err, "alloc(total)"); break; }
+    } while (0);
+    if (rc) {
+        fpnn_aes_engine_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
+    if (!e) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    (void)hipFree(e->d_tables);
+    (void)hipFree(e->d_bstart);
+    (void)hipFree(e->d_wgsums);
+    (void)hipFree(e->d_tile);
+    (void)hipFree(e->d_boundary);
+    (void)hipFree(e->d_total);
+    (void)hipFree(e->d_stage);
+    if (e->h_total) (void)hipHostFree(e->h_total);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    for (auto &v : e->ev)
+        for (auto &p : v) {
+            (void)hipEventDestroy(p.beg);
+            (void)hipEventDestroy(p.end);
+        }
+    if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_sync(fpnn_aes_engine *e) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return FPNN_AES_OK;
+}
+
+void *fpnn_aes_engine_stream(fpnn_aes_engine *e) { return e ? (void *)e->stream : nullptr; }
+
+int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t max_blocks) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    int rc;
+    if ((rc = grow(e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
+    if ((rc = grow(e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
+    const uint64_t nchunks = (max_blocks + 63) / 64;
+    if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
+    if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
+    return FPNN_AES_OK;
+}
+
+// ---- key sets ---------------------------------------------------------------
+
+int fpnn_aes_keyset_create(fpnn_aes_engine *e, uint32_t count, size_t keylen, const uint8_t *keys,
+                           const uint8_t *ivs, int keys_on_host, fpnn_aes_keyset **out) {
+    if (!e || !out || !keys || count == 0) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    if (keylen != 16 && keylen != 24 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
+    DeviceGuard g(e->device);
+    fpnn_aes_keyset *ks = new fpnn_aes_keyset();
+    ks->e = e;
+    ks->count = count;
+    ks->keylen = (uint32_t)keylen;
+    ks->nrounds = (int)keylen / 4 + 6;
+    uint8_t *d_raw = nullptr;
+    int rc = FPNN_AES_OK;
+    do {
+        hipError_t err = hipMalloc(reinterpret_cast<void **>(&ks->d_keys), sizeof(DevKey) * (size_t)count);
+        if (err != hipSuccess) { rc = hip_fail(err, "hipMalloc(keys)"); break; }
+        const uint8_t *k_dev = keys, *iv_dev = ivs;
+        if (keys_on_host) {
+            const size_t kb = (size_t)count * keylen, ib = ivs ? (size_t)count * 16 : 0;
+            err = hipMalloc(reinterpret_cast<void **>(&d_raw), kb + ib);
+            if (err == hipSuccess) err = hipMemcpy(d_raw, keys, kb, hipMemcpyHostToDevice);
+            if (err == hipSuccess && ivs) err = hipMemcpy(d_raw + kb, ivs, ib, hipMemcpyHostToDevice);
+            if (err != hipSuccess) { rc = hip_fail(err, "upload(keys)"); break; }
+            k_dev = d_raw;
+            iv_dev = ivs ? d_raw + kb : nullptr;
+        }
+        err = launch_expand_keys(k_dev, (uint32_t)keylen, iv_dev, count, sbox_of(e), ks->d_keys, e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "expand_keys"); break; }
+    } while (0);
+    if (d_raw) (void)hipFree(d_raw);
+    if (rc) {
+        fpnn_aes_keyset_destroy(ks);
+        return rc;
+    }
+    *out = ks;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpnn_aes_schedule *ctx,
+                                   const uint8_t *ivs, fpnn_aes_keyset **out) {
+    if (!e || !out || !ctx || count == 0) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    const int nr = ctx[0].nrounds;
+    if (nr != 10 && nr != 12 && nr != 14) return FPNN_AES_ERR_KEYLEN;
+    std::vector<DevKey> host(count);
+    for (uint32_t i = 0; i < count; i++) {
+        if (ctx[i].nrounds != nr) return FPNN_AES_ERR_ARG;
+        DevKey &d = host[i];
+        memset(&d, 0, sizeof d);
+        for (int k = 0; k < 4 * (nr + 1); k++) d.rk[k] = bswap32(ctx[i].rk[k]);
+        d.nrounds = (uint32_t)nr;
+        d.keylen = (uint32_t)(nr - 6) * 4;
+        if (ivs) memcpy(d.iv, ivs + 16 * (size_t)i, 16);
+    }
+    DeviceGuard g(e->device);
+    fpnn_aes_keyset *ks = new fpnn_aes_keyset();
+    ks->e = e;
+    ks->count = count;
+    ks->nrounds = nr;
+    ks->keylen = (uint32_t)(nr - 6) * 4;
+    hipError_t err = hipMalloc(reinterpret_cast<void **>(&ks->d_keys), sizeof(DevKey) * (size_t)count);
+    if (err == hipSuccess) err = hipMemcpy(ks->d_keys, host.data(), sizeof(DevKey) * (size_t)count, hipMemcpyHostToDevice);
+    if (err != hipSuccess) {
+        int rc = hip_fail(err, "upload(schedules)");
+        fpnn_aes_keyset_destroy(ks);
+        return rc;
+    }
+    *out = ks;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks) {
+    if (!ks) return FPNN_AES_OK;
+    if (ks->d_keys) {
+        DeviceGuard g(ks->e->device);
+        (void)hipStreamSynchronize(ks->e->stream);
+        (void)hipFree(ks->d_keys);
+    }
+    delete ks;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_keyset_nrounds(const fpnn_aes_keyset *ks) { return ks ? ks->nrounds : 0; }
+
+int fpnn_aes_keyset_get_schedule(fpnn_aes_keyset *ks, uint32_t slot, fpnn_aes_schedule *out) {
+    if (!ks || !out || slot >= ks->count) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(ks->e->device);
+    DevKey d;
+    HIP_TRY(hipMemcpy(&d, ks->d_keys + slot, sizeof d, hipMemcpyDeviceToHost));
+    memset(out, 0, sizeof *out);
+    out->nrounds = (int)d.nrounds;
+    for (int k = 0; k < 4 * ((int)d.nrounds + 1); k++) out->rk[k] = bswap32(d.rk[k]);
+    return FPNN_AES_OK;
+}
+
+// ---- batches ---------------------------------------------------------------------
+
+int fpnn_aes_package_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b) {
+    return run_encrypt(e, b, nullptr, nullptr, false);
+}
+
+int fpnn_aes_package_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b) {
+    return run_decrypt(e, b, nullptr, nullptr, false);
+}
+
+int fpnn_aes_stream_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state) {
+    if (b && (b->flags & FPNN_AES_F_WIRE_PREFIX)) return FPNN_AES_ERR_ARG;
+    return run_encrypt(e, b, iv_state, pos_state, true);
+}
+
+int fpnn_aes_stream_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state) {
+    return run_decrypt(e, b, iv_state, pos_state, true);
+}
+
+// ---- single call from host memory ------------------------------------------------
+
+int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in,
+                      uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num) {
+    if (!e || !ctx || !ivec || !p_num || (len && (!in || !out))) return FPNN_AES_ERR_ARG;
+    const int nr = ctx->nrounds;
+    if (nr != 10 && nr != 12 && nr != 14) return FPNN_AES_ERR_KEYLEN;
+    if (*p_num > 15) return FPNN_AES_ERR_ARG;
+    if (len == 0) return FPNN_AES_OK;
+    if (len > 0xffffffffull) return FPNN_AES_ERR_RANGE;
+    DeviceGuard g(e->device);
+    // staging layout: [DevKey 272][iv 16][pos 4 | pad 12][payload len] ... [out len]
+    const uint64_t hdr = sizeof(DevKey) + 32;
+    const uint64_t pay = (len + 15) & ~15ull;
+    const uint64_t need = hdr + 2 * pay;
+    if (need > e->cap_stage) {
+        uint64_t n = e->cap_stage ? e->cap_stage : 65536;
+        while (n < need) n *= 2;
+        if (e->h_stage) (void)hipHostFree(e->h_stage);
+        if (e->d_stage) (void)hipFree(e->d_stage);
+        e->h_stage = nullptr;
+        e->d_stage = nullptr;
+        e->cap_stage = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_stage), n, 0));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stage), n));
+        e->cap_stage = n;
+    }
+    DevKey *hk = reinterpret_cast<DevKey *>(e->h_stage);
+    memset(hk, 0, sizeof *hk);
+    for (int k = 0; k < 4 * (nr + 1); k++) hk->rk[k] = bswap32(ctx->rk[k]);
+    hk->nrounds = (uint32_t)nr;
+    uint8_t *h_iv = e->h_stage + sizeof(DevKey);
+    uint32_t *h_pos = reinterpret_cast<uint32_t *>(h_iv + 16);
+    memcpy(h_iv, ivec, 16);
+    *h_pos = (uint32_t)*p_num;
+    memcpy(e->h_stage + hdr, in, len);
+    HIP_TRY(hipMemcpyAsync(e->d_stage, e->h_stage, hdr + len, hipMemcpyHostToDevice, e->stream));
+
+    fpnn_aes_keyset ks;
+    ks.e = e;
+    ks.d_keys = reinterpret_cast<DevKey *>(e->d_stage);
+    ks.count = 1;
+    ks.nrounds = nr;
+    ks.keylen = (uint32_t)(nr - 6) * 4;
+    uint8_t *d_iv = e->d_stage + sizeof(DevKey);
+    uint32_t *d_pos = reinterpret_cast<uint32_t *>(d_iv + 16);
+    fpnn_aes_batch b;
+    memset(&b, 0, sizeof b);
+    b.in = e->d_stage + hdr;
+    b.out = e->d_stage + hdr + pay;
+    b.count = 1;
+    b.uniform_len = (uint32_t)len;
+    b.stride = 0;
+    b.keys = &ks;
+    int rc = encrypt ? run_encrypt(e, &b, d_iv, d_pos, true) : run_decrypt(e, &b, d_iv, d_pos, true);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(h_iv, d_iv, 32, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + pay, e->d_stage + hdr + pay, len, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    memcpy(out, e->h_stage + hdr + pay, len);
+    memcpy(ivec, h_iv, 16);
+    *p_num = *h_pos;
+    return FPNN_AES_OK;
+}
+
+// ---- utilities --------------------------------------------------------------------------
+
+int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset) {
+    if (!e || (nbytes && !dst)) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    HIP_TRY(launch_fill_synthetic(dst, nbytes, seed, byte_offset, e->num_cus * 8, e->stream));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_set_timing(fpnn_aes_engine *e, int enable) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    e->timing = enable != 0;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_kernel_stats(fpnn_aes_engine *e, int which, uint64_t *launches, double *total_ms) {
+    if (!e || which < 0 || which > 1 || !launches || !total_ms) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    double sum = 0;
+    for (size_t i = 0; i < e->ev_used[which]; i++) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, e->ev[which][i].beg, e->ev[which][i].end));
+        sum += ms;
+    }
+    *launches = e->ev_used[which];
+    *total_ms = sum;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    e->ev_used[0] = e->ev_used[1] = 0;
+    return FPNN_AES_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,545 @@
+// kernels.hip -- hand-written CDNA4 (gfx950) kernels for FPNN's AES-CFB path.
+//
+//   K1 k_cfb_decrypt_blocks : CFB-128 decryption, one lane per 16-byte block.
+//        P_i = C_i ^ E(C_{i-1}), C_{-1} = IV (base/rijndael.c:1189-1197).  Every
+//        C is known up front, so all blocks of all packets run in parallel; lane l
+//        gets C_{i-1} from lane l-1 by DPP wave_shr:1, only lane 0 reloads it.
+//   K2 k_cfb_encrypt_chains : CFB-128 encryption, one lane per packet / stream chain.
+//        C_i = P_i ^ E(C_{i-1}) is serial inside a chain (base/rijndael.c:1176-1185),
+//        so parallelism is across packets (package mode) or streams (stream mode).
+//   Both keep the T-table image in LDS (aes_device.hpp) and are persistent: one
+//   1024-thread workgroup per CU walks the work with a grid stride.
+//
+//   Segments follow the reference's exact byte semantics (rijndael_cfb_encrypt's
+//   (ivec, pos) carry): a stream segment that starts at CFB position n0 != 0 first
+//   consumes the keystream bytes ivec[n0..15]; block alignment is relative to the
+//   stream, not to memory; partial final blocks leave (ivec, pos) exactly as the
+//   reference's byte loop does.  Package mode is the special case n0 = 0,
+//   ivec = connection IV, state discarded (core/Encryptor.cpp:10-32).
+#include "aes_device.hpp"
+#include "kernels.hpp"
+
+namespace fpnn_aes {
+
+struct Seg {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t len;
+    uint32_t slot;
+};
+
+template <int LAYOUT>
+__device__ __forceinline__ Seg get_seg(const KBatch &b, uint64_t s) {
+    Seg g;
+    if (LAYOUT == LAYOUT_UNIFORM) {
+        const uint64_t o = s * b.stride;
+        g.in = b.in + o;
+        g.out = b.out + o;
+        g.len = b.uniform_len;
+        g.slot = 0;
+    } else {
+        const uint64_t io = b.in_off ? b.in_off[s] : s * b.stride;
+        const uint64_t oo = b.out_off ? b.out_off[s] : io;
+        g.in = b.in + io;
+        g.out = b.out + oo;
+        g.len = b.len ? b.len[s] : b.uniform_len;
+        g.slot = b.key_slot ? b.key_slot[s] : 0u;
+    }
+    return g;
+}
+
+__device__ __forceinline__ uint4 ld_state_iv(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+
+// Virtual (stream-aligned) block `bi` of a segment that starts at CFB position n0:
+// bytes j < n0 of block 0 come from the carried ivec (they are the ciphertext bytes
+// already consumed, base/rijndael.c:1182,1195), data bytes from the segment.
+__device__ __forceinline__ uint4 load_cx(const Seg &g, uint32_t n0, uint32_t bi, const uint4 &ivs) {
+    const int64_t vlo = 16 * (int64_t)bi;
+    const int lo = bi == 0 ? (int)n0 : 0;
+    const int64_t hi64 = (int64_t)n0 + g.len - vlo;
+    const int hi = hi64 > 16 ? 16 : (int)hi64;
+    const uint8_t *base = g.in + (vlo - (int64_t)n0);
+    if (lo == 0 && hi == 16) return load16(base);
+    uint4 d = load_bytes(base, lo, hi);
+    if (lo != 0) d = select_bytes(byte_mask(0, lo), ivs, d);
+    return d;
+}
+
+__device__ __forceinline__ void store_cx(const Seg &g, uint32_t n0, uint32_t bi, const uint4 &v) {
+    const int64_t vlo = 16 * (int64_t)bi;
+    const int lo = bi == 0 ? (int)n0 : 0;
+    const int64_t hi64 = (int64_t)n0 + g.len - vlo;
+    const int hi = hi64 > 16 ? 16 : (int)hi64;
+    uint8_t *base = g.out + (vlo - (int64_t)n0);
+    if (lo == 0 && hi == 16)
+        store16(base, v);
+    else
+        store_bytes(base, v, lo, hi);
+}
+
+__device__ __forceinline__ uint64_t seg_blocks(uint32_t len, uint32_t n0) {
+    return len ? ((uint64_t)n0 + len + 15) >> 4 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// K2: encryption, one lane per chain.
+
+template <int NR, int LAYOUT, int KM, bool STREAM>
+__global__ __launch_bounds__(kThreads, 1) void k_cfb_encrypt_chains(KBatch b) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    lds_fill_tables(lds4, b.t0le);
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const LaneBase lb;
+
+    RoundKeys<NR> rku;
+    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        RoundKeys<NR> rk;
+        if (KM == KEY_UNIFORM)
+            rk = rku;
+        else
+            rk = load_round_keys<NR>(key);
+
+        uint4 iv;
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = ld_state_iv(b.iv_state + 16 * s);
+            n = b.pos_state[s];
+        } else {
+            iv = *reinterpret_cast<const uint4 *>(key->iv);
+        }
+        const uint8_t *p = g.in;
+        uint8_t *q = g.out;
+        uint32_t rem = g.len;
+
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
+            q[0] = (uint8_t)rem;
+            q[1] = (uint8_t)(rem >> 8);
+            q[2] = (uint8_t)(rem >> 16);
+            q[3] = (uint8_t)(rem >> 24);
+            q += 4;
+        }
+
+        if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = (int)n, hi = (int)(n + take);
+            const uint4 o = load_bytes(p - n, lo, hi) ^ iv;
+            store_bytes(q - n, o, lo, hi);
+            iv = select_bytes(byte_mask(lo, hi), o, iv);
+            p += take;
+            q += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+
+        const uint32_t nfull = rem >> 4;
+        uint4 pt = nfull ? load16(p) : make_uint4(0, 0, 0, 0);
+        for (uint32_t i = 0; i < nfull; i++) {
+            const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
+            iv = aes_encrypt_block<NR>(iv, rk, lds, lb) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            store16(q, iv);
+            pt = pn;
+            p += 16;
+            q += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
+            const uint4 ks = aes_encrypt_block<NR>(iv, rk, lds, lb);
+            const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
+            store_bytes(q, o, 0, (int)rem);
+            iv = select_bytes(byte_mask(0, (int)rem), o, ks);
+            n = rem;
+        }
+        if (STREAM) {
+            *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = iv;
+            b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: decryption, one lane per virtual block, 64 consecutive blocks per wave step.
+
+template <int LAYOUT>
+__device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64_t gblk, uint64_t total, uint64_t &s,
+                                             uint32_t &bi) {
+    if (LAYOUT == LAYOUT_UNIFORM) {
+        const uint32_t g32 = (uint32_t)(gblk < total ? gblk : total - 1);
+        const uint32_t q = fast_div(g32, b.magic);
+        s = q;
+        bi = g32 - q * b.nb_uniform;
+    } else {
+        const uint64_t gg = gblk < total ? gblk : total - 1;
+        uint64_t lo = b.tile_first[c], hi = b.tile_first[c + 1];
+        while (lo < hi) {  // largest s in [lo, hi] with bstart[s] <= gg
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if (b.bstart[mid] <= gg)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        s = lo;
+        bi = (uint32_t)(gg - b.bstart[lo]);
+    }
+}
+
+template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE>
+__global__ __launch_bounds__(kThreads, 1) void k_cfb_decrypt_blocks(KBatch b) {
+    __shared__ uint4 lds4[kLdsBytes / 16];
+    lds_fill_tables(lds4, b.t0le);
+    __syncthreads();
+    const char *lds = reinterpret_cast<const char *>(lds4);
+    const LaneBase lb;
+    const uint32_t lane = threadIdx.x & 63u;
+
+    RoundKeys<NR> rku;
+    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+
+    const uint64_t total = b.total_blocks;
+    const uint64_t nchunks = (total + 63) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nchunks; c += nwaves) {
+        const uint64_t gblk = (c << 6) + lane;
+        const bool valid = gblk < total;
+        uint64_t s;
+        uint32_t bi;
+        locate_block<LAYOUT>(b, c, gblk, total, s, bi);
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const uint32_t n0 = STREAM ? b.pos_state[s] : 0u;
+        const uint32_t slot = KM == KEY_UNIFORM ? 0u : g.slot;
+        const DevKey *key = b.keys + slot;
+        const uint4 ivs = STREAM ? ld_state_iv(b.iv_state + 16 * s) : *reinterpret_cast<const uint4 *>(key->iv);
+
+        const uint4 x = valid ? load_cx(g, n0, bi, ivs) : make_uint4(0, 0, 0, 0);
+        uint4 xp = wave_shr1(x);  // C_{i-1} from the neighbouring lane (all 64 lanes active here)
+        if (lane == 0 && bi != 0 && valid) xp = INPLACE ? b.boundary[c] : load_cx(g, n0, bi - 1, ivs);
+        const uint4 kin = bi == 0 ? ivs : xp;
+
+        uint4 ks;
+        if (KM == KEY_UNIFORM) {
+            ks = aes_encrypt_block<NR>(kin, rku, lds, lb);
+        } else {
+            const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slot);
+            const uint32_t my = valid ? slot : slot0;
+            if (__builtin_amdgcn_ballot_w64(my != slot0) == 0) {  // wave-uniform key: SGPR round keys
+                const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + slot0);
+                ks = aes_encrypt_block<NR>(kin, rk, lds, lb);
+            } else {
+                const RoundKeys<NR> rk = load_round_keys<NR>(key);
+                ks = aes_encrypt_block<NR>(kin, rk, lds, lb);
+            }
+        }
+        if (STREAM && bi == 0 && n0 != 0) ks = ivs;  // keystream block already in the carried state
+
+        if (valid) {
+            const uint4 o = x ^ ks;
+            store_cx(g, n0, bi, o);
+            if (STREAM && (uint64_t)bi + 1 == seg_blocks(g.len, n0)) {  // last block: export (ivec, pos)
+                const uint32_t pos = (n0 + g.len) & 15u;
+                const uint4 nv = pos ? select_bytes(byte_mask(0, (int)pos), x, ks) : x;
+                *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = nv;
+                b.pos_state[s] = pos;
+            }
+        }
+    }
+}
+
+// In-place decryption: save the ciphertext block that precedes every 64-block chunk
+// before any wave overwrites it.
+template <int LAYOUT, bool STREAM>
+__global__ __launch_bounds__(256) void k_boundary_save(KBatch b, uint4 *boundary, uint64_t nchunks) {
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t s;
+        uint32_t bi;
+        locate_block<LAYOUT>(b, c, c << 6, b.total_blocks, s, bi);
+        if (bi == 0) continue;
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const uint32_t n0 = STREAM ? b.pos_state[s] : 0u;
+        const DevKey *key = b.keys + g.slot;
+        const uint4 ivs = STREAM ? ld_state_iv(b.iv_state + 16 * s) : *reinterpret_cast<const uint4 *>(key->iv);
+        boundary[c] = load_cx(g, n0, bi - 1, ivs);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// General-layout block map: exclusive scan of per-segment block counts.
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+template <bool STREAM>
+__device__ __forceinline__ uint64_t nblocks_of(const KBatch &b, uint64_t s) {
+    if (s >= b.count) return 0;
+    const uint32_t len = b.len ? b.len[s] : b.uniform_len;
+    return seg_blocks(len, STREAM ? b.pos_state[s] : 0u);
+}
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) {
+        const uint64_t add = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    total = sh[kScanThreads - 1];
+    const uint64_t incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(kScanThreads) void k_scan_local(KBatch b, uint64_t *bstart, uint64_t *wg_sums) {
+    __shared__ uint64_t sh[kScanThreads];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t v[kScanItems], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = nblocks_of<STREAM>(b, base + k);
+        sum += v[k];
+    }
+    uint64_t total;
+    uint64_t run = block_exclusive_scan(sum, sh, total);
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        if (base + k < b.count) bstart[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 0) wg_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_sums(uint64_t *wg_sums, uint64_t nwg, uint64_t *bstart,
+                                                            uint64_t count, uint64_t *total_out) {
+    __shared__ uint64_t sh[kScanThreads];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nwg; base += kScanThreads) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nwg ? wg_sums[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(v, sh, tot);
+        if (i < nwg) wg_sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        bstart[count] = carry;
+        *total_out = carry;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_add(uint64_t *bstart, const uint64_t *wg_sums, uint64_t count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) bstart[i] += wg_sums[i / kScanTile];
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(kScanThreads) void k_tile_map(KBatch b, const uint64_t *bstart, uint64_t *tile_first,
+                                                           uint64_t nchunks) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0) tile_first[nchunks] = b.count ? b.count - 1 : 0;
+    if (s >= b.count) return;
+    const uint64_t nb = nblocks_of<STREAM>(b, s);
+    if (!nb) return;
+    const uint64_t first = bstart[s], last = first + nb - 1;
+    for (uint64_t t = (first + 63) >> 6; (t << 6) <= last; t++) tile_first[t] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Key expansion on the device (one lane per key; base/rijndael.c:712-799).
+
+__global__ __launch_bounds__(256) void k_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs,
+                                                     uint32_t count, const uint8_t *sbox_g, DevKey *out) {
+    __shared__ uint8_t sbox[256];
+    sbox[threadIdx.x] = sbox_g[threadIdx.x];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint8_t *key = keys + (uint64_t)i * keylen;
+    const int nk = (int)keylen / 4, nr = nk + 6;
+    uint32_t w[60];
+    for (int k = 0; k < nk; k++)
+        w[k] = ((uint32_t)key[4 * k] << 24) | ((uint32_t)key[4 * k + 1] << 16) | ((uint32_t)key[4 * k + 2] << 8) |
+               key[4 * k + 3];
+    auto sub = [&](uint32_t t) {
+        return ((uint32_t)sbox[t >> 24] << 24) | ((uint32_t)sbox[(t >> 16) & 0xff] << 16) |
+               ((uint32_t)sbox[(t >> 8) & 0xff] << 8) | sbox[t & 0xff];
+    };
+    uint32_t rcon = 1;
+    for (int k = nk; k < 4 * (nr + 1); k++) {
+        uint32_t t = w[k - 1];
+        if (k % nk == 0) {
+            t = sub((t << 8) | (t >> 24)) ^ (rcon << 24);
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0)) & 0xff;
+        } else if (nk > 6 && k % nk == 4) {
+            t = sub(t);
+        }
+        w[k] = w[k - nk] ^ t;
+    }
+    DevKey *d = out + i;
+    for (int k = 0; k < 60; k++) d->rk[k] = k < 4 * (nr + 1) ? __builtin_bswap32(w[k]) : 0u;
+    d->nrounds = (uint32_t)nr;
+    d->keylen = keylen;
+    d->reserved[0] = d->reserved[1] = 0;
+    for (int k = 0; k < 16; k++) d->iv[k] = ivs ? ivs[16 * (uint64_t)i + k] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic payload: counter-based splitmix64 (same definition as oracle/aes_oracle.c).
+
+__device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t i) {
+    uint64_t z = i + seed * 0xD1B54A32D192ED03ULL;
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t off) {
+    const uint64_t w0 = off >> 3, w1 = (off + nbytes + 7) >> 3;
+    const bool aligned = (((uintptr_t)dst - off) & 7) == 0;
+    for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w1;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = synth_word(seed, w);
+        const uint64_t lo = w << 3;
+        if (aligned && lo >= off && lo + 8 <= off + nbytes) {
+            *reinterpret_cast<uint64_t *>(dst + (lo - off)) = v;
+        } else {
+            for (int k = 0; k < 8; k++) {
+                const uint64_t a = lo + k;
+                if (a >= off && a < off + nbytes) dst[a - off] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (runtime -> template dispatch)
+
+template <int NR>
+static hipError_t enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+#define FPNN_ENC(L, K, S) hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S>), dim3(grid), dim3(kThreads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false);
+    }
+#undef FPNN_ENC
+    return hipGetLastError();
+}
+
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                                 hipStream_t st) {
+    switch (nrounds) {
+        case 10: return enc_nr<10>(b, layout, km, stream, grid, st);
+        case 12: return enc_nr<12>(b, layout, km, stream, grid, st);
+        case 14: return enc_nr<14>(b, layout, km, stream, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int NR, bool INPLACE>
+static hipError_t dec_nr_ip(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+#define FPNN_DEC(L, K, S) \
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE>), dim3(grid), dim3(kThreads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, false);
+    }
+#undef FPNN_DEC
+    return hipGetLastError();
+}
+
+template <int NR>
+static hipError_t dec_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, bool inplace, int grid,
+                         hipStream_t st) {
+    return inplace ? dec_nr_ip<NR, true>(b, layout, km, stream, grid, st)
+                   : dec_nr_ip<NR, false>(b, layout, km, stream, grid, st);
+}
+
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, bool inplace,
+                                 int grid, hipStream_t st) {
+    switch (nrounds) {
+        case 10: return dec_nr<10>(b, layout, km, stream, inplace, grid, st);
+        case 12: return dec_nr<12>(b, layout, km, stream, inplace, grid, st);
+        case 14: return dec_nr<14>(b, layout, km, stream, inplace, grid, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+static int grid_for(uint64_t items, int threads, int cap) {
+    uint64_t g = (items + threads - 1) / threads;
+    if (g < 1) g = 1;
+    return (int)(g > (uint64_t)cap ? cap : g);
+}
+
+hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
+                                hipStream_t st) {
+    const int grid = grid_for(nchunks, 256, 4096);
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream)
+            hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, true>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
+        else
+            hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, false>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
+    } else {
+        if (stream)
+            hipLaunchKernelGGL((k_boundary_save<LAYOUT_GENERAL, true>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
+        else
+            hipLaunchKernelGGL((k_boundary_save<LAYOUT_GENERAL, false>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,
+                                 hipStream_t st) {
+    const uint64_t nwg = (b.count + kScanTile - 1) / kScanTile;
+    if (nwg) {
+        if (stream)
+            hipLaunchKernelGGL((k_scan_local<true>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
+        else
+            hipLaunchKernelGGL((k_scan_local<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
+    }
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, st, wg_sums, nwg, bstart, b.count, total);
+    if (b.count)
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((b.count + kScanThreads - 1) / kScanThreads)),
+                           dim3(kScanThreads), 0, st, bstart, wg_sums, b.count);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first, uint64_t nchunks,
+                           hipStream_t st) {
+    const unsigned grid = (unsigned)((b.count + kScanThreads) / kScanThreads);
+    if (stream)
+        hipLaunchKernelGGL((k_tile_map<true>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
+    else
+        hipLaunchKernelGGL((k_tile_map<false>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
+                              const uint8_t *sbox, DevKey *out, hipStream_t st) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_expand_keys, dim3((count + 255) / 256), dim3(256), 0, st, keys, keylen, ivs, count, sbox, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, int grid,
+                                 hipStream_t st) {
+    if (!nbytes) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(grid), dim3(256), 0, st, dst, nbytes, seed, byte_offset);
+    return hipGetLastError();
+}
+
+}  // namespace fpnn_aes

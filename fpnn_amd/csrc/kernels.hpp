@@ -1,0 +1,60 @@
+// kernels.hpp -- internal launch interface between the C-ABI (engine.hip) and the
+// HIP kernels (kernels.hip).  Not installed; the public boundary is include/fpnn_aes.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aes_common.hpp"
+
+namespace fpnn_aes {
+
+constexpr uint32_t F_WIRE_PREFIX = 0x1u;
+
+// Kernel-side view of one batch (passed by value as the kernel argument).
+struct KBatch {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t count;
+    uint64_t stride;
+    uint32_t uniform_len;
+    uint32_t flags;
+    const uint64_t *in_off;
+    const uint64_t *out_off;
+    const uint32_t *len;
+    const uint32_t *key_slot;
+    const DevKey *keys;
+    uint8_t *iv_state;    // stream mode: 16 B per segment (in/out)
+    uint32_t *pos_state;  // stream mode: CFB position per segment (in/out)
+    const uint32_t *t0le; // 1 KiB T0 source for the LDS image
+    // block map (decrypt)
+    uint64_t total_blocks;   // uniform layout: exact; general: copy of *total_ptr
+    uint32_t nb_uniform;     // uniform layout: blocks per segment
+    uint32_t pad0;
+    uint64_t magic;          // ceil(2^64 / nb_uniform)
+    const uint64_t *bstart;  // general: first virtual block of each segment (count + 1)
+    const uint64_t *tile_first;  // general: segment holding block 64*c (nchunks + 1)
+    const uint4 *boundary;   // in-place: Cx block preceding each 64-block chunk
+};
+
+enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1 };
+enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
+
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream,
+                                 int grid, hipStream_t st);
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream,
+                                 bool inplace, int grid, hipStream_t st);
+hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
+                                hipStream_t st);
+// General-layout block map: bstart[] and *total (device); wg_sums scratch of
+// ceil(count/1024) entries.
+hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
+                                 uint64_t *total, hipStream_t st);
+hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first,
+                           uint64_t nchunks, hipStream_t st);
+hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
+                              const uint8_t *sbox, DevKey *out, hipStream_t st);
+hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, int grid,
+                                 hipStream_t st);
+
+}  // namespace fpnn_aes

@@ -1,0 +1,245 @@
+"""Python host layer over the C-ABI (include/fpnn_aes.h).
+
+Mirrors the reference's interface for this path so the parity tests read like the
+reference's own usage:
+
+* :func:`setup_encrypt`  -- rijndael_setup_encrypt (base/rijndael.c:712-799)
+* :meth:`Engine.cfb`     -- rijndael_cfb_encrypt (base/rijndael.c:1171-1201), host bytes
+* :class:`PackageEncryptor` / :class:`StreamEncryptor` -- core/Encryptor.h:32-61
+* :meth:`Engine.package_encrypt` / ``package_decrypt`` / ``stream_encrypt`` /
+  ``stream_decrypt`` -- the batched device-resident form (the hot path).
+
+Device buffers are torch uint8 tensors on the engine's GPU; torch is used for
+memory and streams only, every payload byte is transformed by the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import torch
+
+from ._lib import (BatchDesc, FpnnAesError, Schedule, check, lib, F_WIRE_PREFIX, K_DECRYPT, K_ENCRYPT,
+                   ERR_KEYLEN, OK)
+
+
+def _buf(b: bytes):
+    return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8))
+
+
+def setup_encrypt(key: bytes) -> Schedule:
+    """rijndael_setup_encrypt: host key expansion, reference rk[] layout."""
+    ctx = Schedule()
+    rc = lib.fpnn_aes_setup_encrypt(C.byref(ctx), _buf(key), len(key))
+    if rc == ERR_KEYLEN:
+        raise FpnnAesError(rc, f"key length {len(key)} (must be 16, 24 or 32)")
+    check(rc, "setup_encrypt")
+    return ctx
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib.fpnn_aes_device_count(C.byref(n))
+    return n.value if rc == OK else 0
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("device array expected (torch tensor on a HIP device)")
+    if not t.is_contiguous():
+        raise ValueError("contiguous tensor expected")
+    return C.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """One GPU + one HIP stream (default: torch's current stream on that device)."""
+
+    def __init__(self, device: int = 0, stream: Optional[torch.cuda.Stream] = None):
+        self.device = device
+        if stream is None:
+            stream = torch.cuda.current_stream(device)
+        self.torch_stream = stream
+        h = C.c_void_p()
+        check(lib.fpnn_aes_engine_create(device, C.c_void_p(stream.cuda_stream), C.byref(h)), "engine_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.fpnn_aes_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(lib.fpnn_aes_engine_sync(self._h), "sync")
+
+    def reserve(self, max_segments: int, max_blocks: int):
+        check(lib.fpnn_aes_engine_reserve(self._h, max_segments, max_blocks), "reserve")
+
+    # -- timing -----------------------------------------------------------------------
+    def set_timing(self, enable: bool):
+        check(lib.fpnn_aes_engine_set_timing(self._h, int(enable)), "set_timing")
+
+    def kernel_stats(self, which: int):
+        n = C.c_uint64()
+        ms = C.c_double()
+        check(lib.fpnn_aes_engine_kernel_stats(self._h, which, C.byref(n), C.byref(ms)), "kernel_stats")
+        return n.value, ms.value
+
+    def reset_stats(self):
+        check(lib.fpnn_aes_engine_reset_stats(self._h), "reset_stats")
+
+    # -- synthetic data ------------------------------------------------------------------
+    def fill_synthetic(self, dst: torch.Tensor, seed: int, byte_offset: int = 0, nbytes: Optional[int] = None):
+        n = dst.numel() * dst.element_size() if nbytes is None else nbytes
+        check(lib.fpnn_aes_fill_synthetic(self._h, _ptr(dst), n, seed, byte_offset), "fill_synthetic")
+
+    # -- single host call (drop-in for rijndael_cfb_encrypt) ------------------------------
+    def cfb(self, ctx: Schedule, encrypt: bool, data: bytes, ivec: bytes, num: int = 0):
+        iv = (C.c_uint8 * 16)(*ivec)
+        n = C.c_size_t(num)
+        out = C.create_string_buffer(max(1, len(data)))
+        check(lib.fpnn_aes_cfb_host(self._h, C.byref(ctx), int(encrypt), C.c_char_p(data), out, len(data), iv,
+                                    C.byref(n)), "cfb_host")
+        return out.raw[: len(data)], bytes(iv), n.value
+
+    # -- batches ----------------------------------------------------------------------------
+    def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,
+              key_slot=None, flags=0) -> BatchDesc:
+        d = BatchDesc()
+        d.in_ = _ptr(inp).value if inp is not None else None
+        d.out = _ptr(out).value if out is not None else None
+        d.count = count
+        d.uniform_len = uniform_len
+        d.stride = stride
+        for name, t, dt in (("in_off", in_off, torch.int64), ("out_off", out_off, torch.int64),
+                            ("len", lens, torch.int32), ("key_slot", key_slot, torch.int32)):
+            if t is not None:
+                if t.dtype not in (dt, torch.uint64 if dt == torch.int64 else torch.uint32):
+                    raise TypeError(f"{name}: dtype {t.dtype}, expected {dt}")
+                if t.numel() < count:
+                    raise ValueError(f"{name}: {t.numel()} entries for {count} segments")
+                setattr(d, name, _ptr(t).value)
+        d.keys = keys.handle.value
+        d.flags = flags
+        return d
+
+    def package_encrypt(self, inp, out, count, keys: "KeySet", wire_prefix: bool = False, **kw):
+        d = self._desc(inp, out, count, keys, flags=F_WIRE_PREFIX if wire_prefix else 0, **kw)
+        check(lib.fpnn_aes_package_encrypt(self._h, C.byref(d)), "package_encrypt")
+
+    def package_decrypt(self, inp, out, count, keys: "KeySet", **kw):
+        d = self._desc(inp, out, count, keys, **kw)
+        check(lib.fpnn_aes_package_decrypt(self._h, C.byref(d)), "package_decrypt")
+
+    def stream_encrypt(self, inp, out, count, keys: "KeySet", iv_state: torch.Tensor, pos_state: torch.Tensor, **kw):
+        d = self._desc(inp, out, count, keys, **kw)
+        check(lib.fpnn_aes_stream_encrypt(self._h, C.byref(d), _ptr(iv_state), _ptr(pos_state)), "stream_encrypt")
+
+    def stream_decrypt(self, inp, out, count, keys: "KeySet", iv_state: torch.Tensor, pos_state: torch.Tensor, **kw):
+        d = self._desc(inp, out, count, keys, **kw)
+        check(lib.fpnn_aes_stream_decrypt(self._h, C.byref(d), _ptr(iv_state), _ptr(pos_state)), "stream_decrypt")
+
+
+class KeySet:
+    """Per-connection (key, IV) table on the device, expanded by the GPU."""
+
+    def __init__(self, engine: Engine, keys, keylen: int, ivs=None):
+        h = C.c_void_p()
+        if isinstance(keys, (bytes, bytearray)):
+            count = len(keys) // keylen
+            kb = bytes(keys)
+            ib = bytes(ivs) if ivs is not None else None
+            rc = lib.fpnn_aes_keyset_create(engine.handle, count, keylen, C.c_char_p(kb),
+                                            C.c_char_p(ib) if ib is not None else None, 1, C.byref(h))
+        else:  # device tensors
+            count = keys.numel() // keylen
+            rc = lib.fpnn_aes_keyset_create(engine.handle, count, keylen, _ptr(keys),
+                                            _ptr(ivs) if ivs is not None else None, 0, C.byref(h))
+        check(rc, "keyset_create")
+        self._h = h
+        self.count = count
+        self.keylen = keylen
+        self.engine = engine
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def nrounds(self) -> int:
+        return lib.fpnn_aes_keyset_nrounds(self._h)
+
+    def schedule(self, slot: int) -> Schedule:
+        s = Schedule()
+        check(lib.fpnn_aes_keyset_get_schedule(self._h, slot, C.byref(s)), "keyset_get_schedule")
+        return s
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.fpnn_aes_keyset_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# -- Encryptor surface (core/Encryptor.h:11-61) -------------------------------------------------
+
+class Encryptor:
+    def __init__(self, engine: Engine, key: bytes, iv: bytes):
+        self._engine = engine
+        self._key = bytes(key)
+        self._iv = bytes(iv[:16])
+        self._ctx = setup_encrypt(self._key)
+
+
+class PackageEncryptor(Encryptor):
+    """core/Encryptor.cpp:10-51: each call is a fresh chain from the connection IV."""
+
+    def decrypt(self, src: bytes) -> bytes:
+        return self._engine.cfb(self._ctx, False, src, self._iv, 0)[0]
+
+    def encrypt(self, src: bytes) -> bytes:
+        return self._engine.cfb(self._ctx, True, src, self._iv, 0)[0]
+
+    def encrypt_frame(self, src: bytes) -> bytes:
+        """encrypt(std::string*): htole32(len) || ciphertext."""
+        return len(src).to_bytes(4, "little") + (self.encrypt(src) if src else b"")
+
+
+class StreamEncryptor(Encryptor):
+    """core/Encryptor.cpp:53-70: (iv, pos) carried across calls."""
+
+    def __init__(self, engine: Engine, key: bytes, iv: bytes):
+        super().__init__(engine, key, iv)
+        self._pos = 0
+
+    def _run(self, enc: bool, src: bytes) -> bytes:
+        if not src:
+            return b""
+        out, self._iv, self._pos = self._engine.cfb(self._ctx, enc, src, self._iv, self._pos)
+        return out
+
+    def decrypt(self, src: bytes) -> bytes:
+        return self._run(False, src)
+
+    def encrypt(self, src: bytes) -> bytes:
+        return self._run(True, src)
+
+    @property
+    def state(self):
+        return self._iv, self._pos

@@ -1,0 +1,93 @@
+/*
+ * Encryptor.h -- source-compatible replacement for the reference's core/Encryptor.h
+ * (core/Encryptor.h:11-61).  Same namespace, class names, constructors, protected
+ * members and virtual methods, so EncryptedPackageReceiver / EncryptedStreamReceiver
+ * (which embed these by value, core/Receiver.h:104,145) and SendBuffer (which owns
+ * one through new/delete, core/IOBuffer.cpp:262-266) compile unchanged against it.
+ *
+ * Every call runs the CFB cipher on the MI355X through the C-ABI in fpnn_aes.h
+ * (per calling thread: one engine, one HIP stream, pinned staging).  Results are
+ * byte-identical to the reference's.  A GPU failure throws fpnn::EncryptorError;
+ * there is no CPU fallback.
+ *
+ * For throughput, frames should be submitted in batches (fpnn_aes_package_* /
+ * fpnn_aes_stream_* in fpnn_aes.h): one GPU round trip per 1 KiB frame costs more
+ * than the frame's CPU cipher time (hard part 6).
+ */
+#ifndef FPNN_AMD_ENCRYPTOR_H
+#define FPNN_AMD_ENCRYPTOR_H
+
+#include <stdint.h>
+#include <string.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "rijndael.h"
+
+namespace fpnn {
+
+class EncryptorError : public std::runtime_error {
+public:
+    explicit EncryptorError(const std::string &what) : std::runtime_error(what) {}
+};
+
+class Encryptor {
+protected:
+    uint8_t _iv[16];
+    uint8_t _key[32];
+    size_t _keyLen;
+
+public:
+    Encryptor(uint8_t *key, size_t key_len, uint8_t *iv) {
+        memcpy(_key, key, key_len);
+        memcpy(_iv, iv, 16);
+        _keyLen = key_len;
+    }
+    virtual ~Encryptor() {}
+
+    virtual void decrypt(uint8_t *dest, uint8_t *src, int len) = 0;
+    virtual void encrypt(uint8_t *dest, uint8_t *src, int len) = 0;
+    virtual void encrypt(std::string *buffer) = 0;
+};
+
+/* One fresh CFB chain per call from the connection IV (core/Encryptor.cpp:10-51). */
+class PackageEncryptor : public Encryptor {
+    rijndael_context _ctx;  // expanded once; the reference re-expands per call (same result)
+
+public:
+    PackageEncryptor(uint8_t *key, size_t key_len, uint8_t *iv) : Encryptor(key, key_len, iv) {
+        rijndael_setup_encrypt(&_ctx, (const uint8_t *)_key, key_len);
+    }
+    virtual ~PackageEncryptor() {}
+
+    virtual void decrypt(uint8_t *dest, uint8_t *src, int len);
+    virtual void encrypt(uint8_t *dest, uint8_t *src, int len);
+    /* buffer := htole32(len) || CFB(buffer) */
+    virtual void encrypt(std::string *buffer);
+};
+
+/* One CFB chain per connection direction, state (_iv, _pos) carried across calls
+ * (core/Encryptor.cpp:53-70). */
+class StreamEncryptor : public Encryptor {
+    rijndael_context _ctx;
+    size_t _pos;
+
+public:
+    StreamEncryptor(uint8_t *key, size_t key_len, uint8_t *iv) : Encryptor(key, key_len, iv), _pos(0) {
+        rijndael_setup_encrypt(&_ctx, (const uint8_t *)_key, key_len);
+    }
+    virtual ~StreamEncryptor() {}
+
+    virtual void decrypt(uint8_t *dest, uint8_t *src, int len);
+    virtual void encrypt(uint8_t *dest, uint8_t *src, int len);
+    virtual void encrypt(std::string *buffer);
+
+    /* state export/import (the only stream-mode state) */
+    const uint8_t *iv() const { return _iv; }
+    size_t pos() const { return _pos; }
+};
+
+}  // namespace fpnn
+
+#endif

@@ -1,0 +1,165 @@
+/*
+ * fpnn_aes.h -- C-ABI of the MI355X AES-CFB packet-encryption path.
+ *
+ * Replaces, for batches of independent packets/streams, the CPU path
+ *   core/Encryptor.cpp:10-70  (PackageEncryptor / StreamEncryptor)
+ *     -> base/rijndael.c:1171-1201 (rijndael_cfb_encrypt)
+ *        -> base/rijndael.c:852-959 (rijndael_encrypt)
+ * of the reference (highras/fpnn v1.3.1).  Plain pointers and sizes only;
+ * no exceptions and no C++/torch types cross this boundary.  Every call
+ * returns an int status (the reference functions are void; see
+ * FPNN_AES_ERR_* below for what is now reported instead of being undefined).
+ *
+ * Device pointers ("dev") are HIP device addresses on the engine's GPU; host
+ * pointers ("host") are ordinary process memory.  All device work is queued on
+ * the engine's HIP stream; calls return after queuing unless they say otherwise.
+ * Results are bit-identical to the reference for every key length (16/24/32),
+ * payload length (including 0 and non-multiples of 16) and CFB position.
+ */
+#ifndef FPNN_AES_H
+#define FPNN_AES_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------- */
+#define FPNN_AES_OK            0
+#define FPNN_AES_ERR_KEYLEN   -1  /* key length not 16/24/32 (reference: setup returns false
+                                     and the cipher then runs with nrounds = 0, rijndael.c:797) */
+#define FPNN_AES_ERR_ARG      -2  /* NULL pointer, bad descriptor, mixed key lengths */
+#define FPNN_AES_ERR_RANGE    -3  /* batch too large (more than 2^32-1 16-byte blocks or packets) */
+#define FPNN_AES_ERR_HIP      -4  /* HIP runtime error (message: fpnn_aes_last_error) */
+#define FPNN_AES_ERR_NODEV    -5  /* no usable gfx950 device / kernels not loadable */
+
+const char *fpnn_aes_strerror(int status);
+/* Thread-local text of the last HIP error seen by this thread (or ""). */
+const char *fpnn_aes_last_error(void);
+
+/* ---- key schedule ------------------------------------------------------------ */
+/* Layout identical to rijndael_context (base/rijndael.h:13-16). */
+typedef struct {
+    int nrounds;
+    uint32_t rk[60];
+} fpnn_aes_schedule;
+
+/* Host key expansion.  Mirrors rijndael_setup_encrypt (base/rijndael.c:712-799):
+ * same big-endian rk[] words, same nrounds; returns FPNN_AES_OK or
+ * FPNN_AES_ERR_KEYLEN (and sets nrounds = 0, like the reference). */
+int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen);
+
+/* ---- engine: one GPU, one HIP stream ---------------------------------------- */
+typedef struct fpnn_aes_engine fpnn_aes_engine;
+#define FPNN_AES_OWN_STREAM ((void *)(intptr_t)-1)
+
+int fpnn_aes_device_count(int *count);
+/* hip_stream: the hipStream_t to queue on (e.g. torch's current stream); NULL is
+ * the device's null stream, as everywhere in HIP; FPNN_AES_OWN_STREAM creates a
+ * private non-blocking stream owned by the engine.  The engine is not thread-safe; use one
+ * engine per submitting thread (the reference's per-connection token discipline,
+ * core/IOBuffer.h:49-62, makes each Encryptor single-threaded in the same way). */
+int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out);
+int fpnn_aes_engine_destroy(fpnn_aes_engine *e);
+int fpnn_aes_engine_sync(fpnn_aes_engine *e);
+void *fpnn_aes_engine_stream(fpnn_aes_engine *e);
+/* Pre-size scratch for batches of up to max_segments packets/streams and
+ * max_blocks total 16-byte blocks, so later calls never allocate (graph-safe). */
+int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t max_blocks);
+
+/* ---- key sets: the per-connection (key, IV) table on the device -------------- */
+/* A key set holds `count` expanded keys of ONE key length plus one 16-byte IV each
+ * (the connection IV of package mode, core/Encryptor.h:14).  keys: count*keylen
+ * bytes, ivs: count*16 bytes (NULL => zero IVs).  keys_on_host != 0 means keys/ivs
+ * are host pointers (copied), otherwise device pointers.  Expansion runs on the GPU. */
+typedef struct fpnn_aes_keyset fpnn_aes_keyset;
+
+int fpnn_aes_keyset_create(fpnn_aes_engine *e, uint32_t count, size_t keylen, const uint8_t *keys,
+                           const uint8_t *ivs, int keys_on_host, fpnn_aes_keyset **out);
+/* Same, from host schedules already expanded by fpnn_aes_setup_encrypt /
+ * rijndael_setup_encrypt (all with the same nrounds). */
+int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpnn_aes_schedule *ctx,
+                                   const uint8_t *ivs, fpnn_aes_keyset **out);
+int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks);
+int fpnn_aes_keyset_nrounds(const fpnn_aes_keyset *ks);
+/* Copy the expanded schedule of slot i back to the host (rijndael_context layout). */
+int fpnn_aes_keyset_get_schedule(fpnn_aes_keyset *ks, uint32_t slot, fpnn_aes_schedule *out);
+
+/* ---- batch descriptor ---------------------------------------------------------- */
+/* A batch is `count` independent segments.  Segment i reads len_i bytes at
+ * in + in_off[i] and writes len_i bytes at out + out_off[i]:
+ *   in_off  == NULL -> in_off[i]  = i * stride
+ *   out_off == NULL -> out_off[i] = in_off[i]
+ *   len     == NULL -> len_i      = uniform_len
+ *   key_slot== NULL -> slot_i     = 0            (index into the key set)
+ * Offsets/lengths/slots are device arrays.  `in` and `out` may be the same
+ * buffer with identical offsets (in-place); any other overlap is undefined. */
+typedef struct {
+    const uint8_t *in;          /* dev */
+    uint8_t *out;               /* dev */
+    uint32_t count;
+    uint32_t uniform_len;
+    uint64_t stride;
+    const uint64_t *in_off;     /* dev, optional */
+    const uint64_t *out_off;    /* dev, optional */
+    const uint32_t *len;        /* dev, optional */
+    const uint32_t *key_slot;   /* dev, optional */
+    const fpnn_aes_keyset *keys;
+    uint32_t flags;             /* FPNN_AES_F_* */
+    uint32_t reserved;
+} fpnn_aes_batch;
+
+/* Package encrypt only: write the wire frame of PackageEncryptor::encrypt(std::string*)
+ * (core/Encryptor.cpp:34-51): htole32(len) at out + out_off[i], ciphertext at +4. */
+#define FPNN_AES_F_WIRE_PREFIX 0x1u
+
+/* ---- package mode (core/Encryptor.cpp:10-51) ------------------------------------- */
+/* Every segment starts a fresh CFB chain from its key slot's IV at position 0,
+ * exactly as PackageEncryptor re-copies _iv and re-expands the key per call.
+ * Decrypt runs one GPU lane per 16-byte block; encrypt one lane per packet chain. */
+int fpnn_aes_package_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b);
+int fpnn_aes_package_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b);
+
+/* ---- stream mode (core/Encryptor.cpp:53-70) ---------------------------------------- */
+/* Segment i continues the CFB stream whose state is (iv_state[16*i .. +16],
+ * pos_state[i]) -- StreamEncryptor::_iv and ::_pos -- with key slot slot_i; the
+ * state is updated in place (dev arrays).  A given stream must appear at most once
+ * per call; successive frames of a stream go in successive calls. */
+int fpnn_aes_stream_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state,
+                            uint32_t *pos_state);
+int fpnn_aes_stream_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state,
+                            uint32_t *pos_state);
+
+/* ---- single call from host memory (the per-frame drop-in) --------------------------- */
+/* Exactly rijndael_cfb_encrypt(ctx, encrypt, in, out, len, ivec, p_num)
+ * (base/rijndael.c:1171-1201) with host buffers: stages through pinned memory,
+ * runs the GPU kernels, copies back and updates ivec/p_num.  Synchronous. */
+int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt,
+                      const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num);
+
+/* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
+/* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */
+int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed,
+                            uint64_t byte_offset);
+
+/* ---- instrumentation ---------------------------------------------------------------- */
+/* When enabled, every batch call records HIP events around its main kernel on the
+ * engine stream; fpnn_aes_engine_kernel_stats returns the count and summed milliseconds
+ * of the main-kernel launches since the last reset (synchronizes the stream). */
+int fpnn_aes_engine_set_timing(fpnn_aes_engine *e, int enable);
+int fpnn_aes_engine_kernel_stats(fpnn_aes_engine *e, int which /* FPNN_AES_K_* */, uint64_t *launches,
+                                 double *total_ms);
+int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e);
+#define FPNN_AES_K_DECRYPT 0
+#define FPNN_AES_K_ENCRYPT 1
+
+/* Version string of the built library (kernel variant + build flags). */
+const char *fpnn_aes_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FPNN_AES_H */

@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ fixtures from the REFERENCE itself -- test infrastructure.
+
+Runs oracle/_ref/libfpnn_ref.so, i.e. the reference's own base/rijndael.c and
+core/Encryptor.cpp compiled by `make -C oracle ref` from /root/reference (this
+container only).  Writes data only -- inputs and the reference's outputs:
+
+  kat.json          FIPS-197 C.1/C.3, SP 800-38A F.3.13/F.3.17 (inputs + reference outputs)
+  cfb_cases.json    random rijndael_cfb_encrypt calls (16/24/32-byte keys, pos carry)
+  package_cases.json PackageEncryptor encrypt / decrypt / encrypt(std::string*) frames
+  stream_cases.json StreamEncryptor call sequences (state carried across frames)
+  digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5)
+
+Usage: python oracle/gen_golden.py [--skip-large]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from pyoracle import Oracle, StreamOracle, synth_bytes  # noqa: E402
+sys.path.insert(0, os.path.dirname(HERE))
+import workloads as configs  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+
+def hx(b: bytes) -> str:
+    return b.hex()
+
+
+def gen_kat(ref: Oracle):
+    k128 = bytes(range(16))
+    k256 = bytes(range(32))
+    pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    sp_pt = bytes.fromhex("6bc1bee22e409f96e93d7e117393172aae2d8a571e03ac9c9eb76fac45af8e51"
+                          "30c81c46a35ce411e5fbc1191a0a52eff69f2445df4f9b17ad2b417be66c3710")
+    k_sp128 = bytes.fromhex("2b7e151628aed2a6abf7158809cf4f3c")
+    k_sp256 = bytes.fromhex("603deb1015ca71be2b73aef0857d77811f352c073b6108d72d9810a30914dff4")
+    iv = bytes(range(16))
+    out = {
+        "ecb": [
+            {"name": "FIPS-197 C.1 AES-128", "key": hx(k128), "in": hx(pt), "out": hx(ref.encrypt_block(k128, pt))},
+            {"name": "FIPS-197 C.3 AES-256", "key": hx(k256), "in": hx(pt), "out": hx(ref.encrypt_block(k256, pt))},
+        ],
+        "cfb": [
+            {"name": "SP800-38A F.3.13 CFB128-AES128", "key": hx(k_sp128), "iv": hx(iv), "in": hx(sp_pt),
+             "out": hx(ref.cfb(k_sp128, True, sp_pt, iv)[0])},
+            {"name": "SP800-38A F.3.17 CFB128-AES256", "key": hx(k_sp256), "iv": hx(iv), "in": hx(sp_pt),
+             "out": hx(ref.cfb(k_sp256, True, sp_pt, iv)[0])},
+        ],
+        "source": "outputs produced by oracle/_ref (reference base/rijndael.c)",
+    }
+    return out
+
+
+def gen_cfb_cases(ref: Oracle, n=240):
+    rng = np.random.default_rng(20261015)
+    cases = []
+    for i in range(n):
+        kl = (16, 24, 32)[i % 3]
+        key = rng.bytes(kl)
+        iv = rng.bytes(16)
+        pos = int(rng.integers(0, 16)) if i % 4 else 0
+        length = int(rng.choice([0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 63, 64, 65, 100, 255, 256, 257, 1000]))
+        data = rng.bytes(length)
+        enc = bool(i & 1)
+        out, iv2, pos2 = ref.cfb(key, enc, data, iv, pos)
+        cases.append({"key": hx(key), "iv": hx(iv), "pos": pos, "encrypt": enc, "in": hx(data), "out": hx(out),
+                      "iv_out": hx(iv2), "pos_out": pos2})
+    return cases
+
+
+def gen_package_cases(ref: Oracle):
+    rng = np.random.default_rng(7)
+    cases = []
+    lens = [0, 1, 3, 15, 16, 17, 31, 32, 33, 64, 100, 145, 1023, 1024, 1025, 1500, 4096]
+    for kl in (16, 32):
+        key = rng.bytes(kl)
+        iv = rng.bytes(16)
+        for L in lens:
+            data = rng.bytes(L)
+            cases.append({"key": hx(key), "iv": hx(iv), "in": hx(data),
+                          "encrypt": hx(ref.package(key, iv, True, data)),
+                          "decrypt": hx(ref.package(key, iv, False, data)),
+                          "frame": hx(ref.package_frame(key, iv, data))})
+    # the reference's own demo inputs (base/test/rijndaelDemo.cpp:13-31, round trip only there)
+    key = b"aaaaaaaaaaaaaaaa"
+    data = b"dasdsa as dsadasd sadsad eesewfsfsf sdfdssfsdfsdf wrwerfw fea fsfdfdsf ewrsfds"
+    cases.append({"key": hx(key), "iv": hx(key), "in": hx(data), "encrypt": hx(ref.package(key, key, True, data)),
+                  "decrypt": hx(ref.package(key, key, False, data)), "frame": hx(ref.package_frame(key, key, data))})
+    return cases
+
+
+def gen_stream_cases(ref: Oracle):
+    rng = np.random.default_rng(11)
+    cases = []
+    for kl in (16, 32):
+        for enc in (True, False):
+            key = rng.bytes(kl)
+            iv = rng.bytes(16)
+            h = ref._snew(ref_buf(key), kl, ref_buf(iv))
+            frames = []
+            for _ in range(12):
+                L = int(rng.choice([0, 1, 5, 11, 12, 16, 29, 64, 100, 333]))
+                data = rng.bytes(L)
+                outb = (np.zeros(max(1, L), dtype=np.uint8))
+                ref._scrypt(h, int(enc), ref_buf(data), outb.ctypes.data_as(ref_u8p()), L)
+                frames.append({"in": hx(data), "out": hx(outb.tobytes()[:L])})
+            ref._sfree(h)
+            cases.append({"key": hx(key), "iv": hx(iv), "encrypt": enc, "frames": frames})
+    return cases
+
+
+def ref_buf(b):
+    import ctypes as C
+    return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8))
+
+
+def ref_u8p():
+    import ctypes as C
+    return C.POINTER(C.c_uint8)
+
+
+def digest_c2(ref: Oracle, threads: int):
+    c = configs.C2
+    key, iv = configs.single_key(c)
+    P, L = c["packets"], c["length"]
+    inp = synth_bytes(P * L, c["payload_seed"], threads=threads)
+    out = np.empty_like(inp)
+    ref.package_batch(True, inp, out, P, stride=L, uniform_len=L, keys=np.frombuffer(key, np.uint8).copy(),
+                      keylen=len(key), ivs=np.frombuffer(iv, np.uint8).copy(), threads=threads)
+    return {"config": "C2", "plain_sha256": hashlib.sha256(inp).hexdigest(),
+            "cipher_sha256": hashlib.sha256(out).hexdigest(),
+            "cipher_head_hex": out[:64].tobytes().hex()}
+
+
+def digest_c5(ref: Oracle, threads: int):
+    c = configs.C5
+    keys, ivs = configs.many_keys(c)
+    P, L = c["packets"], c["length"]
+    inp = synth_bytes(P * L, c["payload_seed"], threads=threads)
+    out = np.empty_like(inp)
+    slots = np.arange(P, dtype=np.uint32)
+    ref.package_batch(True, inp, out, P, stride=L, uniform_len=L, key_slot=slots, keys=keys, keylen=c["keylen"],
+                      ivs=ivs, threads=threads)
+    return {"config": "C5", "plain_sha256": hashlib.sha256(inp).hexdigest(),
+            "cipher_sha256": hashlib.sha256(out).hexdigest()}
+
+
+def digest_c3(ref: Oracle, threads: int):
+    """Whole-stream ciphertext of every stream; digest = sha256(concat(sha256(stream_i)))."""
+    c = configs.C3
+    keys, ivs = configs.many_keys(c)
+    S, L = c["streams"], c["length"]
+    per = []
+    group = 64
+    for g0 in range(0, S, group):
+        n = min(group, S - g0)
+        inp = synth_bytes(n * L, c["payload_seed"], offset=g0 * L, threads=threads)
+        out = np.empty_like(inp)
+        in_off = (np.arange(n, dtype=np.uint64) * L)
+        lens = np.full(n, L, dtype=np.uint32)
+        slots = np.arange(g0, g0 + n, dtype=np.uint32)
+        iv_state = ivs[16 * g0: 16 * (g0 + n)].copy()
+        pos_state = np.zeros(n, dtype=np.uint32)
+        ref.stream_batch(True, inp, out, n, in_off=in_off, out_off=in_off, lens=lens, key_slot=slots, keys=keys,
+                         keylen=c["keylen"], iv_state=iv_state, pos_state=pos_state, threads=threads)
+        for i in range(n):
+            per.append(hashlib.sha256(out[i * L:(i + 1) * L]).digest())
+    return {"config": "C3", "stream_digests_sha256": hashlib.sha256(b"".join(per)).hexdigest(),
+            "first_stream_sha256": per[0].hex()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-large", action="store_true")
+    ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
+    args = ap.parse_args()
+    ref = Oracle("reference")
+    os.makedirs(GOLDEN, exist_ok=True)
+
+    def dump(name, obj):
+        with open(os.path.join(GOLDEN, name), "w") as f:
+            json.dump(obj, f, indent=1)
+        print("wrote", name)
+
+    dump("kat.json", gen_kat(ref))
+    dump("cfb_cases.json", gen_cfb_cases(ref))
+    dump("package_cases.json", gen_package_cases(ref))
+    dump("stream_cases.json", gen_stream_cases(ref))
+    if not args.skip_large:
+        d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
+             "configs": configs.describe()}
+        d["C2"] = digest_c2(ref, args.threads)
+        print("C2", d["C2"])
+        d["C5"] = digest_c5(ref, args.threads)
+        print("C5", d["C5"])
+        d["C3"] = digest_c3(ref, args.threads)
+        print("C3", d["C3"])
+        dump("digests.json", d)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+// dropin.cpp -- uses the MI355X library exactly the way FPNN's own code uses the
+// reference classes (core/IOBuffer.cpp:36-45, core/EncryptedPackageReceiver.cpp:110,
+// core/EncryptedStreamReceiver.cpp:89,124, base/test/rijndaelDemo.cpp), compiled
+// against include/Encryptor.h + include/rijndael.h and linked with libfpnn_aes.so.
+//
+// stdin, one case per line:
+//   P <key> <iv> <data>            -> "<encrypt> <decrypt> <frame>"
+//   S <E|D> <key> <iv> <f1> .. <fn> -> "<out1> .. <outn>"      (StreamEncryptor)
+//   R <key> <iv> <data>            -> "<roundtrip-memcmp> <cipher>" (rijndael.h API)
+// hex fields, "-" for an empty buffer.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "Encryptor.h"
+#include "rijndael.h"
+
+static std::vector<uint8_t> unhex(const std::string &h) {
+    std::vector<uint8_t> v;
+    if (h == "-") return v;
+    for (size_t i = 0; i + 1 < h.size(); i += 2) v.push_back((uint8_t)strtoul(h.substr(i, 2).c_str(), nullptr, 16));
+    return v;
+}
+
+static std::string hex(const uint8_t *p, size_t n) {
+    static const char *d = "0123456789abcdef";
+    std::string s;
+    for (size_t i = 0; i < n; i++) {
+        s += d[p[i] >> 4];
+        s += d[p[i] & 15];
+    }
+    return n ? s : "-";
+}
+
+int main() {
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::istringstream is(line);
+        std::string kind;
+        is >> kind;
+        if (kind == "P") {
+            std::string k, v, d;
+            is >> k >> v >> d;
+            auto key = unhex(k), iv = unhex(v), data = unhex(d);
+            fpnn::PackageEncryptor enc(key.data(), key.size(), iv.data());
+            std::vector<uint8_t> a(data.size() + 1), b(data.size() + 1);
+            enc.encrypt(a.data(), data.data(), (int)data.size());
+            enc.decrypt(b.data(), data.data(), (int)data.size());
+            std::string s((const char *)data.data(), data.size());
+            fpnn::Encryptor *base = &enc;  // SendBuffer holds an Encryptor* (core/IOBuffer.h:117)
+            base->encrypt(&s);
+            std::cout << hex(a.data(), data.size()) << " " << hex(b.data(), data.size()) << " "
+                      << hex((const uint8_t *)s.data(), s.size()) << "\n";
+        } else if (kind == "S") {
+            std::string dir, k, v, f;
+            is >> dir >> k >> v;
+            auto key = unhex(k), iv = unhex(v);
+            fpnn::StreamEncryptor enc(key.data(), key.size(), iv.data());
+            std::string sep;
+            while (is >> f) {
+                auto data = unhex(f);
+                std::vector<uint8_t> o(data.size() + 1);
+                if (dir == "E")
+                    enc.encrypt(o.data(), data.data(), (int)data.size());
+                else
+                    enc.decrypt(o.data(), data.data(), (int)data.size());
+                std::cout << sep << hex(o.data(), data.size());
+                sep = " ";
+            }
+            std::cout << "\n";
+        } else if (kind == "R") {
+            std::string k, v, d;
+            is >> k >> v >> d;
+            auto key = unhex(k), iv = unhex(v), data = unhex(d);
+            rijndael_context enCtx, deCtx;
+            rijndael_setup_encrypt(&enCtx, key.data(), key.size());
+            rijndael_setup_encrypt(&deCtx, key.data(), key.size());
+            std::vector<uint8_t> iva(iv), ivb(iv), buf(data.size() + 1), buf2(data.size() + 1);
+            size_t pos = 0;
+            rijndael_cfb_encrypt(&enCtx, true, data.data(), buf.data(), data.size(), iva.data(), &pos);
+            pos = 0;
+            rijndael_cfb_encrypt(&deCtx, false, buf.data(), buf2.data(), data.size(), ivb.data(), &pos);
+            std::cout << memcmp(data.data(), buf2.data(), data.size()) << " " << hex(buf.data(), data.size()) << "\n";
+        }
+    }
+    return 0;
+}

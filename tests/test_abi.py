@@ -1,0 +1,149 @@
+"""The C-ABI library: loads, exports every symbol include/*.h declares, host-side
+logic matches the oracle (CPU only; no compute calls that need a GPU)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = ["fpnn_aes.h", "rijndael.h"]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", src, flags=re.M):
+            name = m.group(1)
+            if name not in ("if", "while", "for", "sizeof"):
+                names.add(name)
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    import fpnn_amd
+    names = declared_functions()
+    assert "fpnn_aes_package_encrypt" in names and "rijndael_cfb_encrypt" in names
+    out = subprocess.run(["nm", "-D", "--defined-only", fpnn_amd.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = sorted(n for n in names if n not in exported)
+    assert not missing, missing
+    for n in names:  # and ctypes can bind each of them
+        getattr(fpnn_amd.lib, n)
+
+
+def test_signature_table_covers_header():
+    from fpnn_amd._lib import SIGNATURES
+    assert declared_functions() <= set(SIGNATURES)
+
+
+def test_cpp_encryptor_symbols_exported():
+    import fpnn_amd
+    out = subprocess.run(["nm", "-DC", "--defined-only", fpnn_amd.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    for sym in ("fpnn::PackageEncryptor::encrypt(unsigned char*, unsigned char*, int)",
+                "fpnn::PackageEncryptor::decrypt(unsigned char*, unsigned char*, int)",
+                "fpnn::PackageEncryptor::encrypt(std::__cxx11::basic_string",
+                "fpnn::StreamEncryptor::encrypt(unsigned char*, unsigned char*, int)",
+                "fpnn::StreamEncryptor::decrypt(unsigned char*, unsigned char*, int)"):
+        assert sym in out, sym
+
+
+def test_kernels_built_for_gfx950():
+    import fpnn_amd
+    data = open(fpnn_amd.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle id of the embedded code object
+
+
+def test_version_string():
+    import fpnn_amd
+    assert "gfx950" in fpnn_amd.version()
+
+
+@pytest.mark.parametrize("keylen", [16, 24, 32])
+def test_setup_encrypt_matches_oracle(oracle, keylen):
+    import fpnn_amd
+    rng = np.random.default_rng(keylen)
+    for _ in range(50):
+        key = rng.bytes(keylen)
+        ours = fpnn_amd.setup_encrypt(key)
+        theirs = oracle.setup_encrypt(key)
+        nw = 4 * (theirs.nrounds + 1)
+        assert ours.nrounds == theirs.nrounds
+        assert list(ours.rk[:nw]) == list(theirs.rk[:nw])
+
+
+def test_setup_encrypt_matches_reference(ref_oracle):
+    import fpnn_amd
+    rng = np.random.default_rng(5)
+    for kl in (16, 24, 32):
+        key = rng.bytes(kl)
+        a, b = fpnn_amd.setup_encrypt(key), ref_oracle.setup_encrypt(key)
+        nw = 4 * (b.nrounds + 1)
+        assert a.nrounds == b.nrounds and list(a.rk[:nw]) == list(b.rk[:nw])
+
+
+def test_rijndael_setup_encrypt_mirror():
+    import fpnn_amd
+    from fpnn_amd._lib import Schedule
+    ctx = Schedule()
+    key = bytes(range(16))
+    assert fpnn_amd.lib.rijndael_setup_encrypt(C.byref(ctx), C.cast(C.c_char_p(key), C.POINTER(C.c_uint8)), 16)
+    # FIPS-197 C.1 round-10 key 13111d7f e3944a17 f307a78b 4d2b30c5
+    assert ctx.nrounds == 10 and ctx.rk[40] == 0x13111d7f and ctx.rk[43] == 0x4d2b30c5
+    bad = Schedule()
+    assert not fpnn_amd.lib.rijndael_setup_encrypt(C.byref(bad), C.cast(C.c_char_p(key), C.POINTER(C.c_uint8)), 20)
+    assert bad.nrounds == 0
+
+
+def test_bad_key_length_reported():
+    import fpnn_amd
+    with pytest.raises(fpnn_amd.FpnnAesError) as ei:
+        fpnn_amd.setup_encrypt(b"x" * 20)
+    assert ei.value.status == fpnn_amd.ERR_KEYLEN
+
+
+def test_no_device_fails_loudly():
+    """Without a GPU the C-ABI reports NODEV (never a silent CPU path)."""
+    import torch
+    import fpnn_amd
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    rc = fpnn_amd.lib.fpnn_aes_engine_create(0, None, C.byref(h))
+    assert rc == fpnn_amd.ERR_NODEV and not h.value
+    n = C.c_int(-1)
+    fpnn_amd.lib.fpnn_aes_device_count(C.byref(n))
+    assert n.value == 0
+
+
+def test_null_arguments_rejected():
+    import fpnn_amd
+    assert fpnn_amd.lib.fpnn_aes_package_encrypt(None, None) == fpnn_amd.ERR_ARG
+    assert fpnn_amd.lib.fpnn_aes_package_decrypt(None, None) == fpnn_amd.ERR_ARG
+    assert fpnn_amd.lib.fpnn_aes_stream_encrypt(None, None, None, None) == fpnn_amd.ERR_ARG
+    assert fpnn_amd.lib.fpnn_aes_engine_create(0, None, None) == fpnn_amd.ERR_ARG
+    assert fpnn_amd.lib.fpnn_aes_keyset_create(None, 1, 16, None, None, 1, None) == fpnn_amd.ERR_ARG
+    assert fpnn_amd.lib.fpnn_aes_strerror(fpnn_amd.ERR_KEYLEN).startswith(b"key length")
+
+
+def build_dropin(outdir) -> str:
+    """Compile tests/cpp/dropin.cpp against include/Encryptor.h and link libfpnn_aes.so."""
+    import fpnn_amd
+    exe = os.path.join(str(outdir), "dropin")
+    libdir = os.path.dirname(fpnn_amd.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "dropin.cpp"), "-o", exe, "-L", libdir, "-lfpnn_aes",
+                    f"-Wl,-rpath,{libdir}"], check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_cpp_dropin_compiles_against_headers(tmp_path):
+    """include/Encryptor.h is source-compatible with the way FPNN uses core/Encryptor.h
+    (-std=c++11 -Wall -Werror, as the reference's def.mk builds it)."""
+    assert os.access(build_dropin(tmp_path), os.X_OK)

@@ -1,0 +1,435 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the oracle and the
+reference's golden fixtures.  Bit-exact everywhere (byte work, no tolerance)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def to_dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def to_host(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy()
+
+
+def dev_u8(n):
+    return torch.zeros(max(1, n), dtype=torch.uint8, device=DEV)
+
+
+def keyset(engine, keys: np.ndarray, keylen: int, ivs: np.ndarray):
+    import fpnn_amd
+    return fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+
+
+# --------------------------------------------------------------------------------------
+# data generator + key schedule
+
+
+def test_device_fill_matches_generator(engine):
+    for n, off, shift in [(1, 0, 0), (7, 3, 1), (1000, 13, 5), (65536 + 11, 8, 0), (4097, 12345, 3)]:
+        t = dev_u8(n + 8)
+        engine.fill_synthetic(t[shift:shift + n], seed=42, byte_offset=off, nbytes=n)
+        torch.cuda.synchronize()
+        assert (to_host(t)[shift:shift + n] == W.synth_bytes(n, 42, off)).all()
+
+
+@pytest.mark.parametrize("keylen", [16, 24, 32])
+def test_device_key_expansion(engine, oracle, keylen):
+    rng = np.random.default_rng(keylen + 100)
+    n = 300
+    keys = rng.integers(0, 256, n * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, to_dev(keys), keylen, to_dev(ivs))
+    assert ks.nrounds == keylen // 4 + 6
+    for i in (0, 1, 77, n - 1):
+        got = ks.schedule(i)
+        exp = oracle.setup_encrypt(keys[i * keylen:(i + 1) * keylen].tobytes())
+        nw = 4 * (exp.nrounds + 1)
+        assert got.nrounds == exp.nrounds and list(got.rk[:nw]) == list(exp.rk[:nw])
+
+
+# --------------------------------------------------------------------------------------
+# golden fixtures (produced by the compiled reference)
+
+
+def test_golden_kat(engine, golden):
+    import fpnn_amd
+    g = golden("kat.json")
+    for v in g["cfb"]:
+        key, iv, pt = (bytes.fromhex(v[k]) for k in ("key", "iv", "in"))
+        ctx = fpnn_amd.setup_encrypt(key)
+        assert engine.cfb(ctx, True, pt, iv)[0].hex() == v["out"], v["name"]
+        assert engine.cfb(ctx, False, bytes.fromhex(v["out"]), iv)[0] == pt
+        # same through the device batch API (one packet, package mode)
+        ks = fpnn_amd.KeySet(engine, key, len(key), iv)
+        src, dst = to_dev(np.frombuffer(pt, np.uint8)), dev_u8(len(pt))
+        engine.package_encrypt(src, dst, 1, ks, stride=len(pt), uniform_len=len(pt))
+        torch.cuda.synchronize()
+        assert to_host(dst).tobytes().hex() == v["out"]
+    for v in g["ecb"]:  # one CFB block from IV = plaintext block with zero data = E(block)
+        key, pt = bytes.fromhex(v["key"]), bytes.fromhex(v["in"])
+        out = engine.cfb(fpnn_amd.setup_encrypt(key), True, bytes(16), pt)[0]
+        assert out.hex() == v["out"], v["name"]
+
+
+def test_golden_cfb_cases_host_path(engine, golden):
+    """rijndael_cfb_encrypt semantics incl. (ivec, pos) carry via fpnn_aes_cfb_host."""
+    import fpnn_amd
+    for c in golden("cfb_cases.json"):
+        ctx = fpnn_amd.setup_encrypt(bytes.fromhex(c["key"]))
+        out, iv, pos = engine.cfb(ctx, c["encrypt"], bytes.fromhex(c["in"]), bytes.fromhex(c["iv"]), c["pos"])
+        assert (out.hex(), iv.hex(), pos) == (c["out"], c["iv_out"], c["pos_out"])
+
+
+def test_golden_cfb_cases_stream_batch(engine, golden):
+    """The same cases as ONE device stream batch: each case is a stream segment with its
+    own key, carried (iv, pos) in and out (fpnn_aes_stream_encrypt/decrypt)."""
+    cases = golden("cfb_cases.json")
+    for keylen in (16, 24, 32):
+        for enc in (True, False):
+            sel = [c for c in cases if len(c["key"]) == 2 * keylen and c["encrypt"] == enc]
+            n = len(sel)
+            datas = [bytes.fromhex(c["in"]) for c in sel]
+            lens = np.array([len(d) for d in datas], dtype=np.int32)
+            offs = np.concatenate([[0], np.cumsum(lens[:-1] + 5)]).astype(np.int64)  # odd gaps: unaligned segments
+            buf = np.zeros(int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+            for o, d in zip(offs, datas):
+                buf[o:o + len(d)] = np.frombuffer(d, np.uint8)
+            keys = np.concatenate([np.frombuffer(bytes.fromhex(c["key"]), np.uint8) for c in sel])
+            ivs = np.concatenate([np.frombuffer(bytes.fromhex(c["iv"]), np.uint8) for c in sel])
+            ks = keyset(engine, keys, keylen, ivs)
+            src, dst = to_dev(buf), dev_u8(len(buf))
+            iv_state = to_dev(ivs.copy())
+            pos_state = to_dev(np.array([c["pos"] for c in sel], dtype=np.int32))
+            fn = engine.stream_encrypt if enc else engine.stream_decrypt
+            fn(src, dst, n, ks, iv_state, pos_state, in_off=to_dev(offs), lens=to_dev(lens),
+               key_slot=to_dev(np.arange(n, dtype=np.int32)))
+            torch.cuda.synchronize()
+            out, ivo, poso = to_host(dst), to_host(iv_state), to_host(pos_state)
+            for i, c in enumerate(sel):
+                assert out[offs[i]:offs[i] + lens[i]].tobytes().hex() == c["out"]
+                assert ivo[16 * i:16 * i + 16].tobytes().hex() == c["iv_out"]
+                assert int(poso[i]) == c["pos_out"]
+
+
+def test_golden_package_cases(engine, golden):
+    import fpnn_amd
+    cases = golden("package_cases.json")
+    for c in cases:  # per-call drop-in surface
+        key, iv, data = (bytes.fromhex(c[k]) for k in ("key", "iv", "in"))
+        pe = fpnn_amd.PackageEncryptor(engine, key, iv)
+        assert pe.encrypt(data).hex() == c["encrypt"]
+        assert pe.decrypt(data).hex() == c["decrypt"]
+        assert pe.encrypt_frame(data).hex() == c["frame"]
+    # all cases of one key as one device batch, incl. the wire-prefix frame form
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["key"], c["iv"]), []).append(c)
+    for (k, v), cs in groups.items():
+        key, iv = bytes.fromhex(k), bytes.fromhex(v)
+        ks = fpnn_amd.KeySet(engine, key, len(key), iv)
+        datas = [bytes.fromhex(c["in"]) for c in cs]
+        lens = np.array([len(d) for d in datas], dtype=np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1] + 7)]).astype(np.int64)
+        buf = np.zeros(int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+        for o, d in zip(offs, datas):
+            buf[o:o + len(d)] = np.frombuffer(d, np.uint8)
+        src = to_dev(buf)
+        for mode in ("encrypt", "decrypt"):
+            dst = dev_u8(len(buf))
+            fn = engine.package_encrypt if mode == "encrypt" else engine.package_decrypt
+            fn(src, dst, len(cs), ks, in_off=to_dev(offs), lens=to_dev(lens))
+            torch.cuda.synchronize()
+            out = to_host(dst)
+            for i, c in enumerate(cs):
+                assert out[offs[i]:offs[i] + lens[i]].tobytes().hex() == c[mode]
+        out_offs = (offs + 4 * np.arange(len(cs))).astype(np.int64)
+        dst = dev_u8(len(buf) + 4 * len(cs))
+        engine.package_encrypt(src, dst, len(cs), ks, in_off=to_dev(offs), out_off=to_dev(out_offs),
+                               lens=to_dev(lens), wire_prefix=True)
+        torch.cuda.synchronize()
+        out = to_host(dst)
+        for i, c in enumerate(cs):
+            assert out[out_offs[i]:out_offs[i] + lens[i] + 4].tobytes().hex() == c["frame"]
+
+
+def test_golden_stream_cases(engine, golden):
+    import fpnn_amd
+    for c in golden("stream_cases.json"):
+        key, iv = bytes.fromhex(c["key"]), bytes.fromhex(c["iv"])
+        se = fpnn_amd.StreamEncryptor(engine, key, iv)
+        # device-state twin: one stream, one call per frame
+        ks = fpnn_amd.KeySet(engine, key, len(key), iv)
+        iv_state = to_dev(np.frombuffer(iv, np.uint8).copy())
+        pos_state = torch.zeros(1, dtype=torch.int32, device=DEV)
+        for fr in c["frames"]:
+            data = bytes.fromhex(fr["in"])
+            got = se.encrypt(data) if c["encrypt"] else se.decrypt(data)
+            assert got.hex() == fr["out"]
+            if data:
+                src, dst = to_dev(np.frombuffer(data, np.uint8)), dev_u8(len(data))
+                fn = engine.stream_encrypt if c["encrypt"] else engine.stream_decrypt
+                fn(src, dst, 1, ks, iv_state, pos_state, stride=0, uniform_len=len(data))
+                torch.cuda.synchronize()
+                assert to_host(dst)[:len(data)].tobytes().hex() == fr["out"]
+        assert to_host(iv_state).tobytes() == se.state[0] and int(to_host(pos_state)[0]) == se.state[1]
+
+
+# --------------------------------------------------------------------------------------
+# randomized batches against the oracle
+
+
+def make_ragged(rng, n, max_len, align_gap=True):
+    lens = rng.integers(0, max_len + 1, n)
+    special = np.array([0, 1, 15, 16, 17, 31, 32, 33, 1024, 1025, 4096])
+    pick = rng.random(n) < 0.3
+    lens[pick] = rng.choice(special, pick.sum())
+    gaps = rng.integers(0, 9, n) if align_gap else np.zeros(n, np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])]).astype(np.int64) + int(gaps[-1])
+    return lens.astype(np.int32), offs
+
+
+@pytest.mark.parametrize("keylen", [16, 24, 32])
+@pytest.mark.parametrize("nkeys", [1, 7])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_random_package_batch(engine, oracle, keylen, nkeys, inplace):
+    rng = np.random.default_rng(1000 * keylen + 10 * nkeys + inplace)
+    n = 700
+    lens, offs = make_ragged(rng, n, 3000)
+    total = int(offs[-1] + lens[-1] + 64)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+    slots = rng.integers(0, nkeys, n).astype(np.int32)
+    ks = keyset(engine, keys, keylen, ivs)
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens), key_slot=to_dev(slots) if nkeys > 1 else None)
+    for encrypt in (True, False):
+        exp = inp.copy()
+        oracle.package_batch(encrypt, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                             key_slot=slots.astype(np.uint32) if nkeys > 1 else None, keys=keys, keylen=keylen,
+                             ivs=ivs, threads=8)
+        src = to_dev(inp)
+        dst = src if inplace else to_dev(inp)  # untouched gap bytes must survive
+        fn = engine.package_encrypt if encrypt else engine.package_decrypt
+        fn(src, dst, n, ks, **kw)
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(dst), exp), f"encrypt={encrypt}"
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+@pytest.mark.parametrize("length", [1, 5, 16, 17, 64, 100, 1024, 1040, 4096])
+def test_uniform_layout(engine, oracle, keylen, length):
+    """Uniform fast path (stride/length, one key), incl. the in-place variant."""
+    rng = np.random.default_rng(length * 7 + keylen)
+    n = 2500
+    stride = length + (length % 3)  # strides that are not multiples of 16
+    inp = rng.integers(0, 256, n * stride + 8, dtype=np.uint8)
+    key, iv = rng.bytes(keylen), rng.bytes(16)
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, key, keylen, iv)
+    kb, ib = np.frombuffer(key, np.uint8).copy(), np.frombuffer(iv, np.uint8).copy()
+    for encrypt in (True, False):
+        exp = inp.copy()
+        oracle.package_batch(encrypt, inp, exp, n, stride=stride, uniform_len=length, keys=kb, keylen=keylen, ivs=ib,
+                             threads=8)
+        for inplace in (False, True):
+            src = to_dev(inp)
+            dst = src if inplace else to_dev(inp)
+            fn = engine.package_encrypt if encrypt else engine.package_decrypt
+            fn(src, dst, n, ks, stride=stride, uniform_len=length)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (encrypt, inplace)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_random_stream_batches(engine, oracle, keylen):
+    """Many streams, several successive calls each with random lengths; outputs and the
+    carried (iv, pos) state must follow the reference byte loop exactly."""
+    rng = np.random.default_rng(500 + keylen)
+    S = 333
+    keys = rng.integers(0, 256, S * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, S * 16, dtype=np.uint8)
+    ks = keyset(engine, keys, keylen, ivs)
+    for encrypt in (True, False):
+        iv_h = ivs.copy()
+        pos_h = rng.integers(0, 16, S).astype(np.uint32)
+        iv_d, pos_d = to_dev(iv_h), to_dev(pos_h.astype(np.int32))
+        for call in range(6):
+            lens = rng.integers(0, 200 if call % 2 else 2000, S).astype(np.int32)
+            lens[rng.random(S) < 0.1] = 0
+            offs = np.concatenate([[0], np.cumsum(lens[:-1] + 3)]).astype(np.int64)
+            inp = rng.integers(0, 256, int(offs[-1] + lens[-1] + 16), dtype=np.uint8)
+            exp = inp.copy()
+            slots = np.arange(S, dtype=np.uint32)
+            oracle.stream_batch(encrypt, inp, exp, S, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                                lens=lens.astype(np.uint32), key_slot=slots, keys=keys, keylen=keylen,
+                                iv_state=iv_h, pos_state=pos_h, threads=8)
+            src, dst = to_dev(inp), to_dev(inp)
+            fn = engine.stream_encrypt if encrypt else engine.stream_decrypt
+            fn(src, dst, S, ks, iv_d, pos_d, in_off=to_dev(offs), lens=to_dev(lens),
+               key_slot=to_dev(slots.astype(np.int32)))
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (encrypt, call)
+            assert np.array_equal(to_host(iv_d), iv_h), (encrypt, call)
+            assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h), (encrypt, call)
+
+
+def test_empty_and_degenerate(engine):
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, bytes(32), 32, bytes(16))
+    t = dev_u8(64)
+    engine.package_encrypt(t, t, 0, ks, stride=16, uniform_len=16)
+    engine.package_decrypt(t, t, 0, ks, stride=16, uniform_len=16)
+    engine.package_encrypt(t, t, 3, ks, stride=16, uniform_len=0)
+    engine.package_decrypt(t, t, 3, ks, stride=16, uniform_len=0)
+    torch.cuda.synchronize()
+    assert int(t.sum()) == 0
+    with pytest.raises(fpnn_amd.FpnnAesError):
+        fpnn_amd.KeySet(engine, bytes(20), 20, bytes(16))
+
+
+# --------------------------------------------------------------------------------------
+# full-size configs (BASELINE.json configs[1..4]) against reference digests / oracle
+
+
+@pytest.mark.slow
+def test_c2_full_digest(engine, golden):
+    import fpnn_amd
+    d = golden("digests.json")["C2"]
+    c = W.C2
+    P, L = c["packets"], c["length"]
+    key, iv = W.single_key(c)
+    ks = fpnn_amd.KeySet(engine, key, len(key), iv)
+    plain = torch.empty(P * L, dtype=torch.uint8, device=DEV)
+    engine.fill_synthetic(plain, c["payload_seed"])
+    cipher = torch.empty_like(plain)
+    engine.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L)
+    back = torch.empty_like(plain)
+    engine.package_decrypt(cipher, back, P, ks, stride=L, uniform_len=L)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(to_host(plain)).hexdigest() == d["plain_sha256"]
+    assert hashlib.sha256(to_host(cipher)).hexdigest() == d["cipher_sha256"]
+    assert torch.equal(back, plain)
+
+
+@pytest.mark.slow
+def test_c5_full_digest(engine, golden):
+    d = golden("digests.json")["C5"]
+    c = W.C5
+    P, L = c["packets"], c["length"]
+    keys, ivs = W.many_keys(c)
+    ks = keyset(engine, keys, c["keylen"], ivs)
+    slots = torch.arange(P, dtype=torch.int32, device=DEV)
+    plain = torch.empty(P * L, dtype=torch.uint8, device=DEV)
+    engine.fill_synthetic(plain, c["payload_seed"])
+    cipher = torch.empty_like(plain)
+    engine.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L, key_slot=slots)
+    back = torch.empty_like(plain)
+    engine.package_decrypt(cipher, back, P, ks, stride=L, uniform_len=L, key_slot=slots)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(to_host(cipher)).hexdigest() == d["cipher_sha256"]
+    assert torch.equal(back, plain)
+
+
+@pytest.mark.slow
+def test_c3_full_stream_digest(engine, golden):
+    """4096 streams x 4 MiB AES-128, each stream cut into random frames (1 B .. 64 KiB)
+    submitted as successive stream-mode calls; whole-stream digests must match the
+    reference's, and decryption with a different cut must restore the plaintext."""
+    d = golden("digests.json")["C3"]
+    c = W.C3
+    S, L = c["streams"], c["length"]
+    keys, ivs = W.many_keys(c)
+    ks = keyset(engine, keys, c["keylen"], ivs)
+    plain = torch.empty(S * L, dtype=torch.uint8, device=DEV)
+    engine.fill_synthetic(plain, c["payload_seed"])
+    cipher = torch.empty_like(plain)
+    slots = torch.arange(S, dtype=torch.int32, device=DEV)
+    base = torch.arange(S, dtype=torch.int64, device=DEV) * L
+
+    def run(fn, src, dst, split_salt):
+        splits = [W.stream_splits(c, s if split_salt == 0 else s + 100000) for s in range(S)]
+        nmax = max(len(x) for x in splits)
+        lens = np.zeros((nmax, S), dtype=np.int32)
+        for s, x in enumerate(splits):
+            lens[:len(x), s] = x
+        starts = np.cumsum(np.vstack([np.zeros((1, S), np.int64), lens[:-1]]), axis=0)
+        iv_state = to_dev(ivs.copy())
+        pos_state = torch.zeros(S, dtype=torch.int32, device=DEV)
+        for f in range(nmax):
+            offs = base + to_dev(starts[f])
+            fn(src, dst, S, ks, iv_state, pos_state, in_off=offs, lens=to_dev(lens[f]), key_slot=slots)
+        torch.cuda.synchronize()
+
+    run(engine.stream_encrypt, plain, cipher, 0)
+    host = to_host(cipher)
+    per = [hashlib.sha256(host[s * L:(s + 1) * L]).digest() for s in range(S)]
+    assert per[0].hex() == d["first_stream_sha256"]
+    assert hashlib.sha256(b"".join(per)).hexdigest() == d["stream_digests_sha256"]
+    back = torch.empty_like(plain)
+    run(engine.stream_decrypt, cipher, back, 1)
+    assert torch.equal(back, plain)
+
+
+@pytest.mark.slow
+def test_c4_zipf_vs_oracle(engine, oracle):
+    import fpnn_amd
+    c = W.C4
+    sizes = W.zipf_sizes(c)
+    n = len(sizes)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1].astype(np.int64))]).astype(np.int64)
+    total = int(offs[-1] + sizes[-1])
+    key, iv = W.single_key(c)
+    ks = fpnn_amd.KeySet(engine, key, len(key), iv)
+    plain = torch.empty(total, dtype=torch.uint8, device=DEV)
+    engine.fill_synthetic(plain, c["payload_seed"])
+    cipher = torch.empty_like(plain)
+    kw = dict(in_off=to_dev(offs), lens=to_dev(sizes.astype(np.int32)))
+    engine.package_encrypt(plain, cipher, n, ks, **kw)
+    back = torch.empty_like(plain)
+    engine.package_decrypt(cipher, back, n, ks, **kw)
+    torch.cuda.synchronize()
+    inp = to_host(plain)
+    exp = np.empty_like(inp)
+    oracle.package_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), lens=sizes.astype(np.uint32),
+                         keys=np.frombuffer(key, np.uint8).copy(), keylen=len(key),
+                         ivs=np.frombuffer(iv, np.uint8).copy(), threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(to_host(cipher), exp)
+    assert torch.equal(back, plain)
+
+
+# --------------------------------------------------------------------------------------
+# the C++ drop-in surface (include/Encryptor.h, include/rijndael.h) used as FPNN uses it
+
+
+def test_cpp_dropin_matches_reference(golden, tmp_path):
+    from test_abi import build_dropin
+    exe = build_dropin(tmp_path)
+    lines, expect = [], []
+    for c in golden("package_cases.json"):
+        lines.append(f"P {c['key']} {c['iv']} {c['in'] or '-'}")
+        expect.append(f"{c['encrypt'] or '-'} {c['decrypt'] or '-'} {c['frame']}")
+    for c in golden("stream_cases.json"):
+        frames = [f for f in c["frames"]]
+        lines.append(f"S {'E' if c['encrypt'] else 'D'} {c['key']} {c['iv']} " +
+                     " ".join(f["in"] or "-" for f in frames))
+        expect.append(" ".join(f["out"] or "-" for f in frames))
+    demo = golden("package_cases.json")[-1]  # base/test/rijndaelDemo.cpp inputs
+    lines.append(f"R {demo['key']} {demo['iv']} {demo['in']}")
+    expect.append(f"0 {demo['encrypt']}")
+    import subprocess
+    res = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    got = res.stdout.strip().split("\n")
+    assert got == expect

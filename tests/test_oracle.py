@@ -1,0 +1,107 @@
+"""Pin the oracle before trusting it (CPU only).
+
+1. Published known answers: FIPS-197 appendix C.1/C.3 and NIST SP 800-38A F.3.13 /
+   F.3.17 (independent of the reference; the reference reproduces them too).
+2. Golden fixtures produced by the compiled reference (oracle/gen_golden.py).
+3. Live randomized comparison with oracle/_ref when it is built (this container).
+"""
+import numpy as np
+import pytest
+
+FIPS_C1 = ("000102030405060708090a0b0c0d0e0f", "00112233445566778899aabbccddeeff", "69c4e0d86a7b0430d8cdb78070b4c55a")
+FIPS_C3 = ("000102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f", "00112233445566778899aabbccddeeff",
+           "8ea2b7ca516745bfeafc49904b496089")
+SP_PT = ("6bc1bee22e409f96e93d7e117393172aae2d8a571e03ac9c9eb76fac45af8e51"
+         "30c81c46a35ce411e5fbc1191a0a52eff69f2445df4f9b17ad2b417be66c3710")
+SP_F313 = ("2b7e151628aed2a6abf7158809cf4f3c",
+           "3b3fd92eb72dad20333449f8e83cfb4ac8a64537a0b3a93fcde3cdad9f1ce58b"
+           "26751f67a3cbb140b1808cf187a4f4dfc04b05357c5d1c0eeac4c66f9ff7f2e6")
+SP_F317 = ("603deb1015ca71be2b73aef0857d77811f352c073b6108d72d9810a30914dff4",
+           "dc7e84bfda79164b7ecd8486985d386039ffed143b28b1c832113c6331e5407b"
+           "df10132415e54b92a13ed0a8267ae2f975a385741ab9cef82031623d55b1e471")
+IV = bytes(range(16))
+
+
+@pytest.mark.parametrize("kat", [FIPS_C1, FIPS_C3])
+def test_fips197_ecb(oracle, kat):
+    key, pt, ct = (bytes.fromhex(x) for x in kat)
+    assert oracle.encrypt_block(key, pt) == ct
+
+
+@pytest.mark.parametrize("kat", [SP_F313, SP_F317])
+def test_sp800_38a_cfb128(oracle, kat):
+    key, ct = bytes.fromhex(kat[0]), bytes.fromhex(kat[1])
+    pt = bytes.fromhex(SP_PT)
+    assert oracle.cfb(key, True, pt, IV)[0] == ct
+    assert oracle.cfb(key, False, ct, IV)[0] == pt
+    # split calls exercise the (ivec, pos) carry
+    out1, iv1, n1 = oracle.cfb(key, True, pt[:23], IV)
+    out2, _, _ = oracle.cfb(key, True, pt[23:], iv1, n1)
+    assert out1 + out2 == ct
+
+
+def test_golden_kat(oracle, golden):
+    g = golden("kat.json")
+    for v in g["ecb"]:
+        assert oracle.encrypt_block(bytes.fromhex(v["key"]), bytes.fromhex(v["in"])).hex() == v["out"], v["name"]
+    for v in g["cfb"]:
+        out = oracle.cfb(bytes.fromhex(v["key"]), True, bytes.fromhex(v["in"]), bytes.fromhex(v["iv"]))[0]
+        assert out.hex() == v["out"], v["name"]
+
+
+def test_golden_cfb_cases(oracle, golden):
+    cases = golden("cfb_cases.json")
+    assert len(cases) >= 200
+    for c in cases:
+        out, iv, pos = oracle.cfb(bytes.fromhex(c["key"]), c["encrypt"], bytes.fromhex(c["in"]), bytes.fromhex(c["iv"]),
+                                  c["pos"])
+        assert (out.hex(), iv.hex(), pos) == (c["out"], c["iv_out"], c["pos_out"])
+
+
+def test_golden_package_cases(oracle, golden):
+    for c in golden("package_cases.json"):
+        key, iv, data = (bytes.fromhex(c[k]) for k in ("key", "iv", "in"))
+        assert oracle.package(key, iv, True, data).hex() == c["encrypt"]
+        assert oracle.package(key, iv, False, data).hex() == c["decrypt"]
+        assert oracle.package_frame(key, iv, data).hex() == c["frame"]
+
+
+def test_golden_stream_cases(oracle, golden):
+    from pyoracle import StreamOracle
+    for c in golden("stream_cases.json"):
+        s = StreamOracle(oracle, bytes.fromhex(c["key"]), bytes.fromhex(c["iv"]))
+        for fr in c["frames"]:
+            assert s.crypt(c["encrypt"], bytes.fromhex(fr["in"])).hex() == fr["out"]
+
+
+def test_package_batch_matches_single_calls(oracle):
+    rng = np.random.default_rng(3)
+    n = 50
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 3)]).astype(np.uint64)
+    total = int(offs[-1] + lens[-1] + 16)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    out = np.zeros_like(inp)
+    keys = rng.integers(0, 256, 3 * 32, dtype=np.uint8)
+    ivs = rng.integers(0, 256, 3 * 16, dtype=np.uint8)
+    slots = (np.arange(n) % 3).astype(np.uint32)
+    oracle.package_batch(True, inp, out, n, in_off=offs, lens=lens, key_slot=slots, keys=keys, keylen=32, ivs=ivs,
+                         threads=4)
+    for i in range(n):
+        k = keys[32 * slots[i]: 32 * slots[i] + 32].tobytes()
+        v = ivs[16 * slots[i]: 16 * slots[i] + 16].tobytes()
+        seg = inp[offs[i]: offs[i] + lens[i]].tobytes()
+        assert out[offs[i]: offs[i] + lens[i]].tobytes() == oracle.package(k, v, True, seg)
+
+
+def test_live_reference_random(oracle, ref_oracle):
+    rng = np.random.default_rng(99)
+    for t in range(1500):
+        kl = (16, 24, 32)[t % 3]
+        key, iv = rng.bytes(kl), rng.bytes(16)
+        data = rng.bytes(int(rng.integers(0, 700)))
+        pos = int(rng.integers(0, 16))
+        enc = bool(t & 1)
+        assert oracle.cfb(key, enc, data, iv, pos) == ref_oracle.cfb(key, enc, data, iv, pos)
+        if kl != 24:
+            assert oracle.package_frame(key, iv, data) == ref_oracle.package_frame(key, iv, data)
