@@ -70,7 +70,8 @@ struct fpnn_aes_engine {
 };
 
 struct fpnn_aes_keyset {
-    fpnn_aes_engine *e = nullptr;
+    fpnn_aes_engine *e = nullptr;  // creating engine (may be destroyed before the key set)
+    int device = 0;
     DevKey *d_keys = nullptr;
     uint32_t count = 0;
     int nrounds = 0;
@@ -137,7 +138,7 @@ uint64_t magic_for(uint32_t d) {
 int check_batch(const fpnn_aes_engine *e, const fpnn_aes_batch *b) {
     if (!e || !b || !b->keys) return FPNN_AES_ERR_ARG;
     if (b->count && (!b->in || !b->out)) return FPNN_AES_ERR_ARG;
-    if (b->keys->e && b->keys->e->device != e->device) return FPNN_AES_ERR_ARG;
+    if (b->keys->device != e->device) return FPNN_AES_ERR_ARG;
     if (b->keys->count == 0) return FPNN_AES_ERR_ARG;
     return FPNN_AES_OK;
 }
@@ -383,6 +384,7 @@ int fpnn_aes_keyset_create(fpnn_aes_engine *e, uint32_t count, size_t keylen, co
     DeviceGuard g(e->device);
     fpnn_aes_keyset *ks = new fpnn_aes_keyset();
     ks->e = e;
+    ks->device = e->device;
     ks->count = count;
     ks->keylen = (uint32_t)keylen;
     ks->nrounds = (int)keylen / 4 + 6;
@@ -433,6 +435,7 @@ int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpn
     DeviceGuard g(e->device);
     fpnn_aes_keyset *ks = new fpnn_aes_keyset();
     ks->e = e;
+    ks->device = e->device;
     ks->count = count;
     ks->nrounds = nr;
     ks->keylen = (uint32_t)(nr - 6) * 4;
@@ -449,9 +452,8 @@ int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpn
 
 int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks) {
     if (!ks) return FPNN_AES_OK;
-    if (ks->d_keys) {
-        DeviceGuard g(ks->e->device);
-        (void)hipStreamSynchronize(ks->e->stream);
+    if (ks->d_keys) {  // hipFree waits for outstanding work on the device
+        DeviceGuard g(ks->device);
         (void)hipFree(ks->d_keys);
     }
     delete ks;
@@ -462,7 +464,7 @@ int fpnn_aes_keyset_nrounds(const fpnn_aes_keyset *ks) { return ks ? ks->nrounds
 
 int fpnn_aes_keyset_get_schedule(fpnn_aes_keyset *ks, uint32_t slot, fpnn_aes_schedule *out) {
     if (!ks || !out || slot >= ks->count) return FPNN_AES_ERR_ARG;
-    DeviceGuard g(ks->e->device);
+    DeviceGuard g(ks->device);
     DevKey d;
     HIP_TRY(hipMemcpy(&d, ks->d_keys + slot, sizeof d, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof *out);
@@ -530,6 +532,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
 
     fpnn_aes_keyset ks;
     ks.e = e;
+    ks.device = e->device;
     ks.d_keys = reinterpret_cast<DevKey *>(e->d_stage);
     ks.count = 1;
     ks.nrounds = nr;

@@ -14,8 +14,10 @@ memory and streams only, every payload byte is transformed by the HIP kernels.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
-from typing import Optional, Sequence
+import weakref
+from typing import Optional
 
 import torch
 
@@ -25,6 +27,20 @@ from ._lib import (BatchDesc, FpnnAesError, Schedule, check, lib, F_WIRE_PREFIX,
 
 def _buf(b: bytes):
     return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8))
+
+
+# Live handles, released (key sets first) at interpreter exit while the HIP runtime
+# is still up -- finalizers that run during runtime teardown must not call into HIP.
+_live_keysets: "weakref.WeakSet" = weakref.WeakSet()
+_live_engines: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _release_all():
+    for ks in list(_live_keysets):
+        ks.close()
+    for e in list(_live_engines):
+        e.close()
 
 
 def setup_encrypt(key: bytes) -> Schedule:
@@ -64,6 +80,7 @@ class Engine:
         h = C.c_void_p()
         check(lib.fpnn_aes_engine_create(device, C.c_void_p(stream.cuda_stream), C.byref(h)), "engine_create")
         self._h = h
+        _live_engines.add(self)
 
     @property
     def handle(self):
@@ -168,6 +185,7 @@ class KeySet:
                                             _ptr(ivs) if ivs is not None else None, 0, C.byref(h))
         check(rc, "keyset_create")
         self._h = h
+        _live_keysets.add(self)
         self.count = count
         self.keylen = keylen
         self.engine = engine
