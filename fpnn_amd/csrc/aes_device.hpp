@@ -1,11 +1,11 @@
 // aes_device.hpp -- CDNA4 (gfx950) device building blocks for the AES-CFB kernels.
 //
-// LDS table image (128 KiB per workgroup, one workgroup per CU):
-//   The four forward T-tables T0..T3 (little-endian form of the reference's
-//   Te0..Te3, base/rijndael.c:8-278) are replicated 32 times so that lane l reads
-//   copy (l & 31), which lives in bank (l & 31): every ds_read_b32 of a wave is
+// LDS table image:
+//   The forward T-tables (little-endian form of the reference's Te0..Te3,
+//   base/rijndael.c:8-278) are replicated 32 times so that lane l reads copy
+//   (l & 31), which lives in bank (l & 31): every ds_read_b32 of a wave is
 //   bank-conflict free whatever the table indices are.
-//     table k = 2*r + h  (region r in {0,1}, half h in {0,1})
+//     table k = 2*r + h  (region r in {0,1}, half h in {0,1}; NT = 4 layout)
 //     entry (x, copy c) at byte  r*65536 + x*256 + h*128 + c*4
 //   The byte address of a lookup is then a single v_perm_b32:
 //     addr = { lanebase.b0, state.byte_j, lanebase.b2, 0 }   (lanebase = c*4 | r<<16)
@@ -24,16 +24,26 @@
 
 namespace fpnn_aes {
 
-constexpr uint32_t kLdsBytes = 131072;  // 4 tables x 256 entries x 32 copies x 4 B
+// Two LDS layouts (template parameter NT = number of distinct tables in LDS):
+//   NT = 4: T0..T3, 128 KiB -> one 1024-thread workgroup per CU (4 waves/SIMD).
+//   NT = 2: T0 and T2 only, 64 KiB -> two workgroups per CU (8 waves/SIMD);
+//           T1 = rotl8(T0) and T3 = rotl8(T2) cost one v_alignbit each.
+template <int NT>
+struct Lds {
+    static constexpr uint32_t kBytes = NT == 4 ? 131072u : 65536u;
+    static constexpr int kBlocksPerCU = NT == 4 ? 1 : 2;
+};
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t v, uint32_t n) { return __builtin_rotateleft32(v, n); }
 
 // Fill the replicated table image from the 1 KiB T0 (little-endian) source.
+template <int NT>
 __device__ __forceinline__ void lds_fill_tables(uint4 *lds4, const uint32_t *__restrict__ t0le) {
-    for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += blockDim.x) {
+    for (uint32_t i = threadIdx.x; i < Lds<NT>::kBytes / 16; i += blockDim.x) {
         // uint4 index i covers copies c = 4*(i&7) .. +3 of entry (r, x, h)
         const uint32_t r = i >> 12, x = (i >> 4) & 255, h = (i >> 3) & 1;
-        const uint32_t v = rotl32(__ldg(t0le + x), 8u * (2u * r + h));
+        const uint32_t k = NT == 4 ? 2u * r + h : 2u * h;  // which T_k this half holds
+        const uint32_t v = rotl32(__ldg(t0le + x), 8u * k);
         lds4[i] = make_uint4(v, v, v, v);
     }
 }
@@ -55,6 +65,35 @@ __device__ __forceinline__ uint32_t lds_word(const char *lds, uint32_t addr, uin
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+
+// T_j lookup of byte j of w (j = 0..3) and the final-round S-box byte placed at byte j.
+template <int NT>
+struct Tables4 {
+    const char *lds;
+    LaneBase lb;
+    template <int J>
+    __device__ __forceinline__ uint32_t t(uint32_t w) const {
+        if (NT == 4) {
+            const uint32_t base = (J < 2) ? lb.lb0 : lb.lb1;
+            return lds_word(lds, __builtin_amdgcn_perm(base, w, sel(J)), (J & 1) ? 128 : 0);
+        } else {  // T0 at +0, T2 at +128; odd tables by rotation
+            const uint32_t v = lds_word(lds, __builtin_amdgcn_perm(lb.lb0, w, sel(J)), (J >= 2) ? 128 : 0);
+            return (J & 1) ? rotl32(v, 8) : v;
+        }
+    }
+    // S(byte j of w) at byte j: T0 entries hold S in bytes 1,2; T2 entries in bytes 0,3
+    template <int J>
+    __device__ __forceinline__ uint32_t s(uint32_t w) const {
+        constexpr uint32_t mask = 0xffu << (8 * J);
+        constexpr bool from_t2 = (J == 0 || J == 3);
+        if (NT == 4) {
+            const uint32_t base = from_t2 ? lb.lb1 : lb.lb0;
+            return lds_word(lds, __builtin_amdgcn_perm(base, w, sel(J)), 0) & mask;
+        } else {
+            return lds_word(lds, __builtin_amdgcn_perm(lb.lb0, w, sel(J)), from_t2 ? 128 : 0) & mask;
+        }
+    }
+};
 
 // Round keys for NR rounds (block byte order).  Loaded from a uniform pointer they
 // live in SGPRs; from a per-lane pointer in VGPRs.
@@ -78,40 +117,26 @@ __device__ __forceinline__ RoundKeys<NR> load_round_keys(const DevKey *key) {
     return r;
 }
 
-template <int NR>
-__device__ __forceinline__ uint4 aes_encrypt_block(uint4 in, const RoundKeys<NR> &rk, const char *lds,
-                                                   const LaneBase &lb) {
+template <int NR, int NT>
+__device__ __forceinline__ uint4 aes_encrypt_block(uint4 in, const RoundKeys<NR> &rk, const Tables4<NT> &T) {
     uint32_t s0 = in.x ^ rk.k[0], s1 = in.y ^ rk.k[1], s2 = in.z ^ rk.k[2], s3 = in.w ^ rk.k[3];
-#define FPNN_T0(w) lds_word(lds, __builtin_amdgcn_perm(lb.lb0, (w), sel(0)), 0)
-#define FPNN_T1(w) lds_word(lds, __builtin_amdgcn_perm(lb.lb0, (w), sel(1)), 128)
-#define FPNN_T2(w) lds_word(lds, __builtin_amdgcn_perm(lb.lb1, (w), sel(2)), 0)
-#define FPNN_T3(w) lds_word(lds, __builtin_amdgcn_perm(lb.lb1, (w), sel(3)), 128)
 #pragma unroll
     for (int r = 1; r < NR; r++) {
-        const uint32_t t0 = xor3(xor3(FPNN_T0(s0), FPNN_T1(s1), FPNN_T2(s2)), FPNN_T3(s3), rk.k[4 * r + 0]);
-        const uint32_t t1 = xor3(xor3(FPNN_T0(s1), FPNN_T1(s2), FPNN_T2(s3)), FPNN_T3(s0), rk.k[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(FPNN_T0(s2), FPNN_T1(s3), FPNN_T2(s0)), FPNN_T3(s1), rk.k[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(FPNN_T0(s3), FPNN_T1(s0), FPNN_T2(s1)), FPNN_T3(s2), rk.k[4 * r + 3]);
+        const uint32_t t0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s1), T.template t<2>(s2)),
+                                 T.template t<3>(s3), rk.k[4 * r + 0]);
+        const uint32_t t1 = xor3(xor3(T.template t<0>(s1), T.template t<1>(s2), T.template t<2>(s3)),
+                                 T.template t<3>(s0), rk.k[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(T.template t<0>(s2), T.template t<1>(s3), T.template t<2>(s0)),
+                                 T.template t<3>(s1), rk.k[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(T.template t<0>(s3), T.template t<1>(s0), T.template t<2>(s1)),
+                                 T.template t<3>(s2), rk.k[4 * r + 3]);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-#undef FPNN_T0
-#undef FPNN_T1
-#undef FPNN_T2
-#undef FPNN_T3
-    // Final round: S(x) sits in bytes 1,2 of T0 entries and bytes 0,3 of T2 entries.
-#define FPNN_S0(w) (lds_word(lds, __builtin_amdgcn_perm(lb.lb1, (w), sel(0)), 0) & 0x000000ffu)
-#define FPNN_S1(w) (lds_word(lds, __builtin_amdgcn_perm(lb.lb0, (w), sel(1)), 0) & 0x0000ff00u)
-#define FPNN_S2(w) (lds_word(lds, __builtin_amdgcn_perm(lb.lb0, (w), sel(2)), 0) & 0x00ff0000u)
-#define FPNN_S3(w) (lds_word(lds, __builtin_amdgcn_perm(lb.lb1, (w), sel(3)), 0) & 0xff000000u)
     uint4 o;
-    o.x = (FPNN_S0(s0) | FPNN_S1(s1) | FPNN_S2(s2) | FPNN_S3(s3)) ^ rk.k[4 * NR + 0];
-    o.y = (FPNN_S0(s1) | FPNN_S1(s2) | FPNN_S2(s3) | FPNN_S3(s0)) ^ rk.k[4 * NR + 1];
-    o.z = (FPNN_S0(s2) | FPNN_S1(s3) | FPNN_S2(s0) | FPNN_S3(s1)) ^ rk.k[4 * NR + 2];
-    o.w = (FPNN_S0(s3) | FPNN_S1(s0) | FPNN_S2(s1) | FPNN_S3(s2)) ^ rk.k[4 * NR + 3];
-#undef FPNN_S0
-#undef FPNN_S1
-#undef FPNN_S2
-#undef FPNN_S3
+    o.x = (T.template s<0>(s0) | T.template s<1>(s1) | T.template s<2>(s2) | T.template s<3>(s3)) ^ rk.k[4 * NR + 0];
+    o.y = (T.template s<0>(s1) | T.template s<1>(s2) | T.template s<2>(s3) | T.template s<3>(s0)) ^ rk.k[4 * NR + 1];
+    o.z = (T.template s<0>(s2) | T.template s<1>(s3) | T.template s<2>(s0) | T.template s<3>(s1)) ^ rk.k[4 * NR + 2];
+    o.w = (T.template s<0>(s3) | T.template s<1>(s0) | T.template s<2>(s1) | T.template s<3>(s2)) ^ rk.k[4 * NR + 3];
     return o;
 }
 

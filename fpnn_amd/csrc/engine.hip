@@ -7,6 +7,7 @@
 // transformed by the HIP kernels in kernels.hip.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -47,6 +48,7 @@ struct fpnn_aes_engine {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     int num_cus = 256;
+    Variant variant;
     uint8_t *d_tables = nullptr;  // t0le[256] (1 KiB) then sbox[256]
     // general-layout scratch
     uint64_t *d_bstart = nullptr;
@@ -57,6 +59,10 @@ struct fpnn_aes_engine {
     uint64_t cap_tile = 0;
     uint4 *d_boundary = nullptr;
     uint64_t cap_boundary = 0;
+    uint4 *d_snap_iv = nullptr;  // stream-decrypt state snapshot
+    uint64_t cap_snap_iv = 0;
+    uint32_t *d_snap_pos = nullptr;
+    uint64_t cap_snap_pos = 0;
     uint64_t *d_total = nullptr;
     uint64_t *h_total = nullptr;  // pinned
     // host staging for fpnn_aes_cfb_host
@@ -179,10 +185,11 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     const uint64_t want = (b->count + kThreads - 1) / kThreads;
-    const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+    const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
+    const int grid = (int)(want < cap ? (want ? want : 1) : cap);
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, e->stream));
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, e->stream));
     return timing_end(e, ev);
 }
 
@@ -194,6 +201,14 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
+    if (stream) {  // snapshot the incoming (iv, pos) state, see KBatch::iv_snap
+        if ((rc = grow(e->d_snap_iv, e->cap_snap_iv, b->count))) return rc;
+        if ((rc = grow(e->d_snap_pos, e->cap_snap_pos, b->count))) return rc;
+        HIP_TRY(hipMemcpyAsync(e->d_snap_iv, iv_state, 16ull * b->count, hipMemcpyDeviceToDevice, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->d_snap_pos, pos_state, 4ull * b->count, hipMemcpyDeviceToDevice, e->stream));
+        k.iv_snap = e->d_snap_iv;
+        k.pos_snap = e->d_snap_pos;
+    }
     const bool inplace = b->in == b->out && b->out_off == nullptr;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     // Uniform layout: every segment has the same block count, known on the host.
@@ -233,10 +248,11 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.boundary = e->d_boundary;
     }
     const uint64_t want = (nchunks + 15) / 16;  // 16 waves per workgroup
-    const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+    const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
+    const int grid = (int)(want < cap ? (want ? want : 1) : cap);
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, layout, km, stream, inplace, grid, e->stream));
+    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, stream, inplace, grid, e->stream));
     return timing_end(e, ev);
 }
 
@@ -304,6 +320,11 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     fpnn_aes_engine *e = new fpnn_aes_engine();
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
+    if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
+    if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
+        const int c = atoi(v);
+        e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;
+    }
     int rc = FPNN_AES_OK;
     do {
         if (hip_stream != FPNN_AES_OWN_STREAM) {
@@ -339,6 +360,8 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_wgsums);
     (void)hipFree(e->d_tile);
     (void)hipFree(e->d_boundary);
+    (void)hipFree(e->d_snap_iv);
+    (void)hipFree(e->d_snap_pos);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_total) (void)hipHostFree(e->h_total);

@@ -84,13 +84,12 @@ __device__ __forceinline__ uint64_t seg_blocks(uint32_t len, uint32_t n0) {
 // ---------------------------------------------------------------------------
 // K2: encryption, one lane per chain.
 
-template <int NR, int LAYOUT, int KM, bool STREAM>
-__global__ __launch_bounds__(kThreads, 1) void k_cfb_encrypt_chains(KBatch b) {
-    __shared__ uint4 lds4[kLdsBytes / 16];
-    lds_fill_tables(lds4, b.t0le);
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT, int CH>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_encrypt_chains(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
-    const char *lds = reinterpret_cast<const char *>(lds4);
-    const LaneBase lb;
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
 
     RoundKeys<NR> rku;
     if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
@@ -138,10 +137,37 @@ __global__ __launch_bounds__(kThreads, 1) void k_cfb_encrypt_chains(KBatch b) {
         }
 
         const uint32_t nfull = rem >> 4;
-        uint4 pt = nfull ? load16(p) : make_uint4(0, 0, 0, 0);
-        for (uint32_t i = 0; i < nfull; i++) {
+        uint32_t i = 0;
+        if (CH > 1 && nfull >= CH) {
+            // CH-block chunks (CH*16 = 64 or 128 bytes): a chunk's loads and its stores
+            // each go out back to back, so every cache line is read and written whole
+            // while it is in L2; the next chunk's loads are in flight during this
+            // chunk's rounds.
+            uint4 a[CH], c[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = load16(p + 16 * j);
+            for (; i + CH <= nfull; i += CH) {
+                const bool more = i + 2 * CH <= nfull;
+                uint4 nx[CH];
+#pragma unroll
+                for (int j = 0; j < CH; j++) nx[j] = more ? load16(p + 16 * (CH + j)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ a[j];
+                    c[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < CH; j++) store16(q + 16 * j, c[j]);
+#pragma unroll
+                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                p += 16 * CH;
+                q += 16 * CH;
+            }
+        }
+        uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
+        for (; i < nfull; i++) {
             const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
-            iv = aes_encrypt_block<NR>(iv, rk, lds, lb) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ pt;  // C_i = P_i ^ E(C_{i-1})
             store16(q, iv);
             pt = pn;
             p += 16;
@@ -149,7 +175,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cfb_encrypt_chains(KBatch b) {
         }
         rem &= 15u;
         if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
-            const uint4 ks = aes_encrypt_block<NR>(iv, rk, lds, lb);
+            const uint4 ks = aes_encrypt_block<NR, NT>(iv, rk, T);
             const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
             store_bytes(q, o, 0, (int)rem);
             iv = select_bytes(byte_mask(0, (int)rem), o, ks);
@@ -188,13 +214,12 @@ __device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64
     }
 }
 
-template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE>
-__global__ __launch_bounds__(kThreads, 1) void k_cfb_decrypt_blocks(KBatch b) {
-    __shared__ uint4 lds4[kLdsBytes / 16];
-    lds_fill_tables(lds4, b.t0le);
+template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE, int NT>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_blocks(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
-    const char *lds = reinterpret_cast<const char *>(lds4);
-    const LaneBase lb;
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
     const uint32_t lane = threadIdx.x & 63u;
 
     RoundKeys<NR> rku;
@@ -210,10 +235,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_cfb_decrypt_blocks(KBatch b) {
         uint32_t bi;
         locate_block<LAYOUT>(b, c, gblk, total, s, bi);
         const Seg g = get_seg<LAYOUT>(b, s);
-        const uint32_t n0 = STREAM ? b.pos_state[s] : 0u;
+        const uint32_t n0 = STREAM ? b.pos_snap[s] : 0u;
         const uint32_t slot = KM == KEY_UNIFORM ? 0u : g.slot;
         const DevKey *key = b.keys + slot;
-        const uint4 ivs = STREAM ? ld_state_iv(b.iv_state + 16 * s) : *reinterpret_cast<const uint4 *>(key->iv);
+        const uint4 ivs = STREAM ? b.iv_snap[s] : *reinterpret_cast<const uint4 *>(key->iv);
 
         const uint4 x = valid ? load_cx(g, n0, bi, ivs) : make_uint4(0, 0, 0, 0);
         uint4 xp = wave_shr1(x);  // C_{i-1} from the neighbouring lane (all 64 lanes active here)
@@ -222,16 +247,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_cfb_decrypt_blocks(KBatch b) {
 
         uint4 ks;
         if (KM == KEY_UNIFORM) {
-            ks = aes_encrypt_block<NR>(kin, rku, lds, lb);
+            ks = aes_encrypt_block<NR, NT>(kin, rku, T);
         } else {
             const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slot);
             const uint32_t my = valid ? slot : slot0;
             if (__builtin_amdgcn_ballot_w64(my != slot0) == 0) {  // wave-uniform key: SGPR round keys
                 const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + slot0);
-                ks = aes_encrypt_block<NR>(kin, rk, lds, lb);
+                ks = aes_encrypt_block<NR, NT>(kin, rk, T);
             } else {
                 const RoundKeys<NR> rk = load_round_keys<NR>(key);
-                ks = aes_encrypt_block<NR>(kin, rk, lds, lb);
+                ks = aes_encrypt_block<NR, NT>(kin, rk, T);
             }
         }
         if (STREAM && bi == 0 && n0 != 0) ks = ivs;  // keystream block already in the carried state
@@ -260,9 +285,9 @@ __global__ __launch_bounds__(256) void k_boundary_save(KBatch b, uint4 *boundary
         locate_block<LAYOUT>(b, c, c << 6, b.total_blocks, s, bi);
         if (bi == 0) continue;
         const Seg g = get_seg<LAYOUT>(b, s);
-        const uint32_t n0 = STREAM ? b.pos_state[s] : 0u;
+        const uint32_t n0 = STREAM ? b.pos_snap[s] : 0u;
         const DevKey *key = b.keys + g.slot;
-        const uint4 ivs = STREAM ? ld_state_iv(b.iv_state + 16 * s) : *reinterpret_cast<const uint4 *>(key->iv);
+        const uint4 ivs = STREAM ? b.iv_snap[s] : *reinterpret_cast<const uint4 *>(key->iv);
         boundary[c] = load_cx(g, n0, bi - 1, ivs);
     }
 }
@@ -278,7 +303,7 @@ template <bool STREAM>
 __device__ __forceinline__ uint64_t nblocks_of(const KBatch &b, uint64_t s) {
     if (s >= b.count) return 0;
     const uint32_t len = b.len ? b.len[s] : b.uniform_len;
-    return seg_blocks(len, STREAM ? b.pos_state[s] : 0u);
+    return seg_blocks(len, STREAM ? b.pos_snap[s] : 0u);
 }
 
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
@@ -423,60 +448,84 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
 // ---------------------------------------------------------------------------
 // Launchers (runtime -> template dispatch)
 
-template <int NR>
-static hipError_t enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
-#define FPNN_ENC(L, K, S) hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S>), dim3(grid), dim3(kThreads), 0, st, b)
+// Variant selection.  Per-packet keys need ~100 VGPRs of round keys, so they always
+// use the 4-table layout (one workgroup per CU); uniform-key variants take the
+// layout the engine asks for.
+template <int NR, int NT, int CH>
+static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+#define FPNN_ENC(L, K, S, NTX) \
+    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(kThreads), 0, st, b)
     if (layout == LAYOUT_UNIFORM) {
-        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
     } else if (km == KEY_UNIFORM) {
-        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false);
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
     } else {
-        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false);
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false, 4);
     }
 #undef FPNN_ENC
-    return hipGetLastError();
-}
-
-hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
-                                 hipStream_t st) {
-    switch (nrounds) {
-        case 10: return enc_nr<10>(b, layout, km, stream, grid, st);
-        case 12: return enc_nr<12>(b, layout, km, stream, grid, st);
-        case 14: return enc_nr<14>(b, layout, km, stream, grid, st);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <int NR, bool INPLACE>
-static hipError_t dec_nr_ip(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
-#define FPNN_DEC(L, K, S) \
-    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE>), dim3(grid), dim3(kThreads), 0, st, b)
-    if (layout == LAYOUT_UNIFORM) {
-        if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false);
-    } else if (km == KEY_UNIFORM) {
-        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, false);
-    } else {
-        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, false);
-    }
-#undef FPNN_DEC
-    return hipGetLastError();
 }
 
 template <int NR>
-static hipError_t dec_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, bool inplace, int grid,
-                         hipStream_t st) {
-    return inplace ? dec_nr_ip<NR, true>(b, layout, km, stream, grid, st)
-                   : dec_nr_ip<NR, false>(b, layout, km, stream, grid, st);
+static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid,
+                   hipStream_t st) {
+    if (v.tables == 2) {
+        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, st);
+        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, st);
+    } else {
+        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, st);
+        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, st);
+        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, st);
+    }
 }
 
-hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, bool inplace,
-                                 int grid, hipStream_t st) {
+int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }
+
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, int grid, hipStream_t st) {
     switch (nrounds) {
-        case 10: return dec_nr<10>(b, layout, km, stream, inplace, grid, st);
-        case 12: return dec_nr<12>(b, layout, km, stream, inplace, grid, st);
-        case 14: return dec_nr<14>(b, layout, km, stream, inplace, grid, st);
+        case 10: enc_nr<10>(b, v, layout, km, stream, grid, st); break;
+        case 12: enc_nr<12>(b, v, layout, km, stream, grid, st); break;
+        case 14: enc_nr<14>(b, v, layout, km, stream, grid, st); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+template <int NR, bool INPLACE, int NT>
+static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+#define FPNN_DEC(L, K, S, NTX) \
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX>), dim3(grid), dim3(kThreads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
+    } else {
+        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, false, 4);
+    }
+#undef FPNN_DEC
+}
+
+template <int NR>
+static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, bool inplace, int grid,
+                   hipStream_t st) {
+    if (v.tables == 2) {
+        if (inplace) dec_launch<NR, true, 2>(b, layout, km, stream, grid, st);
+        else dec_launch<NR, false, 2>(b, layout, km, stream, grid, st);
+    } else {
+        if (inplace) dec_launch<NR, true, 4>(b, layout, km, stream, grid, st);
+        else dec_launch<NR, false, 4>(b, layout, km, stream, grid, st);
+    }
+}
+
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, bool inplace, int grid, hipStream_t st) {
+    switch (nrounds) {
+        case 10: dec_nr<10>(b, v, layout, km, stream, inplace, grid, st); break;
+        case 12: dec_nr<12>(b, v, layout, km, stream, inplace, grid, st); break;
+        case 14: dec_nr<14>(b, v, layout, km, stream, inplace, grid, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 static int grid_for(uint64_t items, int threads, int cap) {

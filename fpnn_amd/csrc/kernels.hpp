@@ -35,15 +35,28 @@ struct KBatch {
     const uint64_t *bstart;  // general: first virtual block of each segment (count + 1)
     const uint64_t *tile_first;  // general: segment holding block 64*c (nchunks + 1)
     const uint4 *boundary;   // in-place: Cx block preceding each 64-block chunk
+    // stream decrypt: the (iv, pos) state as it was when the call was queued.  The
+    // kernel writes the new state into iv_state/pos_state while other waves may still
+    // be reading the old one, so every read goes to this snapshot.
+    const uint4 *iv_snap;
+    const uint32_t *pos_snap;
 };
 
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
-hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream,
-                                 int grid, hipStream_t st);
-hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream,
-                                 bool inplace, int grid, hipStream_t st);
+// Kernel build variant chosen per engine (defaults tuned on MI355X; overridable with
+// FPNN_AES_TABLES / FPNN_AES_ENC_CHUNK for A/B measurements).
+struct Variant {
+    int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
+    int enc_chunk = 8;  // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
+};
+
+int blocks_per_cu(const Variant &v, KeyMode km);
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, int grid, hipStream_t st);
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, bool inplace, int grid, hipStream_t st);
 hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
                                 hipStream_t st);
 // General-layout block map: bstart[] and *total (device); wg_sums scratch of

@@ -15,7 +15,7 @@ DEV = "cuda:0"
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return torch.from_numpy(np.array(a, copy=True)).to(DEV)
 
 
 def to_host(t: torch.Tensor) -> np.ndarray:
@@ -283,6 +283,41 @@ def test_random_stream_batches(engine, oracle, keylen):
             assert np.array_equal(to_host(dst), exp), (encrypt, call)
             assert np.array_equal(to_host(iv_d), iv_h), (encrypt, call)
             assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h), (encrypt, call)
+
+
+@pytest.mark.parametrize("encrypt", [True, False])
+def test_long_stream_segments(engine, oracle, encrypt):
+    """Few streams, segments of many 64-block chunks: every wave of a segment must see
+    the state the call started from, not the one its last-block lane writes back."""
+    rng = np.random.default_rng(77 + encrypt)
+    S, keylen = 6, 16
+    keys = rng.integers(0, 256, S * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, S * 16, dtype=np.uint8)
+    ks = keyset(engine, keys, keylen, ivs)
+    iv_h, pos_h = ivs.copy(), rng.integers(0, 16, S).astype(np.uint32)
+    iv_d, pos_d = to_dev(iv_h), to_dev(pos_h.astype(np.int32))
+    for call in range(4):
+        lens = rng.integers(100_000, 300_000, S).astype(np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1] + 1)]).astype(np.int64)
+        inp = rng.integers(0, 256, int(offs[-1] + lens[-1]), dtype=np.uint8)
+        exp = inp.copy()
+        slots = np.arange(S, dtype=np.uint32)
+        oracle.stream_batch(encrypt, inp, exp, S, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                            lens=lens.astype(np.uint32), key_slot=slots, keys=keys, keylen=keylen,
+                            iv_state=iv_h, pos_state=pos_h, threads=8)
+        for inplace in ((False, True) if call == 3 else (False,)):
+            if inplace:  # replay the last call in place from the same starting state
+                iv_d, pos_d = to_dev(iv_prev), to_dev(pos_prev.astype(np.int32))
+            else:
+                iv_prev, pos_prev = to_host(iv_d).copy(), to_host(pos_d).astype(np.uint32).copy()
+            src = to_dev(inp)
+            dst = src if inplace else to_dev(inp)
+            fn = engine.stream_encrypt if encrypt else engine.stream_decrypt
+            fn(src, dst, S, ks, iv_d, pos_d, in_off=to_dev(offs), lens=to_dev(lens),
+               key_slot=to_dev(slots.astype(np.int32)))
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (call, inplace)
+            assert np.array_equal(to_host(iv_d), iv_h) and np.array_equal(to_host(pos_d).astype(np.uint32), pos_h)
 
 
 def test_empty_and_degenerate(engine):
