@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time pinned H2D + kernels + D2H (for DESIGN.md)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL; default) or gloo (rehearsal)")
     ap.add_argument("--only", choices=["encrypt", "decrypt"], default=None,
                     help="profiling aid: run one direction only (not a bench line)")
     return ap.parse_args()
@@ -58,28 +59,21 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local % max(1, torch.cuda.device_count())  # == local on a node with one GPU per rank
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    return world, rank, local
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
+    return world, rank, dev
 
 
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-
-
-def max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
-        return x
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 def load_traffic(kernel: str):
@@ -158,6 +152,7 @@ def main():
     args = parse()
     world, rank, local = dist_setup(args)
     import fpnn_amd
+    from fpnn_amd.sharding import max_over_ranks, shard_range
 
     P, L = args.packets, args.length
     cfg = W.C2
@@ -165,8 +160,12 @@ def main():
     eng = fpnn_amd.Engine(local)  # queues on torch's current stream of this device
     ks = fpnn_amd.KeySet(eng, key, len(key), iv)
     nbytes = P * L
+    # weak scaling: the global batch is world * P packets; this rank owns a contiguous
+    # packet range of it (no collective on the data path)
+    first, last = shard_range(P * world, world, rank)
+    assert last - first == P
     plain = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    eng.fill_synthetic(plain, cfg["payload_seed"], byte_offset=rank * nbytes)  # this rank's shard
+    eng.fill_synthetic(plain, cfg["payload_seed"], byte_offset=first * L)
     cipher = torch.empty_like(plain)
     back = torch.empty_like(plain)
 
@@ -193,7 +192,7 @@ def main():
     barrier(world)
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
-    elapsed = max_over_ranks(elapsed, world)
+    elapsed = max_over_ranks(elapsed, world, "cuda" if args.dist_backend == "nccl" else None)
     n_enc, ms_enc = eng.kernel_stats(fpnn_amd.K_ENCRYPT)
     n_dec, ms_dec = eng.kernel_stats(fpnn_amd.K_DECRYPT)
 

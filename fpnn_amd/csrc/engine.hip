@@ -247,7 +247,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         HIP_TRY(launch_boundary_save(k, layout, stream, e->d_boundary, nchunks, e->stream));
         k.boundary = e->d_boundary;
     }
-    const uint64_t want = (nchunks + 15) / 16;  // 16 waves per workgroup
+    const uint64_t want = (nchunks + 63) / 64;  // 16 waves per workgroup x up to 4 chunks per wave step
     const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
     const int grid = (int)(want < cap ? (want ? want : 1) : cap);
     EventPair *ev;

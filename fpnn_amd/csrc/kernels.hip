@@ -214,7 +214,42 @@ __device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64
     }
 }
 
-template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE, int NT>
+// Everything one lane needs for one 64-block chunk; fetch_chunk() only issues the
+// loads, so the next chunk's HBM latency overlaps the current chunk's rounds.
+struct ChunkIn {
+    Seg g;
+    uint64_t s;
+    uint32_t n0, bi, slot;
+    bool valid;
+    uint4 ivs, x, xp0;  // ivs: chunk's carried/connection IV; x: C_i; xp0: lane 0's C_{i-1}
+};
+
+template <int LAYOUT, int KM, bool STREAM, bool INPLACE>
+__device__ __forceinline__ void fetch_chunk(const KBatch &b, uint64_t c, uint64_t total, uint32_t lane, ChunkIn &ci) {
+    const uint64_t nchunks = (total + 63) >> 6;
+    const uint64_t cc = c < nchunks ? c : nchunks - 1;  // steps may overhang the last chunk
+    const uint64_t gblk = (c << 6) + lane;
+    ci.valid = gblk < total;
+    locate_block<LAYOUT>(b, cc, gblk, total, ci.s, ci.bi);
+    ci.g = get_seg<LAYOUT>(b, ci.s);
+    ci.n0 = STREAM ? b.pos_snap[ci.s] : 0u;
+    ci.slot = KM == KEY_UNIFORM ? 0u : ci.g.slot;
+    ci.ivs = STREAM ? b.iv_snap[ci.s] : *reinterpret_cast<const uint4 *>(b.keys[ci.slot].iv);
+    ci.x = ci.valid ? load_cx(ci.g, ci.n0, ci.bi, ci.ivs) : make_uint4(0, 0, 0, 0);
+    ci.xp0 = make_uint4(0, 0, 0, 0);
+    if (lane == 0 && ci.bi != 0 && ci.valid)
+        ci.xp0 = INPLACE ? b.boundary[cc] : load_cx(ci.g, ci.n0, ci.bi - 1, ci.ivs);
+}
+
+__device__ __forceinline__ uint4 readlane63(const uint4 &v) {
+    return make_uint4(__builtin_amdgcn_readlane(v.x, 63), __builtin_amdgcn_readlane(v.y, 63),
+                      __builtin_amdgcn_readlane(v.z, 63), __builtin_amdgcn_readlane(v.w, 63));
+}
+
+// One wave step covers U consecutive 64-block chunks (U blocks per lane): the U loads go
+// out together, the U ciphers are independent (ILP for the LDS pipe), and a lane-0 block
+// whose predecessor sits in the previous chunk gets it from lane 63 by readlane.
+template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE, int NT, int U>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_blocks(KBatch b) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -227,48 +262,43 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
 
     const uint64_t total = b.total_blocks;
     const uint64_t nchunks = (total + 63) >> 6;
+    const uint64_t nsteps = (nchunks + U - 1) / U;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nchunks; c += nwaves) {
-        const uint64_t gblk = (c << 6) + lane;
-        const bool valid = gblk < total;
-        uint64_t s;
-        uint32_t bi;
-        locate_block<LAYOUT>(b, c, gblk, total, s, bi);
-        const Seg g = get_seg<LAYOUT>(b, s);
-        const uint32_t n0 = STREAM ? b.pos_snap[s] : 0u;
-        const uint32_t slot = KM == KEY_UNIFORM ? 0u : g.slot;
-        const DevKey *key = b.keys + slot;
-        const uint4 ivs = STREAM ? b.iv_snap[s] : *reinterpret_cast<const uint4 *>(key->iv);
-
-        const uint4 x = valid ? load_cx(g, n0, bi, ivs) : make_uint4(0, 0, 0, 0);
-        uint4 xp = wave_shr1(x);  // C_{i-1} from the neighbouring lane (all 64 lanes active here)
-        if (lane == 0 && bi != 0 && valid) xp = INPLACE ? b.boundary[c] : load_cx(g, n0, bi - 1, ivs);
-        const uint4 kin = bi == 0 ? ivs : xp;
-
-        uint4 ks;
-        if (KM == KEY_UNIFORM) {
-            ks = aes_encrypt_block<NR, NT>(kin, rku, T);
-        } else {
-            const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slot);
-            const uint32_t my = valid ? slot : slot0;
-            if (__builtin_amdgcn_ballot_w64(my != slot0) == 0) {  // wave-uniform key: SGPR round keys
-                const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + slot0);
-                ks = aes_encrypt_block<NR, NT>(kin, rk, T);
+    for (uint64_t st = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; st < nsteps; st += nwaves) {
+        ChunkIn ci[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) fetch_chunk<LAYOUT, KM, STREAM, INPLACE>(b, st * U + j, total, lane, ci[j]);
+        uint4 ks[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            uint4 xp = wave_shr1(ci[j].x);  // C_{i-1} from the neighbouring lane (all 64 lanes active)
+            if (lane == 0) xp = j == 0 ? ci[0].xp0 : readlane63(ci[j - 1].x);
+            const uint4 kin = ci[j].bi == 0 ? ci[j].ivs : xp;
+            if (KM == KEY_UNIFORM) {
+                ks[j] = aes_encrypt_block<NR, NT>(kin, rku, T);
             } else {
-                const RoundKeys<NR> rk = load_round_keys<NR>(key);
-                ks = aes_encrypt_block<NR, NT>(kin, rk, T);
+                const uint32_t slot0 = __builtin_amdgcn_readfirstlane(ci[j].slot);
+                const uint32_t my = ci[j].valid ? ci[j].slot : slot0;
+                if (__builtin_amdgcn_ballot_w64(my != slot0) == 0) {  // wave-uniform key: SGPR round keys
+                    const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + slot0);
+                    ks[j] = aes_encrypt_block<NR, NT>(kin, rk, T);
+                } else {
+                    const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + ci[j].slot);
+                    ks[j] = aes_encrypt_block<NR, NT>(kin, rk, T);
+                }
             }
+            if (STREAM && ci[j].bi == 0 && ci[j].n0 != 0) ks[j] = ci[j].ivs;  // keystream already in the state
         }
-        if (STREAM && bi == 0 && n0 != 0) ks = ivs;  // keystream block already in the carried state
-
-        if (valid) {
-            const uint4 o = x ^ ks;
-            store_cx(g, n0, bi, o);
-            if (STREAM && (uint64_t)bi + 1 == seg_blocks(g.len, n0)) {  // last block: export (ivec, pos)
-                const uint32_t pos = (n0 + g.len) & 15u;
-                const uint4 nv = pos ? select_bytes(byte_mask(0, (int)pos), x, ks) : x;
-                *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = nv;
-                b.pos_state[s] = pos;
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const ChunkIn &c = ci[j];
+            if (!c.valid) continue;
+            store_cx(c.g, c.n0, c.bi, c.x ^ ks[j]);
+            if (STREAM && (uint64_t)c.bi + 1 == seg_blocks(c.g.len, c.n0)) {  // last block: export (ivec, pos)
+                const uint32_t pos = (c.n0 + c.g.len) & 15u;
+                const uint4 nv = pos ? select_bytes(byte_mask(0, (int)pos), c.x, ks[j]) : c.x;
+                *reinterpret_cast<uint4 *>(b.iv_state + 16 * c.s) = nv;
+                b.pos_state[c.s] = pos;
             }
         }
     }
@@ -491,10 +521,14 @@ hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v,
     return hipGetLastError();
 }
 
+// 64-block chunks per wave step in K1: 4 where the extra state fits in registers
+// (package mode, one key), 1 for stream / per-packet-key variants (they would spill).
+constexpr int dec_u(bool stream, int km) { return (!stream && km == KEY_UNIFORM) ? 4 : 1; }
+
 template <int NR, bool INPLACE, int NT>
 static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
 #define FPNN_DEC(L, K, S, NTX) \
-    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX>), dim3(grid), dim3(kThreads), 0, st, b)
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K)>), dim3(grid), dim3(kThreads), 0, st, b)
     if (layout == LAYOUT_UNIFORM) {
         if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
     } else if (km == KEY_UNIFORM) {

@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Throughput of every BASELINE.json GPU config (device-resident, HIP-event timed),
+for DESIGN.md -- bench.py's single JSON line covers C2 only.
+
+  C2  1M x 1 KiB AES-256 package                    (also: PCIe-inclusive rate)
+  C3  4096 streams x 4 MiB AES-128 stream mode      (whole stream per call, and cut into
+                                                      random 1 B..64 KiB frames = one call per frame round)
+  C4  Zipf 64 B..64 KiB, 4 GiB, AES-256 package
+  C5  65536 keys x 4 KiB AES-256, per-key IV
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import workloads as W  # noqa: E402
+
+
+def timed(eng, which, fn, reps):
+    import fpnn_amd
+    fn()  # warm
+    torch.cuda.synchronize()
+    eng.reset_stats()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    eng.set_timing(False)
+    n, ms = eng.kernel_stats(which)
+    return wall / reps, ms / max(1, n) / 1e3, n // reps
+
+
+def gib(nbytes, sec):
+    return round(nbytes / sec / 2**30, 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    args = ap.parse_args()
+    import fpnn_amd
+    E, D = fpnn_amd.K_ENCRYPT, fpnn_amd.K_DECRYPT
+    eng = fpnn_amd.Engine(0)
+    out = {}
+    todo = args.configs.split(",")
+
+    if "C2" in todo:
+        c = W.C2
+        P, L = c["packets"], c["length"]
+        key, iv = W.single_key(c)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, stride=L, uniform_len=L), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, stride=L, uniform_len=L), args.reps)
+        assert torch.equal(r, a)
+        # PCIe-inclusive: pinned host -> H2D -> kernel -> D2H, per direction
+        h_in = torch.empty(P * L, dtype=torch.uint8, pin_memory=True)
+        h_out = torch.empty_like(h_in, pin_memory=True)
+        h_in.copy_(a)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            b.copy_(h_in, non_blocking=True)
+            eng.package_encrypt(b, r, P, ks, stride=L, uniform_len=L)
+            h_out.copy_(r, non_blocking=True)
+        torch.cuda.synchronize()
+        pe = (time.perf_counter() - t0) / args.reps
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            b.copy_(h_in, non_blocking=True)
+            torch.cuda.synchronize()
+        h2d = (time.perf_counter() - t0) / args.reps
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            h_out.copy_(r, non_blocking=True)
+            torch.cuda.synchronize()
+        d2h = (time.perf_counter() - t0) / args.reps
+        out["C2"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd),
+                     "encrypt_wall_GiBs": gib(P * L, we), "decrypt_wall_GiBs": gib(P * L, wd),
+                     "pcie_inclusive_encrypt_GiBs": gib(P * L, pe), "h2d_GiBs": gib(P * L, h2d),
+                     "d2h_GiBs": gib(P * L, d2h),
+                     "note": "PCIe-inclusive = pinned H2D + encrypt + D2H serialized on one stream"}
+        del a, b, r, h_in, h_out
+        print(json.dumps({"C2": out["C2"]}), flush=True)
+
+    if "C5" in todo:
+        c = W.C5
+        P, L = c["packets"], c["length"]
+        keys, ivs = W.many_keys(c)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), c["keylen"], ivs.tobytes())
+        slots = torch.arange(P, dtype=torch.int32, device="cuda")
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        kw = dict(stride=L, uniform_len=L, key_slot=slots)
+        we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, **kw), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
+        assert torch.equal(r, a)
+        t0 = time.perf_counter()
+        ks2 = fpnn_amd.KeySet(eng, keys.tobytes(), c["keylen"], ivs.tobytes())
+        kexp = time.perf_counter() - t0
+        out["C5"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd),
+                     "encrypt_wall_GiBs": gib(P * L, we), "decrypt_wall_GiBs": gib(P * L, wd),
+                     "keyset_create_65536_keys_ms": round(kexp * 1e3, 2)}
+        del a, b, r, ks2
+        print(json.dumps({"C5": out["C5"]}), flush=True)
+
+    if "C4" in todo:
+        c = W.C4
+        sizes = W.zipf_sizes(c)
+        n = len(sizes)
+        offs = np.concatenate([[0], np.cumsum(sizes[:-1].astype(np.int64))]).astype(np.int64)
+        total = int(offs[-1] + sizes[-1])
+        key, iv = W.single_key(c)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        a = torch.empty(total, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        kw = dict(in_off=torch.from_numpy(offs).cuda(), lens=torch.from_numpy(sizes.astype(np.int32)).cuda())
+        we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, n, ks, **kw), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, n, ks, **kw), args.reps)
+        assert torch.equal(r, a)
+        out["C4"] = {"packets": n, "bytes": total, "encrypt_kernel_GiBs": gib(total, ke),
+                     "decrypt_kernel_GiBs": gib(total, kd), "encrypt_wall_GiBs": gib(total, we),
+                     "decrypt_wall_GiBs": gib(total, wd)}
+        del a, b, r
+        print(json.dumps({"C4": out["C4"]}), flush=True)
+
+    if "C3" in todo:
+        c = W.C3
+        S, L = c["streams"], c["length"]
+        keys, ivs = W.many_keys(c)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), c["keylen"], ivs.tobytes())
+        a = torch.empty(S * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        slots = torch.arange(S, dtype=torch.int32, device="cuda")
+        iv0 = torch.from_numpy(ivs.copy()).cuda()
+        st_iv, st_pos = iv0.clone(), torch.zeros(S, dtype=torch.int32, device="cuda")
+
+        def whole(fn, src, dst):
+            st_iv.copy_(iv0)
+            st_pos.zero_()
+            fn(src, dst, S, ks, st_iv, st_pos, stride=L, uniform_len=L, key_slot=slots,
+               in_off=torch.arange(S, dtype=torch.int64, device="cuda") * L)
+
+        we, ke, _ = timed(eng, E, lambda: whole(eng.stream_encrypt, a, b), max(1, args.reps // 2))
+        wd, kd, _ = timed(eng, D, lambda: whole(eng.stream_decrypt, b, r), max(1, args.reps // 2))
+        assert torch.equal(r, a)
+        # framed: one call per frame round (every stream's next frame)
+        splits = [W.stream_splits(c, s) for s in range(S)]
+        nmax = max(len(x) for x in splits)
+        lens = np.zeros((nmax, S), dtype=np.int32)
+        for s_, x in enumerate(splits):
+            lens[:len(x), s_] = x
+        starts = np.cumsum(np.vstack([np.zeros((1, S), np.int64), lens[:-1]]), axis=0) + \
+            np.arange(S, dtype=np.int64)[None, :] * L
+        d_lens = [torch.from_numpy(lens[f]).cuda() for f in range(nmax)]
+        d_offs = [torch.from_numpy(starts[f]).cuda() for f in range(nmax)]
+
+        def framed(fn, src, dst):
+            st_iv.copy_(iv0)
+            st_pos.zero_()
+            for f in range(nmax):
+                fn(src, dst, S, ks, st_iv, st_pos, in_off=d_offs[f], lens=d_lens[f], key_slot=slots)
+
+        wfe, _, _ = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), 1)
+        wfd, _, _ = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), 1)
+        assert torch.equal(r, a)
+        out["C3"] = {"whole_stream_encrypt_kernel_GiBs": gib(S * L, ke),
+                     "whole_stream_decrypt_kernel_GiBs": gib(S * L, kd),
+                     "framed_calls": nmax, "framed_encrypt_wall_GiBs": gib(S * L, wfe),
+                     "framed_decrypt_wall_GiBs": gib(S * L, wfd),
+                     "note": "encrypt = 4096 serial CFB chains (one lane each, latency bound); "
+                             "decrypt parallel per block"}
+        print(json.dumps({"C3": out["C3"]}), flush=True)
+    print(json.dumps({"configs": out}))
+
+
+if __name__ == "__main__":
+    main()
