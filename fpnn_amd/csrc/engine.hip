@@ -69,6 +69,9 @@ struct fpnn_aes_engine {
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
     uint64_t cap_stage = 0;
+    // side stream for the bitsliced co-kernel
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // instrumentation
     bool timing = false;
     std::vector<EventPair> ev[2];
@@ -184,12 +187,18 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
-    const uint64_t want = (b->count + kThreads - 1) / kThreads;
-    const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
-    const int grid = (int)(want < cap ? (want ? want : 1) : cap);
+    // One lane per chain.  Workgroup size: the smallest power of two (>= one wave) that
+    // still spreads the chains over every CU -- with few chains (C3: 4096 streams) a
+    // 1024-thread workgroup would pack them onto a handful of CUs whose LDS they then
+    // saturate, while the rest of the chip idles.
+    const uint64_t slots = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
+    int threads = 64;
+    while (threads < kThreads && (uint64_t)threads * slots < b->count) threads *= 2;
+    const uint64_t want = (b->count + threads - 1) / threads;
+    const int grid = (int)(want < slots ? (want ? want : 1) : slots);
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, e->stream));
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, threads, e->stream));
     return timing_end(e, ev);
 }
 
@@ -241,6 +250,35 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.bstart = e->d_bstart;
         k.tile_first = e->d_tile;
     }
+    // Bitsliced co-kernel: the last share of a uniform, out-of-place, one-key package
+    // batch whose packets are whole 32-block groups goes to K1b on the side stream,
+    // concurrently with K1 on the main stream.
+    uint64_t bs_pkts = 0;
+    const uint64_t nb_all = ((uint64_t)b->uniform_len + 15) >> 4;
+    if (layout == LAYOUT_UNIFORM && !inplace && km == KEY_UNIFORM && e->variant.bs_frac > 0.f &&
+        (b->uniform_len & 511) == 0 && (b->stride & 15) == 0)
+        bs_pkts = (uint64_t)((double)e->variant.bs_frac * (double)b->count + 0.5);
+    if (bs_pkts > b->count) bs_pkts = b->count;
+    EventPair *ev = nullptr;
+    if (bs_pkts) {
+        if (!e->side) {
+            HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+        }
+        if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+        HIP_TRY(hipEventRecord(e->ev_fork, e->stream));
+        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+        const uint64_t first = b->count - bs_pkts;
+        HIP_TRY(launch_bs_decrypt(k, b->keys->nrounds, first, bs_pkts, (uint32_t)(nb_all / 32), e->num_cus,
+                                  e->side));
+        HIP_TRY(hipEventRecord(e->ev_join, e->side));
+        k.total_blocks = first * nb_all;  // K1 takes the leading packets
+        if (!k.total_blocks) {
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
+            return timing_end(e, ev);
+        }
+    }
     const uint64_t nchunks = (k.total_blocks + 63) >> 6;
     if (inplace) {
         if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks))) return rc;
@@ -250,9 +288,9 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     const uint64_t want = (nchunks + 63) / 64;  // 16 waves per workgroup x up to 4 chunks per wave step
     const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
     const int grid = (int)(want < cap ? (want ? want : 1) : cap);
-    EventPair *ev;
-    if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+    if (!bs_pkts && (rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
     HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, stream, inplace, grid, e->stream));
+    if (bs_pkts) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
     return timing_end(e, ev);
 }
 
@@ -321,6 +359,10 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
     if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
+    if (const char *v = getenv("FPNN_AES_BITSLICE_FRAC")) {
+        const float f = (float)atof(v);
+        e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
+    }
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;
@@ -371,6 +413,9 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
             (void)hipEventDestroy(p.beg);
             (void)hipEventDestroy(p.end);
         }
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return FPNN_AES_OK;

@@ -482,9 +482,10 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
 // use the 4-table layout (one workgroup per CU); uniform-key variants take the
 // layout the engine asks for.
 template <int NR, int NT, int CH>
-static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads,
+                       hipStream_t st) {
 #define FPNN_ENC(L, K, S, NTX) \
-    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(kThreads), 0, st, b)
+    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(threads), 0, st, b)
     if (layout == LAYOUT_UNIFORM) {
         if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
     } else if (km == KEY_UNIFORM) {
@@ -496,26 +497,26 @@ static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
 }
 
 template <int NR>
-static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid,
+static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid, int threads,
                    hipStream_t st) {
     if (v.tables == 2) {
-        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, st);
-        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, st);
+        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, threads, st);
     } else {
-        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, st);
-        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, st);
-        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, st);
+        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, threads, st);
+        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, threads, st);
     }
 }
 
 int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }
 
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool stream, int grid, hipStream_t st) {
+                                 bool stream, int grid, int threads, hipStream_t st) {
     switch (nrounds) {
-        case 10: enc_nr<10>(b, v, layout, km, stream, grid, st); break;
-        case 12: enc_nr<12>(b, v, layout, km, stream, grid, st); break;
-        case 14: enc_nr<14>(b, v, layout, km, stream, grid, st); break;
+        case 10: enc_nr<10>(b, v, layout, km, stream, grid, threads, st); break;
+        case 12: enc_nr<12>(b, v, layout, km, stream, grid, threads, st); break;
+        case 14: enc_nr<14>(b, v, layout, km, stream, grid, threads, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
