@@ -45,6 +45,12 @@ class Schedule(C.Structure):
     _fields_ = [("nrounds", C.c_int), ("rk", C.c_uint32 * 60)]
 
 
+class HostFrame(C.Structure):
+    """fpnn_aes_host_frame (include/fpnn_aes.h)."""
+
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("len", C.c_uint32), ("key_slot", C.c_uint32)]
+
+
 class BatchDesc(C.Structure):
     """fpnn_aes_batch (include/fpnn_aes.h)."""
 
@@ -90,6 +96,7 @@ SIGNATURES = {
     "fpnn_aes_stream_decrypt": (C.c_int, [_vp, C.POINTER(BatchDesc), _vp, _vp]),
     "fpnn_aes_cfb_host": (C.c_int, [_vp, C.POINTER(Schedule), C.c_int, _vp, _vp, C.c_size_t, _u8p,
                                     C.POINTER(C.c_size_t)]),
+    "fpnn_aes_package_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, C.c_uint32]),
     "fpnn_aes_fill_synthetic": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
     "fpnn_aes_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),

@@ -10,8 +10,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fpnn_aes.h"
@@ -41,6 +43,19 @@ struct EventPair {
     hipEvent_t beg, end;
 };
 
+// One slot of the host-frame pipeline (fpnn_aes_package_host): pinned + device staging
+// and its own stream, so chunk i+1's copies overlap chunk i's kernel.
+struct HostSlot {
+    uint8_t *h = nullptr, *d = nullptr;
+    uint64_t cap = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    uint32_t first = 0, count = 0;
+    uint64_t out_at = 0;  // offset of the output payload inside the slot
+    std::vector<uint64_t> out_off;
+};
+
 }  // namespace
 
 struct fpnn_aes_engine {
@@ -63,12 +78,18 @@ struct fpnn_aes_engine {
     uint64_t cap_snap_iv = 0;
     uint32_t *d_snap_pos = nullptr;
     uint64_t cap_snap_pos = 0;
+    uint32_t *d_perm = nullptr;  // ragged encrypt: longest-first order
+    uint64_t cap_perm = 0;
+    uint32_t *d_buckets = nullptr;  // 2 x 128 counters
+    uint64_t cap_buckets = 0;
     uint64_t *d_total = nullptr;
     uint64_t *h_total = nullptr;  // pinned
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
     uint64_t cap_stage = 0;
+    // host-frame pipeline
+    HostSlot hs[2];
     // side stream for the bitsliced co-kernel
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -187,6 +208,30 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
+    // Few chains (fewer than the lanes of a full chip) or ragged lengths: one quad per
+    // chain (K2c); otherwise one lane per chain with 8-block chunks (K2).
+    const uint64_t full_chip = (uint64_t)e->num_cus * kThreads;
+    const bool coop = e->variant.coop == 1 || (e->variant.coop == -1 && (b->count < full_chip || b->len != nullptr));
+    if (coop) {
+        const uint64_t lanes = 4 * b->count;
+        int threads = 64;
+        while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
+        const uint64_t want = (lanes + threads - 1) / threads;
+        const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+        if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
+            if ((rc = grow(e->d_perm, e->cap_perm, b->count))) return rc;
+            if ((rc = grow(e->d_buckets, e->cap_buckets, 256))) return rc;
+            if (stream) {  // bucket sizes read pos_state (the encrypt kernel reads it later)
+                k.pos_snap = pos_state;
+            }
+            HIP_TRY(launch_length_order(k, stream, e->d_perm, e->d_buckets, e->stream));
+            k.perm = e->d_perm;
+        }
+        EventPair *ev;
+        if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
+        HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
+        return timing_end(e, ev);
+    }
     // One lane per chain.  Workgroup size: the smallest power of two (>= one wave) that
     // still spreads the chains over every CU -- with few chains (C3: 4096 streams) a
     // 1024-thread workgroup would pack them onto a handful of CUs whose LDS they then
@@ -359,6 +404,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
     if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
+    if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_BITSLICE_FRAC")) {
         const float f = (float)atof(v);
         e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
@@ -404,6 +450,8 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_boundary);
     (void)hipFree(e->d_snap_iv);
     (void)hipFree(e->d_snap_pos);
+    (void)hipFree(e->d_perm);
+    (void)hipFree(e->d_buckets);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_total) (void)hipHostFree(e->h_total);
@@ -413,6 +461,12 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
             (void)hipEventDestroy(p.beg);
             (void)hipEventDestroy(p.end);
         }
+    for (auto &h : e->hs) {
+        if (h.h) (void)hipHostFree(h.h);
+        if (h.d) (void)hipFree(h.d);
+        if (h.done) (void)hipEventDestroy(h.done);
+        if (h.st) (void)hipStreamDestroy(h.st);
+    }
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -626,7 +680,160 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     return FPNN_AES_OK;
 }
 
+// ---- many frames from host memory -----------------------------------------------------
+
+namespace {
+
+// memcpy jobs spread over a few threads (gathering many small frames is the host cost
+// of the batch path; FPNN frames live in separate std::strings).
+struct CopyJob {
+    uint8_t *dst;
+    const uint8_t *src;
+    uint64_t n;
+};
+
+void parallel_copy(const std::vector<CopyJob> &jobs, uint64_t total) {
+    unsigned nt = (unsigned)std::min<uint64_t>(8, total / (4u << 20));
+    const unsigned hw = std::thread::hardware_concurrency();
+    if (hw && nt > hw) nt = hw;
+    if (nt <= 1 || jobs.size() < 2) {
+        for (const auto &j : jobs) memcpy(j.dst, j.src, j.n);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (unsigned t = 0; t < nt; t++)
+        ts.emplace_back([&jobs, t, nt] {
+            for (size_t i = t; i < jobs.size(); i += nt) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+        });
+    for (auto &t : ts) t.join();
+}
+
+int slot_reserve(HostSlot &s, int device, uint64_t need) {
+    if (!s.st) {
+        HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+    if (need <= s.cap) return FPNN_AES_OK;
+    uint64_t n = s.cap ? s.cap : (8u << 20);
+    while (n < need) n *= 2;
+    if (s.h) (void)hipHostFree(s.h);
+    if (s.d) (void)hipFree(s.d);
+    s.h = nullptr;
+    s.d = nullptr;
+    s.cap = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h), n, 0));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d), n));
+    s.cap = n;
+    (void)device;
+    return FPNN_AES_OK;
+}
+
+// wait for a slot's chunk and scatter its outputs to the callers' buffers
+int slot_drain(HostSlot &s, const fpnn_aes_host_frame *frames, uint32_t flags) {
+    if (!s.busy) return FPNN_AES_OK;
+    HIP_TRY(hipEventSynchronize(s.done));
+    const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
+    std::vector<CopyJob> jobs;
+    jobs.reserve(s.count);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < s.count; i++) {
+        const fpnn_aes_host_frame &f = frames[s.first + i];
+        jobs.push_back({f.dst, s.h + s.out_at + s.out_off[i], f.len + pre});
+        total += f.len + pre;
+    }
+    parallel_copy(jobs, total);
+    s.busy = false;
+    return FPNN_AES_OK;
+}
+
+}  // namespace
+
 // ---- utilities --------------------------------------------------------------------------
+
+int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                          const fpnn_aes_keyset *keys, uint32_t flags) {
+    if (!e || !keys || (n && !frames)) return FPNN_AES_ERR_ARG;
+    if (!encrypt && (flags & FPNN_AES_F_WIRE_PREFIX)) return FPNN_AES_ERR_ARG;
+    if (keys->device != e->device) return FPNN_AES_ERR_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if ((frames[i].len && (!frames[i].src || !frames[i].dst)) || frames[i].key_slot >= keys->count)
+            return FPNN_AES_ERR_ARG;
+    if (!n) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
+    const uint64_t kChunk = 32ull << 20;  // input bytes per pipeline chunk
+    hipStream_t main_stream = e->stream;
+    int rc = FPNN_AES_OK;
+    uint32_t i = 0;
+    int k = 0;
+    while (i < n && rc == FPNN_AES_OK) {
+        HostSlot &s = e->hs[k];
+        if ((rc = slot_drain(s, frames, flags))) break;
+        // chunk = frames [i, j) with at most kChunk input bytes (at least one frame)
+        uint32_t j = i;
+        uint64_t in_b = 0, out_b = 0;
+        while (j < n && (j == i || in_b + frames[j].len <= kChunk)) {
+            in_b += frames[j].len;
+            out_b += frames[j].len + pre;
+            j++;
+        }
+        const uint32_t cnt = j - i;
+        const uint64_t in_pad = (in_b + 15) & ~15ull, out_pad = (out_b + 15) & ~15ull;
+        const uint64_t arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
+        if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
+        uint8_t *h_in = s.h, *h_arr = s.h + in_pad;
+        uint64_t *in_off = reinterpret_cast<uint64_t *>(h_arr);
+        uint64_t *out_off = in_off + cnt;
+        uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
+        uint32_t *slots = lens + cnt;
+        s.out_at = in_pad + ((arr + 15) & ~15ull);
+        s.out_off.resize(cnt);
+        std::vector<CopyJob> jobs;
+        jobs.reserve(cnt);
+        uint64_t io = 0, oo = 0;
+        for (uint32_t t = 0; t < cnt; t++) {
+            const fpnn_aes_host_frame &f = frames[i + t];
+            in_off[t] = io;
+            out_off[t] = oo;
+            s.out_off[t] = oo;
+            lens[t] = f.len;
+            slots[t] = f.key_slot;
+            if (f.len) jobs.push_back({h_in + io, f.src, f.len});
+            io += f.len;
+            oo += f.len + pre;
+        }
+        parallel_copy(jobs, in_b);
+        const uint64_t up = in_pad + arr;
+        HIP_TRY(hipMemcpyAsync(s.d, s.h, up, hipMemcpyHostToDevice, s.st));
+        fpnn_aes_batch b;
+        memset(&b, 0, sizeof b);
+        b.in = s.d;
+        b.out = s.d + s.out_at;
+        b.count = cnt;
+        b.in_off = reinterpret_cast<const uint64_t *>(s.d + in_pad);
+        b.out_off = b.in_off + cnt;
+        b.len = reinterpret_cast<const uint32_t *>(b.out_off + cnt);
+        b.key_slot = keys->count > 1 ? b.len + cnt : nullptr;
+        b.keys = keys;
+        b.flags = flags;
+        e->stream = s.st;  // queue this chunk's kernels on the slot stream
+        rc = encrypt ? run_encrypt(e, &b, nullptr, nullptr, false) : run_decrypt(e, &b, nullptr, nullptr, false);
+        e->stream = main_stream;
+        if (rc) break;
+        HIP_TRY(hipMemcpyAsync(s.h + s.out_at, s.d + s.out_at, out_pad, hipMemcpyDeviceToHost, s.st));
+        HIP_TRY(hipEventRecord(s.done, s.st));
+        s.busy = true;
+        s.first = i;
+        s.count = cnt;
+        i = j;
+        k ^= 1;
+    }
+    for (auto &s : e->hs) {
+        const int r2 = slot_drain(s, frames, flags);
+        if (!rc) rc = r2;
+    }
+    return rc;
+}
 
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset) {
     if (!e || (nbytes && !dst)) return FPNN_AES_ERR_ARG;

@@ -189,6 +189,156 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 }
 
 // ---------------------------------------------------------------------------
+// K2c: encryption, one lane QUAD per chain.  Lane q of the quad owns state column q:
+// per round it fetches the other three columns from its quad neighbours with DPP
+// quad_perm (VALU only), then does the 4 T-table lookups of its output column.  A
+// chain therefore issues 4 LDS reads per round instead of 16 -- 4x the lanes per
+// chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
+// lane instead of 60.  Used when chains are few (streams) or long/ragged.
+
+template <int SHIFT>  // value held by lane (q + SHIFT) & 3 of this lane's quad
+__device__ __forceinline__ uint32_t quad_from(uint32_t v) {
+    constexpr int ctl = ((0 + SHIFT) & 3) | (((1 + SHIFT) & 3) << 2) | (((2 + SHIFT) & 3) << 4) | (((3 + SHIFT) & 3) << 6);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctl, 0xf, 0xf, false);
+}
+
+template <int NR, int NT>
+__device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32_t *rkq, const Tables4<NT> &T) {
+    uint32_t s0 = sq ^ rkq[0];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
+        s0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s1), T.template t<2>(s2)), T.template t<3>(s3), rkq[r]);
+    }
+    const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
+    return (T.template s<0>(s0) | T.template s<1>(s1) | T.template s<2>(s2) | T.template s<3>(s3)) ^ rkq[NR];
+}
+
+typedef uint32_t __attribute__((aligned(1))) uint32_u;
+
+// bytes [lo, hi) of this lane's word (word covers block bytes [4q, 4q+4))
+__device__ __forceinline__ uint32_t load_word_bytes(const uint8_t *p, int lo, int hi) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) w |= (uint32_t)p[j] << (8 * j);
+    return w;
+}
+
+__device__ __forceinline__ void store_word_bytes(uint8_t *p, uint32_t w, int lo, int hi) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) p[j] = (uint8_t)(w >> (8 * j));
+}
+
+__device__ __forceinline__ uint32_t word_mask(int lo, int hi) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) m |= (j >= lo && j < hi) ? (0xffu << (8 * j)) : 0u;
+    return m;
+}
+
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const int q = (int)(threadIdx.x & 3u);
+    constexpr int CH = 8;
+
+    const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; t < b.count; t += nquads) {
+        const uint64_t s = b.perm ? b.perm[t] : t;  // longest chains first (ragged batches)
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        uint32_t rkq[NR + 1];
+#pragma unroll
+        for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+
+        uint32_t iv;  // this lane's word of the 16-byte feedback register
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            n = b.pos_state[s];
+        } else {
+            iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
+        }
+        const uint8_t *p = g.in;
+        uint8_t *o = g.out;
+        uint32_t rem = g.len;
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
+            if (q == 0) store_word_bytes(o, rem, 0, 4);
+            o += 4;
+        }
+        const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+        if (STREAM && n != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
+            if (lo < hi) {
+                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
+                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (iv & ~m);
+            }
+            p += take;
+            o += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+        const uint32_t nfull = rem >> 4;
+        uint32_t i = 0;
+        if (nfull >= CH) {
+            uint32_t a[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo);
+            for (; i + CH <= nfull; i += CH) {
+                const bool more = i + 2 * CH <= nfull;
+                uint32_t nx[CH], c[CH];
+#pragma unroll
+                for (int j = 0; j < CH; j++) nx[j] = more ? *reinterpret_cast<const uint32_u *>(p + 16 * (CH + j) + wlo) : 0u;
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
+                    c[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
+#pragma unroll
+                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                p += 16 * CH;
+                o += 16 * CH;
+            }
+        }
+        for (; i < nfull; i++) {
+            const uint32_t pt = *reinterpret_cast<const uint32_u *>(p + wlo);
+            iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ pt;
+            *reinterpret_cast<uint32_u *>(o + wlo) = iv;
+            p += 16;
+            o += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const int lo = 0, hi = min((int)rem, wlo + 4) - wlo;
+            if (hi > lo) {
+                const uint32_t c = load_word_bytes(p + wlo, lo, hi) ^ ks;
+                store_word_bytes(o + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (ks & ~m);
+            } else {
+                iv = ks;
+            }
+            n = rem;
+        }
+        if (STREAM) {
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
+            if (q == 0) b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K1: decryption, one lane per virtual block, 64 consecutive blocks per wave step.
 
 template <int LAYOUT>
@@ -408,6 +558,86 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_map(KBatch b, const uint6
 }
 
 // ---------------------------------------------------------------------------
+// Length ordering for ragged encrypt batches: counting sort into 128 descending
+// quarter-octave buckets of the block count (order inside a bucket is arbitrary; it
+// only affects speed, never results).
+
+constexpr int kBuckets = 128;
+
+template <bool STREAM>
+__device__ __forceinline__ uint32_t length_bucket(const KBatch &b, uint64_t s) {
+    const uint64_t nb = nblocks_of<STREAM>(b, s) + 1;  // >= 1
+    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
+    const int lz = 31 - __builtin_clz(x);
+    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
+    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);  // descending length
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts) {
+    __shared__ uint32_t h[kBuckets];
+    if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[length_bucket<STREAM>(b, s)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
+    __shared__ uint32_t sh[kBuckets];
+    const int t = threadIdx.x;
+    sh[t] = counts[t];
+    __syncthreads();
+    for (int off = 1; off < kBuckets; off <<= 1) {
+        const uint32_t add = t >= off ? sh[t - off] : 0u;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    cursor[t] = sh[t] - counts[t];  // exclusive
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm, uint64_t per_wg) {
+    __shared__ uint32_t cnt[kBuckets], base[kBuckets];
+    if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * per_wg;
+    const uint64_t hi = lo + per_wg < b.count ? lo + per_wg : b.count;
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) atomicAdd(&cnt[length_bucket<STREAM>(b, s)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kBuckets) {
+        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]) : 0u;
+        cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
+        const uint32_t k = length_bucket<STREAM>(b, s);
+        perm[base[k] + atomicAdd(&cnt[k], 1u)] = (uint32_t)s;
+    }
+}
+
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st) {
+    uint32_t *cursor = counts + kBuckets;
+    hipError_t e = hipMemsetAsync(counts, 0, kBuckets * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)((b.count + 255) / 256 < 1024 ? (b.count + 255) / 256 : 1024);
+    if (stream)
+        hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
+    else
+        hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor);
+    const uint64_t per_wg = 4096;
+    const unsigned sgrid = (unsigned)((b.count + per_wg - 1) / per_wg);
+    if (stream)
+        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+    else
+        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Key expansion on the device (one lane per key; base/rijndael.c:712-799).
 
 __global__ __launch_bounds__(256) void k_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs,
@@ -507,6 +737,31 @@ static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km,
         else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, threads, st);
         else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, threads, st);
     }
+}
+
+template <int NR>
+static void coop_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads, hipStream_t st) {
+#define FPNN_COOP(L, K, S) \
+    hipLaunchKernelGGL((k_cfb_encrypt_coop<NR, L, K, S, 4>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, false);
+    }
+#undef FPNN_COOP
+}
+
+hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                               int threads, hipStream_t st) {
+    switch (nrounds) {
+        case 10: coop_nr<10>(b, layout, km, stream, grid, threads, st); break;
+        case 12: coop_nr<12>(b, layout, km, stream, grid, threads, st); break;
+        case 14: coop_nr<14>(b, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }

@@ -40,6 +40,8 @@ struct KBatch {
     // be reading the old one, so every read goes to this snapshot.
     const uint4 *iv_snap;
     const uint32_t *pos_snap;
+    // encrypt of ragged batches: segment visiting order (longest first), or null
+    const uint32_t *perm;
 };
 
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1 };
@@ -50,7 +52,8 @@ enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 struct Variant {
     float bs_frac = 0.0f;  // share of uniform package-decrypt packets given to the bitsliced K1b
     int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
-    int enc_chunk = 8;  // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
+    int enc_chunk = 8;
+    int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c  // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
@@ -58,6 +61,12 @@ int blocks_per_cu(const Variant &v, KeyMode km);
 // CUs with small workgroups instead of packed into a few full ones.
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
                                  bool stream, int grid, int threads, hipStream_t st);
+// K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
+hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                               int threads, hipStream_t st);
+// Ragged batches: perm[] = segment indices ordered by block count, longest first
+// (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
                                  bool stream, bool inplace, int grid, hipStream_t st);
 // Bitsliced K1b over packets [first_pkt, first_pkt + npkt) of a uniform package batch

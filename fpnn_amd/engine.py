@@ -21,7 +21,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import (BatchDesc, FpnnAesError, Schedule, check, lib, F_WIRE_PREFIX, K_DECRYPT, K_ENCRYPT,
+from ._lib import (BatchDesc, FpnnAesError, HostFrame, Schedule, check, lib, F_WIRE_PREFIX, K_DECRYPT, K_ENCRYPT,
                    ERR_KEYLEN, OK)
 
 
@@ -41,6 +41,14 @@ def _release_all():
         ks.close()
     for e in list(_live_engines):
         e.close()
+
+
+# numpy mirror of fpnn_aes_host_frame for building large frame lists without a Python loop
+import numpy as _np  # noqa: E402
+
+HOST_FRAME_DTYPE = _np.dtype([("src", _np.uint64), ("dst", _np.uint64), ("len", _np.uint32),
+                              ("key_slot", _np.uint32)])
+assert HOST_FRAME_DTYPE.itemsize == C.sizeof(HostFrame)
 
 
 def setup_encrypt(key: bytes) -> Schedule:
@@ -129,6 +137,25 @@ class Engine:
         check(lib.fpnn_aes_cfb_host(self._h, C.byref(ctx), int(encrypt), C.c_char_p(data), out, len(data), iv,
                                     C.byref(n)), "cfb_host")
         return out.raw[: len(data)], bytes(iv), n.value
+
+    # -- many frames in host memory (the cross-connection batch path) ----------------------
+    def package_host(self, encrypt: bool, frames, keys: "KeySet", wire_prefix: bool = False):
+        """frames: sequence of (src, dst, key_slot) with src/dst contiguous uint8 numpy
+        arrays in host memory (dst may be src; with wire_prefix dst holds len + 4)."""
+        arr = (HostFrame * max(1, len(frames)))()
+        for i, (src, dst, slot) in enumerate(frames):
+            arr[i].src = src.ctypes.data if src.size else None
+            arr[i].dst = dst.ctypes.data if dst.size else None
+            arr[i].len = src.size
+            arr[i].key_slot = slot
+        check(lib.fpnn_aes_package_host(self._h, int(encrypt), arr, len(frames), keys.handle,
+                                        F_WIRE_PREFIX if wire_prefix else 0), "package_host")
+
+    def package_host_array(self, encrypt: bool, frames_np, keys: "KeySet", wire_prefix: bool = False):
+        """frames_np: numpy structured array with HOST_FRAME_DTYPE (vectorized form)."""
+        ptr = C.cast(C.c_void_p(frames_np.ctypes.data), C.POINTER(HostFrame))
+        check(lib.fpnn_aes_package_host(self._h, int(encrypt), ptr, len(frames_np), keys.handle,
+                                        F_WIRE_PREFIX if wire_prefix else 0), "package_host")
 
     # -- batches ----------------------------------------------------------------------------
     def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,

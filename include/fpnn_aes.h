@@ -139,6 +139,24 @@ int fpnn_aes_stream_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t
 int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt,
                       const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num);
 
+/* ---- many frames from host memory (the cross-connection batch path, §8f row 1) ------- */
+/* One entry per frame.  src/dst are host pointers (dst may equal src for in-place;
+ * with FPNN_AES_F_WIRE_PREFIX, dst receives htole32(len) || ciphertext and must hold
+ * len + 4 bytes and not overlap src).  key_slot indexes `keys`. */
+typedef struct {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t len;
+    uint32_t key_slot;
+} fpnn_aes_host_frame;
+
+/* Package-mode encrypt (encrypt != 0) or decrypt of n host frames: the frames are
+ * gathered into pinned staging by a few host threads, and chunks are pipelined
+ * (H2D of chunk i+1 || kernel of chunk i || D2H of chunk i-1) over the engine's
+ * streams.  Results equal n PackageEncryptor calls.  Synchronous. */
+int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                          const fpnn_aes_keyset *keys, uint32_t flags);
+
 /* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
 /* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed,

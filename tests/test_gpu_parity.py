@@ -468,3 +468,36 @@ def test_cpp_dropin_matches_reference(golden, tmp_path):
     assert res.returncode == 0, res.stderr
     got = res.stdout.strip().split("\n")
     assert got == expect
+
+
+# --------------------------------------------------------------------------------------
+# many frames straight from host memory (fpnn_aes_package_host: gather -> pinned ->
+# pipelined H2D / kernel / D2H -> scatter)
+
+
+@pytest.mark.parametrize("wire_prefix", [False, True])
+def test_package_host_frames(engine, oracle, wire_prefix):
+    import fpnn_amd
+    rng = np.random.default_rng(4242 + wire_prefix)
+    nkeys, keylen = 5, 32
+    keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+    lens = list(rng.integers(0, 5000, 3000)) + [0, 1, 16, 17, 40 << 20]  # one frame > a pipeline chunk
+    frames, srcs = [], []
+    for i, L in enumerate(lens):
+        src = rng.integers(0, 256, int(L), dtype=np.uint8)
+        dst = np.zeros(int(L) + (4 if wire_prefix else 0), dtype=np.uint8)
+        frames.append((src, dst, i % nkeys))
+        srcs.append(src)
+    engine.package_host(True, frames, ks, wire_prefix=wire_prefix)
+    for src, dst, slot in frames[:400] + frames[-5:]:
+        k = keys[slot * keylen:(slot + 1) * keylen].tobytes()
+        v = ivs[slot * 16:(slot + 1) * 16].tobytes()
+        exp = oracle.package_frame(k, v, src.tobytes()) if wire_prefix else oracle.package(k, v, True, src.tobytes())
+        assert dst.tobytes() == exp
+    if not wire_prefix:  # decrypt back, in place
+        back = [(d.copy(), None, sl) for _, d, sl in frames]
+        engine.package_host(False, [(c, c, sl) for c, _, sl in back], ks)
+        for (c, _, _), src in zip(back, srcs):
+            assert np.array_equal(c, src)
