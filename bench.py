@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=W.C2["packets"])
     ap.add_argument("--length", type=int, default=W.C2["length"])
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5,
+                    help="target wall time of the multi-thread CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time pinned H2D + kernels + D2H (for DESIGN.md)")
@@ -93,22 +94,33 @@ def cpu_baseline(plain_host: np.ndarray, P: int, L: int, key: bytes, iv: bytes, 
     kind = "reference" if ref_available() else "port"
     o = Oracle(kind)
     threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate on a small sample, then size the sample to ~target_s of wall time
+    # calibrate on a small sample, then size the sample (packets x repetitions) to
+    # ~target_s of wall time on `threads` threads (target_s * threads s of CPU work)
     n = min(P, 8192)
     tmp = np.empty(n * L, np.uint8)
     out = np.empty(n * L, np.uint8)
     t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, 1)
-    n = int(min(P, max(n, n * target_s / max(t, 1e-6))))
+    want = n * target_s / max(t, 1e-6)
+    n = int(min(P, max(n, want)))
+    reps = max(1, int(round(want / n)))
     tmp = np.empty(n * L, np.uint8)
     out = np.empty(n * L, np.uint8)
-    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, 1)
+    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, reps)
     ok = bool(np.array_equal(tmp, gpu_cipher[:n * L])) and bool(np.array_equal(out, plain_host[:n * L]))
-    gib = 2.0 * n * L / t / 2**30
+    gib = 2.0 * n * L * reps / t / 2**30
+    # one core, as SURVEY.md 8(d) asks for both: ~1 s on a prefix of the same batch
+    n1 = min(n, 16384)
+    t1 = o.time_package_roundtrip(plain_host[:n1 * L], tmp[:n1 * L], out[:n1 * L], n1, L, key, iv, 1, 1)
+    n1 = int(min(n, max(n1, n1 * 1.0 / max(t1, 1e-6))))
+    t1 = o.time_package_roundtrip(plain_host[:n1 * L], tmp[:n1 * L], out[:n1 * L], n1, L, key, iv, 1, 1)
     src = "oracle/_ref: reference base/rijndael.c + core/Encryptor.cpp (-O2)" if kind == "reference" \
         else "oracle/aes_oracle.c restatement (-O2)"
     return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} x {L} B packets (first {n} of the C2 batch), PackageEncryptor::encrypt then "
-                      f"::decrypt per packet, {threads} threads; {src}; {t:.2f} s wall; matches GPU output: {ok}",
+            "sample": f"{n} x {L} B packets (first {n} of the C2 batch) x {reps} passes, "
+                      f"PackageEncryptor::encrypt then ::decrypt per packet, {threads} threads; {src}; "
+                      f"{t:.2f} s wall = {t * threads:.1f} s of CPU work; matches GPU output: {ok}",
+            "single_core": {"value": round(2.0 * n1 * L / t1 / 2**30, 4), "cores": 1,
+                            "sample": f"first {n1} packets, {t1:.2f} s"},
             "cpu_model": _cpu_model()}
 
 

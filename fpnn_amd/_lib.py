@@ -97,6 +97,7 @@ SIGNATURES = {
     "fpnn_aes_cfb_host": (C.c_int, [_vp, C.POINTER(Schedule), C.c_int, _vp, _vp, C.c_size_t, _u8p,
                                     C.POINTER(C.c_size_t)]),
     "fpnn_aes_package_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, C.c_uint32]),
+    "fpnn_aes_stream_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, _vp, _vp]),
     "fpnn_aes_fill_synthetic": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
     "fpnn_aes_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),

@@ -11,6 +11,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -43,17 +47,114 @@ struct EventPair {
     hipEvent_t beg, end;
 };
 
-// One slot of the host-frame pipeline (fpnn_aes_package_host): pinned + device staging
-// and its own stream, so chunk i+1's copies overlap chunk i's kernel.
+// memcpy job of the host-frame gather/scatter
+struct CopyJob {
+    uint8_t *dst;
+    const uint8_t *src;
+    uint64_t n;
+};
+
+// One slot of the host-frame pipeline (fpnn_aes_package_host / fpnn_aes_stream_host):
+// pinned + device staging and its own stream, so the copies of one chunk overlap the
+// kernel of the other.
 struct HostSlot {
     uint8_t *h = nullptr, *d = nullptr;
     uint64_t cap = 0;
     hipStream_t st = nullptr;
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;   // chunk's D2H finished
+    hipEvent_t kdone = nullptr;  // chunk's kernel finished (stream mode chains chunks on it)
     bool busy = false;
+    std::vector<CopyJob> scatter;  // staged output -> callers' buffers, run after `done`
+    uint64_t scatter_bytes = 0;
+    // package chunks scatter whole frames [first, first + count) straight from the staged
+    // out_off array instead (no per-frame job list)
+    const fpnn_aes_host_frame *frames = nullptr;
     uint32_t first = 0, count = 0;
-    uint64_t out_at = 0;  // offset of the output payload inside the slot
-    std::vector<uint64_t> out_off;
+    uint64_t pre = 0, out_at = 0;
+    const uint64_t *out_off = nullptr;  // pinned, inside h
+};
+
+// Persistent host workers for the host-frame path.  Gathering 1M separate 1 KiB frames
+// into pinned staging (and scattering the results back) is the host-memory-bound part
+// of fpnn_aes_package_host; threads are kept across calls so a chunk does not pay
+// thread start-up.  run(k, fn) calls fn(0..k-1) across the caller and k-1 workers.
+class HostPool {
+public:
+    explicit HostPool(unsigned workers) {
+        for (unsigned t = 0; t < workers; t++) th_.emplace_back([this, t] { loop(t + 1); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    unsigned parts() const { return (unsigned)th_.size() + 1; }
+
+    template <class F>
+    void run(unsigned want, const F &fn) {
+        want = std::max(1u, std::min(want, parts()));
+        if (want == 1) {
+            fn(0u);
+            return;
+        }
+        const std::function<void(unsigned)> f(fn);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &f;
+            active_ = want;
+            pending_ = want - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+    // memcpy jobs split into contiguous, byte-balanced ranges
+    void copy(const std::vector<CopyJob> &jobs, uint64_t total, unsigned want) {
+        want = std::max(1u, std::min<unsigned>(want, (unsigned)std::min<size_t>(jobs.size(), parts())));
+        std::vector<size_t> cut(want + 1, jobs.size());
+        cut[0] = 0;
+        uint64_t acc = 0;
+        unsigned p = 1;
+        for (size_t i = 0; i < jobs.size() && p < want; i++) {
+            acc += jobs[i].n;
+            while (p < want && acc >= total * p / want) cut[p++] = i + 1;
+        }
+        run(want, [&](unsigned q) {
+            for (size_t i = cut[q]; i < cut[q + 1]; i++) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+        });
+    }
+
+private:
+    void loop(unsigned me) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            if (me >= active_) continue;
+            const std::function<void(unsigned)> *f = fn_;
+            lk.unlock();
+            (*f)(me);
+            lk.lock();
+            if (--pending_ == 0) done_cv_.notify_one();
+        }
+    }
+
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(unsigned)> *fn_ = nullptr;
+    unsigned active_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
 };
 
 }  // namespace
@@ -90,6 +191,7 @@ struct fpnn_aes_engine {
     uint64_t cap_stage = 0;
     // host-frame pipeline
     HostSlot hs[2];
+    std::unique_ptr<HostPool> pool;  // created on first use
     // side stream for the bitsliced co-kernel
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -247,7 +349,12 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     return timing_end(e, ev);
 }
 
-int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
+// total_hint: the batch's total 16-byte block count when the caller knows it on the host
+// (the host-frame paths), which saves the general layout's device->host round trip.
+constexpr uint64_t kNoHint = ~0ull;
+
+int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream,
+                uint64_t total_hint = kNoHint) {
     int rc = check_batch(e, b);
     if (rc) return rc;
     if (stream && b->count && (!iv_state || !pos_state || ((uintptr_t)iv_state & 15))) return FPNN_AES_ERR_ARG;
@@ -284,9 +391,12 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if ((rc = grow(e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
         if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
         HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
-        HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-        HIP_TRY(hipStreamSynchronize(e->stream));
-        const uint64_t total = *e->h_total;
+        uint64_t total = total_hint;
+        if (total == kNoHint) {
+            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+            HIP_TRY(hipStreamSynchronize(e->stream));
+            total = *e->h_total;
+        }
         if (!total) return FPNN_AES_OK;
         const uint64_t nchunks = (total + 63) >> 6;
         if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
@@ -465,6 +575,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         if (h.h) (void)hipHostFree(h.h);
         if (h.d) (void)hipFree(h.d);
         if (h.done) (void)hipEventDestroy(h.done);
+        if (h.kdone) (void)hipEventDestroy(h.kdone);
         if (h.st) (void)hipStreamDestroy(h.st);
     }
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
@@ -684,34 +795,34 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
 
 namespace {
 
-// memcpy jobs spread over a few threads (gathering many small frames is the host cost
-// of the batch path; FPNN frames live in separate std::strings).
-struct CopyJob {
-    uint8_t *dst;
-    const uint8_t *src;
-    uint64_t n;
-};
+// Host threads for gathering/scattering frames: FPNN_AES_HOST_THREADS, default
+// min(16, hardware threads) -- the GPU box grants a 16-CPU share per GPU.
+unsigned host_threads() {
+    unsigned hw = std::thread::hardware_concurrency();
+    unsigned n = std::min(16u, hw ? hw : 1u);
+    if (const char *v = getenv("FPNN_AES_HOST_THREADS")) n = (unsigned)std::max(1, atoi(v));
+    return std::min(n, 64u);  // package chunks keep per-part sums in a 64-entry array
+}
 
-void parallel_copy(const std::vector<CopyJob> &jobs, uint64_t total) {
-    unsigned nt = (unsigned)std::min<uint64_t>(8, total / (4u << 20));
-    const unsigned hw = std::thread::hardware_concurrency();
-    if (hw && nt > hw) nt = hw;
-    if (nt <= 1 || jobs.size() < 2) {
-        for (const auto &j : jobs) memcpy(j.dst, j.src, j.n);
-        return;
-    }
-    std::vector<std::thread> ts;
-    for (unsigned t = 0; t < nt; t++)
-        ts.emplace_back([&jobs, t, nt] {
-            for (size_t i = t; i < jobs.size(); i += nt) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
-        });
-    for (auto &t : ts) t.join();
+HostPool *pool_of(fpnn_aes_engine *e) {
+    if (!e->pool) e->pool.reset(new HostPool(host_threads() - 1));
+    return e->pool.get();
+}
+
+// parts for `bytes` of copying: about 1 MiB per thread at least
+unsigned copy_parts(fpnn_aes_engine *e, uint64_t bytes) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pool_of(e)->parts(), bytes >> 20));
+}
+
+void parallel_copy(fpnn_aes_engine *e, const std::vector<CopyJob> &jobs, uint64_t total) {
+    pool_of(e)->copy(jobs, total, copy_parts(e, total));
 }
 
 int slot_reserve(HostSlot &s, int device, uint64_t need) {
     if (!s.st) {
         HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming));
     }
     if (need <= s.cap) return FPNN_AES_OK;
     uint64_t n = s.cap ? s.cap : (8u << 20);
@@ -728,21 +839,39 @@ int slot_reserve(HostSlot &s, int device, uint64_t need) {
     return FPNN_AES_OK;
 }
 
-// wait for a slot's chunk and scatter its outputs to the callers' buffers
-int slot_drain(HostSlot &s, const fpnn_aes_host_frame *frames, uint32_t flags) {
-    if (!s.busy) return FPNN_AES_OK;
-    HIP_TRY(hipEventSynchronize(s.done));
-    const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
-    std::vector<CopyJob> jobs;
-    jobs.reserve(s.count);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < s.count; i++) {
-        const fpnn_aes_host_frame &f = frames[s.first + i];
-        jobs.push_back({f.dst, s.h + s.out_at + s.out_off[i], f.len + pre});
-        total += f.len + pre;
+// FPNN_AES_HOST_STATS=1: per-call breakdown of the host-frame pipeline on stderr
+struct HostStats {
+    bool on = getenv("FPNN_AES_HOST_STATS") != nullptr;
+    double gather = 0, scatter = 0, wait = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     }
-    parallel_copy(jobs, total);
+};
+
+// wait for a slot's chunk and scatter its outputs to the callers' buffers
+int slot_drain(fpnn_aes_engine *e, HostSlot &s, HostStats &st) {
+    if (!s.busy) return FPNN_AES_OK;
     s.busy = false;
+    const double t0 = st.on ? HostStats::now() : 0;
+    HIP_TRY(hipEventSynchronize(s.done));
+    const double t1 = st.on ? HostStats::now() : 0;
+    if (s.frames) {
+        const unsigned parts = copy_parts(e, s.scatter_bytes);
+        pool_of(e)->run(parts, [&](unsigned p) {
+            const uint32_t a = (uint32_t)((uint64_t)s.count * p / parts), b = (uint32_t)((uint64_t)s.count * (p + 1) / parts);
+            for (uint32_t t = a; t < b; t++) {
+                const fpnn_aes_host_frame &f = s.frames[s.first + t];
+                if (f.len + s.pre) memcpy(f.dst, s.h + s.out_at + s.out_off[t], f.len + s.pre);
+            }
+        });
+        s.frames = nullptr;
+    } else {
+        parallel_copy(e, s.scatter, s.scatter_bytes);
+    }
+    if (st.on) {
+        st.wait += t1 - t0;
+        st.scatter += HostStats::now() - t1;
+    }
     return FPNN_AES_OK;
 }
 
@@ -750,89 +879,334 @@ int slot_drain(HostSlot &s, const fpnn_aes_host_frame *frames, uint32_t flags) {
 
 // ---- utilities --------------------------------------------------------------------------
 
-int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
-                          const fpnn_aes_keyset *keys, uint32_t flags) {
+namespace {
+
+// A contiguous part of one frame's bytes, in staging order.
+struct Piece {
+    uint32_t frame, off, len;
+};
+
+// Host-frame pipeline shared by the package and stream entry points.
+//   package: one segment per frame (key slot frames[i].key_slot, fresh chain).
+//   stream : one segment per distinct stream slot = the concatenation of that
+//            stream's frames in array order (CFB over a concatenation equals the
+//            successive calls, base/rijndael.c:1171-1201 carries ivec/num), whose
+//            state lives in iv_state/pos_state[slot] on the host.
+// Chunks of <= kChunk input bytes are gathered into pinned staging by the copy pool,
+// then H2D, kernel, D2H run on the slot's stream while the host gathers the next chunk.
+// In stream mode a stream may be split across chunks; the chunks' kernels are then
+// chained with events so each continues from the state the previous one left.
+int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_host_frame *frames, uint32_t n,
+                  const fpnn_aes_keyset *keys, uint32_t flags, uint8_t *iv_state, uint32_t *pos_state) {
+    const uint64_t pre = (!stream && (flags & FPNN_AES_F_WIRE_PREFIX)) ? 4 : 0;
+    const uint64_t kChunk = 32ull << 20;  // input bytes per pipeline chunk
+    // ---- segments in staging order -------------------------------------------------
+    std::vector<uint32_t> order;  // frame indices
+    struct Seg {
+        uint32_t slot, first, nframes;  // frames order[first .. first+nframes)
+        uint64_t bytes;
+    };
+    std::vector<Seg> segs;  // stream mode only (package chunks walk `frames` directly)
+    if (stream) {
+        // stable counting sort by stream slot (slots are < keys->count)
+        std::vector<uint32_t> cnt;
+        const bool dense = (uint64_t)keys->count <= 4ull * n + 1024;
+        order.resize(n);
+        if (dense) {
+            cnt.assign((size_t)keys->count + 1, 0);
+            for (uint32_t i = 0; i < n; i++) cnt[frames[i].key_slot + 1]++;
+            for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
+            for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
+        } else {
+            for (uint32_t i = 0; i < n; i++) order[i] = i;
+            std::stable_sort(order.begin(), order.end(),
+                             [frames](uint32_t x, uint32_t y) { return frames[x].key_slot < frames[y].key_slot; });
+        }
+        for (uint32_t i = 0; i < n;) {
+            const uint32_t slot = frames[order[i]].key_slot;
+            uint32_t j = i;
+            uint64_t bytes = 0;
+            while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
+            if (bytes) segs.push_back({slot, i, j - i, bytes});  // empty streams keep their state
+            i = j;
+        }
+    }
+    if (stream && segs.empty()) return FPNN_AES_OK;
+    const uint64_t nseg = stream ? segs.size() : n;
+    HostStats hst;
+    const double t_call = hst.on ? HostStats::now() : 0;
+    uint64_t nchunks = 0;
+    DeviceGuard g(e->device);
+    hipStream_t main_stream = e->stream;
+    // order the slot streams after work already queued on the engine stream
+    for (auto &sl : e->hs)
+        if (int rc = slot_reserve(sl, e->device, 0)) return rc;
+    HIP_TRY(hipEventRecord(e->hs[0].kdone, main_stream));
+    for (auto &sl : e->hs) HIP_TRY(hipStreamWaitEvent(sl.st, e->hs[0].kdone, 0));
+    // ---- stream state: compact (iv, pos) of the touched streams on the device ----------
+    uint8_t *d_state = nullptr, *h_state = nullptr;
+    // stream round-robin cursors: bytes left, frame cursor, host model of pos (for the
+    // decrypt block count) per segment
+    struct {
+        std::vector<uint64_t> rem;
+        std::vector<uint32_t> fi, fo, pos;
+        uint64_t left = 0, next = 0, chunk = 0, quota = 0;
+    } sr;
+    if (stream) {
+        const uint64_t bytes = nseg * 20;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_state), bytes, 0));
+        if (hipMalloc(reinterpret_cast<void **>(&d_state), bytes) != hipSuccess) {
+            (void)hipHostFree(h_state);
+            return hip_fail(hipErrorOutOfMemory, "hipMalloc(stream state)");
+        }
+        sr.rem.resize(nseg);
+        sr.fi.assign(nseg, 0);
+        sr.fo.assign(nseg, 0);
+        sr.pos.resize(nseg);
+        uint32_t *hp = reinterpret_cast<uint32_t *>(h_state + 16 * nseg);
+        for (uint64_t t = 0; t < nseg; t++) {
+            memcpy(h_state + 16 * t, iv_state + 16ull * segs[t].slot, 16);
+            hp[t] = sr.pos[t] = pos_state[segs[t].slot] & 15u;
+            sr.rem[t] = segs[t].bytes;
+            sr.left += segs[t].bytes;
+        }
+        // bigger chunks for few long streams (more chain steps per launch), quota per
+        // stream so one chunk spans as many streams as it can
+        sr.chunk = std::min<uint64_t>(256ull << 20, std::max<uint64_t>(kChunk, sr.left / 4));
+        sr.quota = std::max<uint64_t>(16u << 10, (sr.chunk / nseg + 15) & ~15ull);
+        (void)hipMemcpyAsync(d_state, h_state, bytes, hipMemcpyHostToDevice, e->hs[0].st);
+    }
+    int rc = FPNN_AES_OK;
+    uint64_t si = 0;  // package: next segment; stream: nseg once every byte is queued
+    int k = 0;
+    HostSlot *prev = nullptr;
+    std::vector<Piece> pieces;
+    std::vector<CopyJob> gather;
+    while (si < nseg && rc == FPNN_AES_OK) {
+        HostSlot &s = e->hs[k];
+        if ((rc = slot_drain(e, s, hst))) break;
+        // ---- choose this chunk's segments / pieces ----
+        pieces.clear();
+        struct CSeg {
+            uint32_t slot;
+            uint64_t at, len;
+            uint32_t pos;
+        };
+        std::vector<CSeg> cs;
+        uint64_t state0 = si;  // stream: state index of the chunk's first segment
+        uint64_t in_b = 0;
+        uint32_t cnt = 0;
+        uint64_t out_b = 0, total_blocks = 0, in_pad = 0, out_pad = 0, arr = 0, out_at = 0;
+        if (!stream) {
+            // whole frames [si, j) with <= kChunk input bytes (at least one frame)
+            uint64_t j = si;
+            while (j < n && (j == si || in_b + frames[j].len <= kChunk)) in_b += frames[j++].len;
+            cnt = (uint32_t)(j - si);
+            out_b = in_b + pre * cnt;
+            in_pad = (in_b + 15) & ~15ull;
+            out_pad = (out_b + 15) & ~15ull;
+            arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
+            out_at = in_pad + ((arr + 15) & ~15ull);
+            if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
+            uint64_t *in_off = reinterpret_cast<uint64_t *>(s.h + in_pad);
+            uint64_t *out_off = in_off + cnt;
+            uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
+            uint32_t *slots = lens + cnt;
+            // frame-parallel: per-part byte sums, then offsets + arrays + gather per part
+            const unsigned parts = copy_parts(e, in_b);
+            uint64_t psum[64 + 1] = {0}, pblk[64] = {0};
+            const fpnn_aes_host_frame *fr = frames + si;
+            auto range = [&](unsigned p, uint32_t &a, uint32_t &b) {
+                a = (uint32_t)((uint64_t)cnt * p / parts);
+                b = (uint32_t)((uint64_t)cnt * (p + 1) / parts);
+            };
+            const double tg = hst.on ? HostStats::now() : 0;
+            pool_of(e)->run(parts, [&](unsigned p) {
+                uint32_t a, b;
+                range(p, a, b);
+                uint64_t sum = 0, blk = 0;
+                for (uint32_t t = a; t < b; t++) {
+                    sum += fr[t].len;
+                    blk += (fr[t].len + 15ull) >> 4;
+                }
+                psum[p + 1] = sum;
+                pblk[p] = blk;
+            });
+            for (unsigned p = 0; p < parts; p++) {
+                psum[p + 1] += psum[p];
+                total_blocks += pblk[p];
+            }
+            uint8_t *h_in = s.h;
+            pool_of(e)->run(parts, [&](unsigned p) {
+                uint32_t a, b;
+                range(p, a, b);
+                uint64_t io = psum[p], oo = psum[p] + pre * a;
+                for (uint32_t t = a; t < b; t++) {
+                    const fpnn_aes_host_frame &f = fr[t];
+                    in_off[t] = io;
+                    out_off[t] = oo;
+                    lens[t] = f.len;
+                    slots[t] = f.key_slot;
+                    if (f.len) memcpy(h_in + io, f.src, f.len);
+                    io += f.len;
+                    oo += f.len + pre;
+                }
+            });
+            if (hst.on) hst.gather += HostStats::now() - tg;
+            s.frames = frames;
+            s.first = (uint32_t)si;
+            s.count = cnt;
+            s.pre = pre;
+            s.out_at = out_at;
+            s.out_off = out_off;
+            s.scatter_bytes = out_b;
+            si = j;
+        } else {
+            // Round robin: each chunk takes up to `quota` bytes from each of a run of
+            // consecutive streams, so every kernel advances many CFB chains at once (the
+            // encrypt chain is serial: parallelism = streams per kernel).
+            uint64_t t = sr.next < nseg ? sr.next : 0;
+            while (sr.rem[t] == 0) t = t + 1 < nseg ? t + 1 : 0;  // left_total > 0: terminates
+            state0 = t;
+            for (; t < nseg && in_b < sr.chunk; t++) {
+                const Seg &sg = segs[t];
+                const uint64_t take = std::min(sr.rem[t], sr.quota);
+                uint64_t took = 0;
+                while (took < take) {
+                    const fpnn_aes_host_frame &f = frames[order[sg.first + sr.fi[t]]];
+                    const uint32_t part = (uint32_t)std::min<uint64_t>(f.len - sr.fo[t], take - took);
+                    if (part) pieces.push_back({order[sg.first + sr.fi[t]], sr.fo[t], part});
+                    took += part;
+                    sr.fo[t] += part;
+                    if (sr.fo[t] == f.len) {
+                        sr.fi[t]++;
+                        sr.fo[t] = 0;
+                    }
+                }
+                cs.push_back({sg.slot, in_b, take, sr.pos[t]});
+                sr.pos[t] = (uint32_t)((sr.pos[t] + take) & 15u);
+                sr.rem[t] -= take;
+                sr.left -= take;
+                in_b += take;
+            }
+            sr.next = t;
+            if (sr.left == 0) si = nseg;
+            // stream chunk: arrays and gather/scatter jobs from the pieces
+            cnt = (uint32_t)cs.size();
+            out_b = in_b;
+            in_pad = (in_b + 15) & ~15ull;
+            out_pad = in_pad;
+            arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
+            out_at = in_pad + ((arr + 15) & ~15ull);
+            if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
+            uint64_t *in_off = reinterpret_cast<uint64_t *>(s.h + in_pad);
+            uint64_t *out_off = in_off + cnt;
+            uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
+            uint32_t *slots = lens + cnt;
+            for (uint32_t t = 0; t < cnt; t++) {
+                in_off[t] = out_off[t] = cs[t].at;
+                lens[t] = (uint32_t)cs[t].len;
+                slots[t] = cs[t].slot;
+                total_blocks += cs[t].len ? (cs[t].pos + cs[t].len + 15) >> 4 : 0;
+            }
+            gather.clear();
+            s.scatter.clear();
+            s.scatter_bytes = in_b;
+            uint64_t at = 0;
+            for (const Piece &pc : pieces) {
+                const fpnn_aes_host_frame &f = frames[pc.frame];
+                gather.push_back({s.h + at, f.src + pc.off, pc.len});
+                s.scatter.push_back({f.dst + pc.off, s.h + out_at + at, pc.len});
+                at += pc.len;
+            }
+            const double tg = hst.on ? HostStats::now() : 0;
+            parallel_copy(e, gather, in_b);
+            if (hst.on) hst.gather += HostStats::now() - tg;
+        }
+        nchunks++;
+        HIP_TRY(hipMemcpyAsync(s.d, s.h, in_pad + arr, hipMemcpyHostToDevice, s.st));
+        if (stream && prev) HIP_TRY(hipStreamWaitEvent(s.st, prev->kdone, 0));
+        fpnn_aes_batch b;
+        memset(&b, 0, sizeof b);
+        b.in = s.d;
+        b.out = s.d + out_at;
+        b.count = cnt;
+        b.in_off = reinterpret_cast<const uint64_t *>(s.d + in_pad);
+        b.out_off = pre ? b.in_off + cnt : nullptr;
+        b.len = reinterpret_cast<const uint32_t *>(s.d + in_pad + 16ull * cnt);
+        b.key_slot = keys->count > 1 ? b.len + cnt : nullptr;
+        b.keys = keys;
+        b.flags = pre ? FPNN_AES_F_WIRE_PREFIX : 0;
+        uint8_t *ivp = stream ? d_state + 16 * state0 : nullptr;
+        uint32_t *posp = stream ? reinterpret_cast<uint32_t *>(d_state + 16 * nseg) + state0 : nullptr;
+        e->stream = s.st;  // queue this chunk's kernels on the slot stream
+        rc = encrypt ? run_encrypt(e, &b, ivp, posp, stream) : run_decrypt(e, &b, ivp, posp, stream, total_blocks);
+        e->stream = main_stream;
+        if (rc) break;
+        HIP_TRY(hipEventRecord(s.kdone, s.st));
+        HIP_TRY(hipMemcpyAsync(s.h + out_at, s.d + out_at, out_pad, hipMemcpyDeviceToHost, s.st));
+        HIP_TRY(hipEventRecord(s.done, s.st));
+        s.busy = true;
+        prev = &s;
+        k ^= 1;
+    }
+    for (auto &sl : e->hs) {
+        const int r2 = slot_drain(e, sl, hst);
+        if (!rc) rc = r2;
+    }
+    if (stream) {
+        if (!rc && prev) {
+            const hipError_t err = hipMemcpy(h_state, d_state, nseg * 20, hipMemcpyDeviceToHost);
+            if (err != hipSuccess) rc = hip_fail(err, "hipMemcpy(stream state)");
+        }
+        if (!rc) {
+            const uint32_t *hp = reinterpret_cast<const uint32_t *>(h_state + 16 * nseg);
+            for (uint64_t t = 0; t < nseg; t++) {
+                memcpy(iv_state + 16ull * segs[t].slot, h_state + 16 * t, 16);
+                pos_state[segs[t].slot] = hp[t];
+            }
+        }
+        (void)hipFree(d_state);
+        (void)hipHostFree(h_state);
+    }
+    if (hst.on)
+        fprintf(stderr, "[fpnn_aes host] %s %s: %u frames, %llu segments, %llu chunks, %.2f ms total, gather %.2f, "
+                "scatter %.2f, wait %.2f ms, %u copy threads\n", stream ? "stream" : "package",
+                encrypt ? "encrypt" : "decrypt", n, (unsigned long long)nseg, (unsigned long long)nchunks,
+                1e3 * (HostStats::now() - t_call), 1e3 * hst.gather, 1e3 * hst.scatter, 1e3 * hst.wait,
+                e->pool ? e->pool->parts() : 1u);
+    return rc;
+}
+
+int check_host_frames(const fpnn_aes_engine *e, const fpnn_aes_host_frame *frames, uint32_t n,
+                      const fpnn_aes_keyset *keys) {
     if (!e || !keys || (n && !frames)) return FPNN_AES_ERR_ARG;
-    if (!encrypt && (flags & FPNN_AES_F_WIRE_PREFIX)) return FPNN_AES_ERR_ARG;
     if (keys->device != e->device) return FPNN_AES_ERR_ARG;
     for (uint32_t i = 0; i < n; i++)
         if ((frames[i].len && (!frames[i].src || !frames[i].dst)) || frames[i].key_slot >= keys->count)
             return FPNN_AES_ERR_ARG;
+    return FPNN_AES_OK;
+}
+
+}  // namespace
+
+int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                          const fpnn_aes_keyset *keys, uint32_t flags) {
+    if (int rc = check_host_frames(e, frames, n, keys)) return rc;
+    if (!encrypt && (flags & FPNN_AES_F_WIRE_PREFIX)) return FPNN_AES_ERR_ARG;
+    if (flags & FPNN_AES_F_WIRE_PREFIX)
+        for (uint32_t i = 0; i < n; i++)
+            if (!frames[i].dst) return FPNN_AES_ERR_ARG;
     if (!n) return FPNN_AES_OK;
-    DeviceGuard g(e->device);
-    const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
-    const uint64_t kChunk = 32ull << 20;  // input bytes per pipeline chunk
-    hipStream_t main_stream = e->stream;
-    int rc = FPNN_AES_OK;
-    uint32_t i = 0;
-    int k = 0;
-    while (i < n && rc == FPNN_AES_OK) {
-        HostSlot &s = e->hs[k];
-        if ((rc = slot_drain(s, frames, flags))) break;
-        // chunk = frames [i, j) with at most kChunk input bytes (at least one frame)
-        uint32_t j = i;
-        uint64_t in_b = 0, out_b = 0;
-        while (j < n && (j == i || in_b + frames[j].len <= kChunk)) {
-            in_b += frames[j].len;
-            out_b += frames[j].len + pre;
-            j++;
-        }
-        const uint32_t cnt = j - i;
-        const uint64_t in_pad = (in_b + 15) & ~15ull, out_pad = (out_b + 15) & ~15ull;
-        const uint64_t arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
-        if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
-        uint8_t *h_in = s.h, *h_arr = s.h + in_pad;
-        uint64_t *in_off = reinterpret_cast<uint64_t *>(h_arr);
-        uint64_t *out_off = in_off + cnt;
-        uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
-        uint32_t *slots = lens + cnt;
-        s.out_at = in_pad + ((arr + 15) & ~15ull);
-        s.out_off.resize(cnt);
-        std::vector<CopyJob> jobs;
-        jobs.reserve(cnt);
-        uint64_t io = 0, oo = 0;
-        for (uint32_t t = 0; t < cnt; t++) {
-            const fpnn_aes_host_frame &f = frames[i + t];
-            in_off[t] = io;
-            out_off[t] = oo;
-            s.out_off[t] = oo;
-            lens[t] = f.len;
-            slots[t] = f.key_slot;
-            if (f.len) jobs.push_back({h_in + io, f.src, f.len});
-            io += f.len;
-            oo += f.len + pre;
-        }
-        parallel_copy(jobs, in_b);
-        const uint64_t up = in_pad + arr;
-        HIP_TRY(hipMemcpyAsync(s.d, s.h, up, hipMemcpyHostToDevice, s.st));
-        fpnn_aes_batch b;
-        memset(&b, 0, sizeof b);
-        b.in = s.d;
-        b.out = s.d + s.out_at;
-        b.count = cnt;
-        b.in_off = reinterpret_cast<const uint64_t *>(s.d + in_pad);
-        b.out_off = b.in_off + cnt;
-        b.len = reinterpret_cast<const uint32_t *>(b.out_off + cnt);
-        b.key_slot = keys->count > 1 ? b.len + cnt : nullptr;
-        b.keys = keys;
-        b.flags = flags;
-        e->stream = s.st;  // queue this chunk's kernels on the slot stream
-        rc = encrypt ? run_encrypt(e, &b, nullptr, nullptr, false) : run_decrypt(e, &b, nullptr, nullptr, false);
-        e->stream = main_stream;
-        if (rc) break;
-        HIP_TRY(hipMemcpyAsync(s.h + s.out_at, s.d + s.out_at, out_pad, hipMemcpyDeviceToHost, s.st));
-        HIP_TRY(hipEventRecord(s.done, s.st));
-        s.busy = true;
-        s.first = i;
-        s.count = cnt;
-        i = j;
-        k ^= 1;
-    }
-    for (auto &s : e->hs) {
-        const int r2 = slot_drain(s, frames, flags);
-        if (!rc) rc = r2;
-    }
-    return rc;
+    return host_pipeline(e, encrypt != 0, false, frames, n, keys, flags, nullptr, nullptr);
+}
+
+int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                         const fpnn_aes_keyset *keys, uint8_t *iv_state, uint32_t *pos_state) {
+    if (int rc = check_host_frames(e, frames, n, keys)) return rc;
+    if (n && (!iv_state || !pos_state)) return FPNN_AES_ERR_ARG;
+    if (!n) return FPNN_AES_OK;
+    return host_pipeline(e, encrypt != 0, true, frames, n, keys, 0, iv_state, pos_state);
 }
 
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset) {

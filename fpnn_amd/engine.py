@@ -19,6 +19,8 @@ import ctypes as C
 import weakref
 from typing import Optional
 
+import numpy as np
+
 import torch
 
 from ._lib import (BatchDesc, FpnnAesError, HostFrame, Schedule, check, lib, F_WIRE_PREFIX, K_DECRYPT, K_ENCRYPT,
@@ -44,10 +46,8 @@ def _release_all():
 
 
 # numpy mirror of fpnn_aes_host_frame for building large frame lists without a Python loop
-import numpy as _np  # noqa: E402
-
-HOST_FRAME_DTYPE = _np.dtype([("src", _np.uint64), ("dst", _np.uint64), ("len", _np.uint32),
-                              ("key_slot", _np.uint32)])
+HOST_FRAME_DTYPE = np.dtype([("src", np.uint64), ("dst", np.uint64), ("len", np.uint32),
+                             ("key_slot", np.uint32)])
 assert HOST_FRAME_DTYPE.itemsize == C.sizeof(HostFrame)
 
 
@@ -156,6 +156,33 @@ class Engine:
         ptr = C.cast(C.c_void_p(frames_np.ctypes.data), C.POINTER(HostFrame))
         check(lib.fpnn_aes_package_host(self._h, int(encrypt), ptr, len(frames_np), keys.handle,
                                         F_WIRE_PREFIX if wire_prefix else 0), "package_host")
+
+    def stream_host(self, encrypt: bool, frames, keys: "KeySet", iv_state: np.ndarray, pos_state: np.ndarray):
+        """Stream-mode host frames.  frames: sequence of (src, dst, stream_slot); a stream's
+        frames are processed in sequence order.  iv_state: uint8 [keys.count, 16] and
+        pos_state: uint32 [keys.count] host arrays, updated in place."""
+        arr = (HostFrame * max(1, len(frames)))()
+        for i, (src, dst, slot) in enumerate(frames):
+            arr[i].src = src.ctypes.data if src.size else None
+            arr[i].dst = dst.ctypes.data if dst.size else None
+            arr[i].len = src.size
+            arr[i].key_slot = slot
+        self._stream_host(encrypt, arr, len(frames), keys, iv_state, pos_state)
+
+    def stream_host_array(self, encrypt: bool, frames_np, keys: "KeySet", iv_state: np.ndarray,
+                          pos_state: np.ndarray):
+        ptr = C.cast(C.c_void_p(frames_np.ctypes.data), C.POINTER(HostFrame))
+        self._stream_host(encrypt, ptr, len(frames_np), keys, iv_state, pos_state)
+
+    def _stream_host(self, encrypt, arr, n, keys, iv_state, pos_state):
+        if iv_state.dtype != np.uint8 or pos_state.dtype != np.uint32:
+            raise TypeError("iv_state must be uint8, pos_state uint32")
+        if iv_state.size < 16 * keys.count or pos_state.size < keys.count:
+            raise ValueError("state arrays must hold keys.count streams")
+        if not (iv_state.flags.c_contiguous and pos_state.flags.c_contiguous):
+            raise ValueError("state arrays must be contiguous")
+        check(lib.fpnn_aes_stream_host(self._h, int(encrypt), arr, n, keys.handle,
+                                       iv_state.ctypes.data, pos_state.ctypes.data), "stream_host")
 
     # -- batches ----------------------------------------------------------------------------
     def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,

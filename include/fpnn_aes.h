@@ -157,6 +157,15 @@ typedef struct {
 int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                           const fpnn_aes_keyset *keys, uint32_t flags);
 
+/* Stream-mode encrypt/decrypt of n host frames (StreamEncryptor::encrypt/decrypt,
+ * core/Encryptor.cpp:53-70, one call per frame in the reference).  key_slot names the
+ * stream: its key slot in `keys` AND its state (iv_state[16*slot .. +16], pos_state[slot],
+ * host arrays of keys->count entries, StreamEncryptor::_iv/_pos), updated in place.  A
+ * stream may appear many times: its frames are processed in array order, exactly as
+ * that many successive calls.  Synchronous. */
+int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                         const fpnn_aes_keyset *keys, uint8_t *iv_state, uint32_t *pos_state);
+
 /* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
 /* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed,

@@ -123,13 +123,19 @@ void ao_encrypt_block(const ao_ctx *ctx, const uint8_t in[16], uint8_t out[16])
     uint32_t s[4], t[4];
     for (int i = 0; i < 4; i++)
         s[i] = load_be32(in + 4 * i) ^ rk[i];
+    /* one full round per iteration, columns written out (same arithmetic as the
+       indexed form t[i] = Te0[s_i] ^ Te1[s_i+1] ^ Te2[s_i+2] ^ Te3[s_i+3] ^ rk) */
+#define AO_COL(i0, i1, i2, i3, k)                                                            \
+    (g_te[0][s[i0] >> 24] ^ g_te[1][(s[i1] >> 16) & 0xff] ^ g_te[2][(s[i2] >> 8) & 0xff] ^ \
+     g_te[3][s[i3] & 0xff] ^ rk[k])
     for (int r = 1; r < nr; r++) {
-        for (int i = 0; i < 4; i++)
-            t[i] = g_te[0][s[i] >> 24] ^ g_te[1][(s[(i + 1) & 3] >> 16) & 0xff] ^
-                   g_te[2][(s[(i + 2) & 3] >> 8) & 0xff] ^ g_te[3][s[(i + 3) & 3] & 0xff] ^
-                   rk[4 * r + i];
-        memcpy(s, t, sizeof s);
+        t[0] = AO_COL(0, 1, 2, 3, 4 * r);
+        t[1] = AO_COL(1, 2, 3, 0, 4 * r + 1);
+        t[2] = AO_COL(2, 3, 0, 1, 4 * r + 2);
+        t[3] = AO_COL(3, 0, 1, 2, 4 * r + 3);
+        s[0] = t[0]; s[1] = t[1]; s[2] = t[2]; s[3] = t[3];
     }
+#undef AO_COL
     for (int i = 0; i < 4; i++) {
         uint32_t v = ((uint32_t)g_sbox[s[i] >> 24] << 24) |
                      ((uint32_t)g_sbox[(s[(i + 1) & 3] >> 16) & 0xff] << 16) |

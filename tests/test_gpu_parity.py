@@ -501,3 +501,46 @@ def test_package_host_frames(engine, oracle, wire_prefix):
         engine.package_host(False, [(c, c, sl) for c, _, sl in back], ks)
         for (c, _, _), src in zip(back, srcs):
             assert np.array_equal(c, src)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_stream_host_frames(engine, oracle, keylen):
+    """fpnn_aes_stream_host: frames of many streams interleaved in one call, each
+    stream's frames in order, equal to successive StreamEncryptor calls; one stream
+    is longer than a pipeline chunk (split across chunks, state chained)."""
+    import fpnn_amd
+    rng = np.random.default_rng(777 + keylen)
+    ns = 37
+    keys = rng.integers(0, 256, ns * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, ns * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+    iv0 = rng.integers(0, 256, (ns, 16), dtype=np.uint8)
+    pos0 = rng.integers(0, 16, ns).astype(np.uint32)
+    pos0[:3] = 0
+    frames = []
+    for i in range(2500):
+        s = int(rng.integers(0, ns - 1))  # stream ns-1 is untouched: state must stay
+        L = int(rng.choice([0, 1, 15, 16, 17, int(rng.integers(0, 3000))]))
+        frames.append((rng.integers(0, 256, L, dtype=np.uint8), s))
+    big = 3
+    frames.insert(100, (rng.integers(0, 256, 21 << 20, dtype=np.uint8), big))
+    frames.insert(900, (rng.integers(0, 256, (19 << 20) + 5, dtype=np.uint8), big))
+    outs = [np.zeros_like(f) for f, _ in frames]
+    iv_s, pos_s = iv0.copy(), pos0.copy()
+    engine.stream_host(True, [(f, o, s) for (f, s), o in zip(frames, outs)], ks, iv_s, pos_s)
+    # oracle: per stream, successive calls
+    st = {s: (iv0[s].tobytes(), int(pos0[s])) for s in range(ns)}
+    for (f, s), o in zip(frames, outs):
+        k = keys[s * keylen:(s + 1) * keylen].tobytes()
+        exp, iv, pos = oracle.cfb(k, True, f.tobytes(), st[s][0], st[s][1])
+        st[s] = (iv, pos)
+        assert o.tobytes() == exp, s
+    for s in range(ns):
+        assert iv_s[s].tobytes() == st[s][0] and int(pos_s[s]) == st[s][1], s
+    # decrypt in place from the initial state
+    iv_d, pos_d = iv0.copy(), pos0.copy()
+    bufs = [o.copy() for o in outs]
+    engine.stream_host(False, [(b, b, s) for b, (_, s) in zip(bufs, frames)], ks, iv_d, pos_d)
+    for b, (f, _) in zip(bufs, frames):
+        assert np.array_equal(b, f)
+    assert np.array_equal(iv_d, iv_s) and np.array_equal(pos_d, pos_s)

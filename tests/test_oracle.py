@@ -105,3 +105,21 @@ def test_live_reference_random(oracle, ref_oracle):
         assert oracle.cfb(key, enc, data, iv, pos) == ref_oracle.cfb(key, enc, data, iv, pos)
         if kl != 24:
             assert oracle.package_frame(key, iv, data) == ref_oracle.package_frame(key, iv, data)
+
+
+def test_port_speed_tracks_reference(oracle, ref_oracle):
+    """the restatement runs the same algorithm (T-tables, per-frame key
+    setup, byte-loop CFB), so one core of it should time close to the compiled reference
+    (measured here: within ~12%).  The bound is loose so that a loaded CI host cannot
+    flake it; it catches an accidentally de-optimised oracle."""
+    n, L = 2048, 1024
+    a = np.random.default_rng(5).integers(0, 256, n * L, dtype=np.uint8)
+    t, o = np.empty_like(a), np.empty_like(a)
+    key, iv = bytes(range(32)), bytes(16)
+    best = {}
+    for _ in range(3):
+        for name, orc in (("port", oracle), ("reference", ref_oracle)):
+            dt = orc.time_package_roundtrip(a, t, o, n, L, key, iv, 1, 1)
+            best[name] = min(best.get(name, 1e9), dt)
+    ratio = best["reference"] / best["port"]  # port speed relative to the reference
+    assert 0.6 < ratio < 1.7, ratio

@@ -101,8 +101,13 @@ def main():
             eng.package_host_array(True, fr, ks)
         hb = (time.perf_counter() - t0) / args.reps
         assert np.array_equal(dst_h, r.cpu().numpy())  # r = encrypt(a) from the PCIe loop
+        fr["src"] = fr["dst"]  # decrypt in place
+        t0 = time.perf_counter()
+        eng.package_host_array(False, fr, ks)
+        hbd = time.perf_counter() - t0
+        assert np.array_equal(dst_h, src_h)
         out["C2"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd),
-                     "host_frames_encrypt_GiBs": gib(P * L, hb),
+                     "host_frames_encrypt_GiBs": gib(P * L, hb), "host_frames_decrypt_GiBs": gib(P * L, hbd),
                      "encrypt_wall_GiBs": gib(P * L, we), "decrypt_wall_GiBs": gib(P * L, wd),
                      "pcie_inclusive_encrypt_GiBs": gib(P * L, pe), "h2d_GiBs": gib(P * L, h2d),
                      "d2h_GiBs": gib(P * L, d2h),
@@ -194,10 +199,36 @@ def main():
         wfe, _, _ = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), 1)
         wfd, _, _ = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), 1)
         assert torch.equal(r, a)
+        # host frames, one stream_host call for the framed streams of a 1 GiB subset
+        HS = 256
+        src_h = a[:HS * L].cpu().numpy()
+        dst_h = np.empty_like(src_h)
+        fl = [(s_, int(starts[f, s_]), int(lens[f, s_])) for f in range(nmax) for s_ in range(HS) if lens[f, s_]]
+        fr = np.zeros(len(fl), dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
+        fr["src"] = src_h.ctypes.data + np.array([o for _, o, _ in fl], dtype=np.uint64)
+        fr["dst"] = dst_h.ctypes.data + np.array([o for _, o, _ in fl], dtype=np.uint64)
+        fr["len"] = [x for _, _, x in fl]
+        fr["key_slot"] = [s_ for s_, _, _ in fl]
+        h_iv = np.ascontiguousarray(np.resize(ivs, (S, 16)))
+        h_pos = np.zeros(S, dtype=np.uint32)
+        eng.stream_host_array(True, fr, ks, h_iv.copy(), h_pos.copy())  # warm: staging allocation
+        t0 = time.perf_counter()
+        eng.stream_host_array(True, fr, ks, h_iv, h_pos)
+        hse = time.perf_counter() - t0
+        assert np.array_equal(dst_h, b[:HS * L].cpu().numpy())
+        h_iv = np.ascontiguousarray(np.resize(ivs, (S, 16)))
+        h_pos[:] = 0
+        fr["src"] = fr["dst"]
+        t0 = time.perf_counter()
+        eng.stream_host_array(False, fr, ks, h_iv, h_pos)  # in place
+        hsd = time.perf_counter() - t0
+        assert np.array_equal(dst_h, src_h)
         out["C3"] = {"whole_stream_encrypt_kernel_GiBs": gib(S * L, ke),
                      "whole_stream_decrypt_kernel_GiBs": gib(S * L, kd),
                      "framed_calls": nmax, "framed_encrypt_wall_GiBs": gib(S * L, wfe),
                      "framed_decrypt_wall_GiBs": gib(S * L, wfd),
+                     "host_frames_streams": HS, "host_frames": len(fl),
+                     "host_frames_encrypt_GiBs": gib(HS * L, hse), "host_frames_decrypt_GiBs": gib(HS * L, hsd),
                      "note": "encrypt = 4096 serial CFB chains (one lane each, latency bound); "
                              "decrypt parallel per block"}
         print(json.dumps({"C3": out["C3"]}), flush=True)
