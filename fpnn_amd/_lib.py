@@ -29,6 +29,8 @@ ERR_HIP = -4
 ERR_NODEV = -5
 
 F_WIRE_PREFIX = 0x1
+SCAN_OK, SCAN_FULL, SCAN_TOO_LARGE, SCAN_BAD_MAGIC, SCAN_BAD_MTYPE, SCAN_BAD_LENGTH = range(6)
+MAX_RECV_PACKAGE_LENGTH = 8 * 1024 * 1024  # FPNN_DEFAULT_MAX_PACKAGE_LEN, core/Config.h:14
 K_DECRYPT = 0
 K_ENCRYPT = 1
 
@@ -98,6 +100,9 @@ SIGNATURES = {
                                     C.POINTER(C.c_size_t)]),
     "fpnn_aes_package_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, C.c_uint32]),
     "fpnn_aes_stream_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, _vp, _vp]),
+    "fpnn_aes_package_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), C.c_uint32, C.c_uint32, _vp, _vp, _vp]),
+    "fpnn_aes_stream_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
+                                       _vp]),
     "fpnn_aes_fill_synthetic": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64]),
     "fpnn_aes_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),

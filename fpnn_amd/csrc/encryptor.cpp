@@ -7,8 +7,11 @@
 
 #include <memory>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/Encryptor.h"
+#include "../../include/EncryptorBatch.h"
 #include "../../include/fpnn_aes.h"
 
 namespace {
@@ -124,6 +127,137 @@ void StreamEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:63-7
     cfb_or_throw(&_ctx, true, reinterpret_cast<const uint8_t *>(buffer->data()), reinterpret_cast<uint8_t *>(&out[0]),
                  n, _iv, &_pos);
     buffer->swap(out);
+}
+
+// ---- EncryptorBatch (include/EncryptorBatch.h) ------------------------------------------
+
+void EncryptorBatch::add(Encryptor *enc, bool encrypt, uint8_t *dest, const uint8_t *src, int len,
+                         std::string *buffer) {
+    if (!enc) throw EncryptorError("EncryptorBatch: null encryptor");
+    if (!dynamic_cast<PackageEncryptor *>(enc) && !dynamic_cast<StreamEncryptor *>(enc))
+        throw EncryptorError("EncryptorBatch: unsupported Encryptor subclass");
+    if (!buffer && len <= 0) return;  // the per-call methods do nothing for len <= 0
+    _ops.push_back({enc, dest, src, buffer ? (uint32_t)buffer->size() : (uint32_t)len, encrypt, buffer});
+    _bytes += _ops.back().len;
+}
+
+void EncryptorBatch::encrypt(Encryptor *enc, std::string *buffer) {
+    if (!buffer) throw EncryptorError("EncryptorBatch: null buffer");
+    add(enc, true, nullptr, nullptr, 0, buffer);
+}
+
+void EncryptorBatch::encrypt(Encryptor *enc, uint8_t *dest, uint8_t *src, int len) {
+    add(enc, true, dest, src, len, nullptr);
+}
+
+void EncryptorBatch::decrypt(Encryptor *enc, uint8_t *dest, uint8_t *src, int len) {
+    add(enc, false, dest, src, len, nullptr);
+}
+
+namespace {
+
+struct KeySetGuard {
+    fpnn_aes_keyset *ks = nullptr;
+    ~KeySetGuard() {
+        if (ks) fpnn_aes_keyset_destroy(ks);
+    }
+};
+
+}  // namespace
+
+void EncryptorBatch::flush() {
+    std::vector<Op> ops;
+    ops.swap(_ops);
+    _bytes = 0;
+    if (ops.empty()) return;
+    int rc;
+    fpnn_aes_engine *e = thread_engine(&rc);
+    if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
+    // group by (mode, direction, wire prefix, rounds); queue order is kept inside a group
+    struct Group {
+        bool stream, encrypt, prefix;
+        int nrounds;
+        std::vector<size_t> idx;
+    };
+    std::vector<Group> groups;
+    std::unordered_map<const StreamEncryptor *, bool> stream_dir;
+    for (size_t i = 0; i < ops.size(); i++) {
+        const Op &op = ops[i];
+        StreamEncryptor *se = dynamic_cast<StreamEncryptor *>(op.enc);
+        const bool stream = se != nullptr;
+        const bool prefix = !stream && op.buffer != nullptr;
+        const int nr = stream ? se->_ctx.nrounds : static_cast<PackageEncryptor *>(op.enc)->_ctx.nrounds;
+        if (stream) {
+            auto it = stream_dir.emplace(se, op.encrypt).first;
+            if (it->second != op.encrypt)
+                throw EncryptorError("EncryptorBatch: a StreamEncryptor used in both directions in one batch");
+            if (op.buffer && op.buffer->empty()) continue;  // StreamEncryptor::encrypt(std::string*) of ""
+        }
+        size_t g = 0;
+        while (g < groups.size() && !(groups[g].stream == stream && groups[g].encrypt == op.encrypt &&
+                                      groups[g].prefix == prefix && groups[g].nrounds == nr))
+            g++;
+        if (g == groups.size()) groups.push_back({stream, op.encrypt, prefix, nr, {}});
+        groups[g].idx.push_back(i);
+    }
+    for (const Group &gr : groups) {
+        std::unordered_map<const Encryptor *, uint32_t> slot_of;
+        std::vector<fpnn_aes_schedule> scheds;
+        std::vector<uint8_t> ivs;
+        std::vector<const Encryptor *> members;
+        std::vector<fpnn_aes_host_frame> frames(gr.idx.size());
+        std::vector<std::string> framed;  // package std::string outputs (len + 4)
+        if (gr.prefix) framed.resize(gr.idx.size());
+        for (size_t t = 0; t < gr.idx.size(); t++) {
+            Op &op = ops[gr.idx[t]];
+            auto ins = slot_of.emplace(op.enc, (uint32_t)members.size());
+            if (ins.second) {
+                const rijndael_context &ctx = gr.stream ? static_cast<StreamEncryptor *>(op.enc)->_ctx
+                                                        : static_cast<PackageEncryptor *>(op.enc)->_ctx;
+                scheds.push_back(*reinterpret_cast<const fpnn_aes_schedule *>(&ctx));
+                ivs.insert(ivs.end(), op.enc->_iv, op.enc->_iv + 16);
+                members.push_back(op.enc);
+            }
+            fpnn_aes_host_frame &f = frames[t];
+            f.len = op.len;
+            f.key_slot = ins.first->second;
+            if (op.buffer) {
+                f.src = reinterpret_cast<const uint8_t *>(op.buffer->data());
+                if (gr.prefix) {
+                    framed[t].assign(op.len + sizeof(uint32_t), '\0');
+                    f.dst = reinterpret_cast<uint8_t *>(&framed[t][0]);
+                } else {
+                    f.dst = reinterpret_cast<uint8_t *>(&(*op.buffer)[0]);  // in place, same length
+                }
+            } else {
+                f.src = op.src;
+                f.dst = op.dest;
+            }
+        }
+        KeySetGuard ks;
+        rc = fpnn_aes_keyset_from_schedules(e, (uint32_t)members.size(), scheds.data(), ivs.data(), &ks.ks);
+        if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: key set: " + describe(rc));
+        if (!gr.stream) {
+            rc = fpnn_aes_package_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), ks.ks,
+                                       gr.prefix ? FPNN_AES_F_WIRE_PREFIX : 0);
+            if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: package batch: " + describe(rc));
+            if (gr.prefix)
+                for (size_t t = 0; t < gr.idx.size(); t++) ops[gr.idx[t]].buffer->swap(framed[t]);
+        } else {
+            std::vector<uint8_t> iv_state(ivs);
+            std::vector<uint32_t> pos_state(members.size());
+            for (size_t m = 0; m < members.size(); m++)
+                pos_state[m] = (uint32_t)static_cast<const StreamEncryptor *>(members[m])->_pos;
+            rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), ks.ks,
+                                      iv_state.data(), pos_state.data());
+            if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: stream batch: " + describe(rc));
+            for (size_t m = 0; m < members.size(); m++) {
+                StreamEncryptor *se = const_cast<StreamEncryptor *>(static_cast<const StreamEncryptor *>(members[m]));
+                memcpy(se->_iv, &iv_state[16 * m], 16);
+                se->_pos = pos_state[m];
+            }
+        }
+    }
 }
 
 }  // namespace fpnn

@@ -183,6 +183,10 @@ struct fpnn_aes_engine {
     uint64_t cap_perm = 0;
     uint32_t *d_buckets = nullptr;  // 2 x 128 counters
     uint64_t cap_buckets = 0;
+    uint64_t *d_fr_off = nullptr;  // package receive: absolute body offset per frame slot
+    uint64_t cap_fr_off = 0;
+    uint32_t *d_fr_slot = nullptr;  // package receive: key slot per frame slot
+    uint64_t cap_fr_slot = 0;
     uint64_t *d_total = nullptr;
     uint64_t *h_total = nullptr;  // pinned
     // host staging for fpnn_aes_cfb_host
@@ -562,6 +566,8 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_snap_pos);
     (void)hipFree(e->d_perm);
     (void)hipFree(e->d_buckets);
+    (void)hipFree(e->d_fr_off);
+    (void)hipFree(e->d_fr_slot);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_total) (void)hipHostFree(e->h_total);
@@ -723,6 +729,80 @@ int fpnn_aes_stream_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t
 
 int fpnn_aes_stream_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state) {
     return run_decrypt(e, b, iv_state, pos_state, true);
+}
+
+// ---- receive side: wire framing on the device ------------------------------------
+
+int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t max_len, uint32_t max_frames,
+                          uint64_t *frame_off, uint32_t *frame_len, fpnn_aes_frame_scan *scan) {
+    int rc = check_batch(e, b);
+    if (rc) return rc;
+    if (b->out_off || b->flags) return FPNN_AES_ERR_ARG;
+    if (!b->count) return FPNN_AES_OK;
+    if (!frame_off || !frame_len || !scan || !max_frames) return FPNN_AES_ERR_ARG;
+    const uint64_t slots = (uint64_t)b->count * max_frames;
+    if (slots > 0xffffffffull) return FPNN_AES_ERR_RANGE;
+    DeviceGuard g(e->device);
+    const bool per_key = b->key_slot && b->keys->count > 1;
+    if ((rc = grow(e->d_fr_off, e->cap_fr_off, slots))) return rc;
+    if (per_key && (rc = grow(e->d_fr_slot, e->cap_fr_slot, slots))) return rc;
+    KScan s;
+    memset(&s, 0, sizeof s);
+    s.buf = b->in;
+    s.count = b->count;
+    s.off = b->in_off;
+    s.stride = b->stride;
+    s.len = b->len;
+    s.uniform_len = b->uniform_len;
+    s.max_len = max_len;
+    s.key_slot = per_key ? b->key_slot : nullptr;
+    s.max_frames = max_frames;
+    s.frame_off = frame_off;
+    s.frame_len = frame_len;
+    s.scan = reinterpret_cast<ScanResult *>(scan);
+    s.abs_off = e->d_fr_off;
+    s.abs_slot = per_key ? e->d_fr_slot : nullptr;
+    static_assert(sizeof(ScanResult) == sizeof(fpnn_aes_frame_scan), "scan layout");
+    HIP_TRY(launch_scan_frames(s, false, e->num_cus, e->stream));
+    // every frame slot is one package segment (unused ones have length 0)
+    fpnn_aes_batch fb;
+    memset(&fb, 0, sizeof fb);
+    fb.in = b->in;
+    fb.out = b->out;
+    fb.count = (uint32_t)slots;
+    fb.in_off = e->d_fr_off;
+    fb.len = frame_len;
+    fb.key_slot = per_key ? e->d_fr_slot : nullptr;
+    fb.keys = b->keys;
+    return run_decrypt(e, &fb, nullptr, nullptr, false);
+}
+
+int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state,
+                         const uint32_t *carry, uint32_t max_len, uint32_t max_frames, uint64_t *frame_off,
+                         uint32_t *frame_len, fpnn_aes_frame_scan *scan) {
+    int rc = check_batch(e, b);
+    if (rc) return rc;
+    if (!b->count) return FPNN_AES_OK;
+    if (!frame_off || !frame_len || !scan || !max_frames) return FPNN_AES_ERR_ARG;
+    if ((uint64_t)b->count * max_frames > 0xffffffffull) return FPNN_AES_ERR_RANGE;
+    if ((rc = run_decrypt(e, b, iv_state, pos_state, true))) return rc;
+    DeviceGuard g(e->device);
+    KScan s;
+    memset(&s, 0, sizeof s);
+    s.buf = b->out;
+    s.count = b->count;
+    s.off = b->out_off ? b->out_off : b->in_off;
+    s.stride = b->stride;
+    s.len = b->len;
+    s.uniform_len = b->uniform_len;
+    s.max_len = max_len;
+    s.carry = carry;
+    s.max_frames = max_frames;
+    s.frame_off = frame_off;
+    s.frame_len = frame_len;
+    s.scan = reinterpret_cast<ScanResult *>(scan);
+    HIP_TRY(launch_scan_frames(s, true, e->num_cus, e->stream));
+    return FPNN_AES_OK;
 }
 
 // ---- single call from host memory ------------------------------------------------

@@ -59,6 +59,33 @@ struct Variant {
 int blocks_per_cu(const Variant &v, KeyMode km);
 // threads = workgroup size (64..1024, multiple of 64): few chains are spread over all
 // CUs with small workgroups instead of packed into a few full ones.
+// Frame scan of received segments (framing.hip).
+enum : uint32_t { SCAN_OK = 0, SCAN_FULL = 1, SCAN_TOO_LARGE = 2, SCAN_BAD_MAGIC = 3, SCAN_BAD_MTYPE = 4,
+                  SCAN_BAD_LENGTH = 5 };
+struct ScanResult {  // == fpnn_aes_frame_scan
+    uint32_t frames, status;
+    uint64_t consumed;
+};
+struct KScan {
+    const uint8_t *buf;       // package: received bytes; stream: decrypted plaintext
+    uint64_t count;
+    const uint64_t *off;      // segment starts (NULL: i * stride)
+    uint64_t stride;
+    const uint32_t *len;      // segment lengths (NULL: uniform_len)
+    uint32_t uniform_len;
+    uint32_t max_len;
+    const uint32_t *carry;    // stream: plaintext bytes before each segment (NULL: 0)
+    const uint32_t *key_slot; // package: segment key slots (NULL: 0)
+    uint32_t max_frames;
+    uint32_t pad;
+    uint64_t *frame_off;      // [count * max_frames], relative to the segment (region) start
+    uint32_t *frame_len;
+    ScanResult *scan;         // [count]
+    uint64_t *abs_off;        // package: absolute body offsets, for the decrypt batch
+    uint32_t *abs_slot;       // package: key slot per frame slot (NULL: one key)
+};
+
+hipError_t launch_scan_frames(const KScan &s, bool stream, int num_cus, hipStream_t st);
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
                                  bool stream, int grid, int threads, hipStream_t st);
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.

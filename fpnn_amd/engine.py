@@ -184,6 +184,37 @@ class Engine:
         check(lib.fpnn_aes_stream_host(self._h, int(encrypt), arr, n, keys.handle,
                                        iv_state.ctypes.data, pos_state.ctypes.data), "stream_host")
 
+    # -- receive side: framing on the device -------------------------------------------------
+    @staticmethod
+    def _scan_buffers(count, max_frames, device):
+        off = torch.empty(count * max_frames, dtype=torch.int64, device=device)
+        ln = torch.empty(count * max_frames, dtype=torch.int32, device=device)
+        scan = torch.empty(count * 2, dtype=torch.int64, device=device)  # fpnn_aes_frame_scan[count]
+        return off, ln, scan
+
+    @staticmethod
+    def decode_scan(scan: torch.Tensor):
+        """fpnn_aes_frame_scan[count] -> numpy (frames, status, consumed) columns."""
+        a = scan.cpu().numpy().view(np.uint32).reshape(-1, 4)
+        return a[:, 0].copy(), a[:, 1].copy(), scan.cpu().numpy().reshape(-1, 2)[:, 1].copy()
+
+    def package_recv(self, inp, out, count, keys: "KeySet", max_len: int, max_frames: int, **kw):
+        """fpnn_aes_package_recv: returns device tensors (frame_off, frame_len, scan)."""
+        d = self._desc(inp, out, count, keys, **kw)
+        off, ln, scan = self._scan_buffers(count, max_frames, inp.device)
+        check(lib.fpnn_aes_package_recv(self._h, C.byref(d), max_len, max_frames, _ptr(off), _ptr(ln), _ptr(scan)),
+              "package_recv")
+        return off, ln, scan
+
+    def stream_recv(self, inp, out, count, keys: "KeySet", iv_state, pos_state, max_len: int, max_frames: int,
+                    carry: Optional[torch.Tensor] = None, **kw):
+        """fpnn_aes_stream_recv: returns device tensors (frame_off, frame_len, scan)."""
+        d = self._desc(inp, out, count, keys, **kw)
+        off, ln, scan = self._scan_buffers(count, max_frames, inp.device)
+        check(lib.fpnn_aes_stream_recv(self._h, C.byref(d), _ptr(iv_state), _ptr(pos_state), _ptr(carry), max_len,
+                                       max_frames, _ptr(off), _ptr(ln), _ptr(scan)), "stream_recv")
+        return off, ln, scan
+
     # -- batches ----------------------------------------------------------------------------
     def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,
               key_slot=None, flags=0) -> BatchDesc:

@@ -27,12 +27,16 @@
 
 namespace fpnn {
 
+class EncryptorBatch;  // EncryptorBatch.h: runs queued calls of many encryptors in one GPU pass
+
 class EncryptorError : public std::runtime_error {
 public:
     explicit EncryptorError(const std::string &what) : std::runtime_error(what) {}
 };
 
 class Encryptor {
+    friend class EncryptorBatch;
+
 protected:
     uint8_t _iv[16];
     uint8_t _key[32];
@@ -53,6 +57,7 @@ public:
 
 /* One fresh CFB chain per call from the connection IV (core/Encryptor.cpp:10-51). */
 class PackageEncryptor : public Encryptor {
+    friend class EncryptorBatch;
     rijndael_context _ctx;  // expanded once; the reference re-expands per call (same result)
 
 public:
@@ -70,6 +75,7 @@ public:
 /* One CFB chain per connection direction, state (_iv, _pos) carried across calls
  * (core/Encryptor.cpp:53-70). */
 class StreamEncryptor : public Encryptor {
+    friend class EncryptorBatch;
     rijndael_context _ctx;
     size_t _pos;
 

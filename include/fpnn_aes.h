@@ -166,6 +166,45 @@ int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_f
 int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                          const fpnn_aes_keyset *keys, uint8_t *iv_state, uint32_t *pos_state);
 
+/* ---- receive side: wire framing on the device (§8f row 3) --------------------------- */
+/* Per received segment (the bytes one connection delivered), the outcome of walking its
+ * frames: `frames` complete frames cover the first `consumed` bytes; the rest is an
+ * incomplete frame to keep for the next call, unless status says the connection is bad. */
+typedef struct {
+    uint32_t frames;
+    uint32_t status;   /* FPNN_AES_SCAN_* */
+    uint64_t consumed;
+} fpnn_aes_frame_scan;
+#define FPNN_AES_SCAN_OK         0 /* stopped at the end of the data (maybe mid-frame) */
+#define FPNN_AES_SCAN_FULL       1 /* max_frames frames recorded; call again from `consumed` */
+#define FPNN_AES_SCAN_TOO_LARGE  2 /* frame above max_len: the reference closes the connection */
+#define FPNN_AES_SCAN_BAD_MAGIC  3 /* stream: header magic is not "FPNN" */
+#define FPNN_AES_SCAN_BAD_MTYPE  4 /* stream: mtype not 0/1/2 (FPMessage::BodyLen throws) */
+#define FPNN_AES_SCAN_BAD_LENGTH 5 /* stream: message length <= 0 by the reference's int arithmetic */
+
+/* Package-mode receive: EncryptedPackageReceiver::recvPackage + fetch
+ * (core/EncryptedPackageReceiver.cpp:60-118) for many connections at once.  Segment i of
+ * b (b->in + in_off[i], len_i bytes, key slot slot_i) starts at a frame boundary and holds
+ * [htole32(n)][n bytes ciphertext] wire frames.  The complete frames' bodies are
+ * decrypted (fresh chain each, like PackageEncryptor::decrypt) to b->out at the same
+ * offsets (b->out_off must be NULL; in place when b->out == b->in); prefixes and the
+ * trailing incomplete frame are not written.  Frame j of segment i is reported at
+ * [i*max_frames + j]: frame_off = body offset within the segment, frame_len = n
+ * (dev arrays; scan[count] dev).  max_len: Config::_max_recv_package_length (8 MiB). */
+int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t max_len, uint32_t max_frames,
+                          uint64_t *frame_off, uint32_t *frame_len, fpnn_aes_frame_scan *scan);
+
+/* Stream-mode receive: EncryptedStreamReceiver (core/EncryptedStreamReceiver.cpp:72-163).
+ * Segment i is the ciphertext newly received on stream i; it is decrypted exactly as
+ * fpnn_aes_stream_decrypt (state advanced over every byte) and the plaintext, preceded
+ * by carry[i] bytes already in b->out (the previous call's incomplete message, NULL = 0),
+ * is split into FPNN messages: 12-byte header + FPMessage::BodyLen (proto/FPMessage.cpp:27-44).
+ * frame_off is relative to the region start (out + out_off[i] - carry[i]), frame_len is the
+ * whole message length (what fetch() hands to the decoder). */
+int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state,
+                         const uint32_t *carry, uint32_t max_len, uint32_t max_frames, uint64_t *frame_off,
+                         uint32_t *frame_len, fpnn_aes_frame_scan *scan);
+
 /* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
 /* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed,

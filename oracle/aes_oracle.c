@@ -357,3 +357,64 @@ double ao_time_package_roundtrip(const uint8_t *in, uint8_t *tmp, uint8_t *out, 
     }
     return now_s() - t0;
 }
+
+/* ------------------------------------------------------------------------- */
+/* Receive-side framing                                                        */
+
+static uint32_t le32_at(const uint8_t *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+void ao_scan_package(const uint8_t *seg, uint64_t len, uint32_t max_len, uint32_t max_frames, uint64_t *off,
+                     uint32_t *flen, ao_scan *res)
+{
+    uint64_t pos = 0;
+    uint32_t f = 0, status = AO_SCAN_OK;
+    while (len - pos >= 4) {                      /* _packageLen read complete (:62-71) */
+        uint32_t n = le32_at(seg + pos);          /* le32toh(_packageLen) (:76) */
+        if (n > max_len) { status = AO_SCAN_TOO_LARGE; break; }   /* (:77-81) */
+        if (len - pos - 4 < n) break;             /* body still incomplete (:62-71 again) */
+        if (f == max_frames) { status = AO_SCAN_FULL; break; }
+        off[f] = pos + 4;
+        flen[f] = n;
+        f++;
+        pos += 4 + (uint64_t)n;
+    }
+    res->frames = f;
+    res->status = status;
+    res->consumed = pos;
+}
+
+void ao_scan_stream(const uint8_t *plain, uint64_t len, uint32_t max_len, uint32_t max_frames, uint64_t *off,
+                    uint32_t *flen, ao_scan *res)
+{
+    uint64_t pos = 0;
+    uint32_t f = 0, status = AO_SCAN_OK;
+    while (len - pos >= 12) {                     /* 12 header bytes received and decrypted (:87-89) */
+        const uint8_t *h = plain + pos;
+        uint32_t mtype, ss, psize, body;
+        int64_t length;
+        if (memcmp(h, "FPNN", 4) != 0) { status = AO_SCAN_BAD_MAGIC; break; }  /* isTCP (:11) */
+        mtype = h[6];                             /* Header{magic, version, flag, mtype, ss, psize} */
+        ss = h[7];
+        psize = le32_at(h + 8);
+        if (mtype == 1) body = psize + ss + 4u;   /* FP_MT_TWOWAY (FPMessage.cpp:31-34) */
+        else if (mtype == 2) body = psize + 4u;   /* FP_MT_ANSWER (:35-37) */
+        else if (mtype == 0) body = psize + ss;   /* FP_MT_ONEWAY (:38-40) */
+        else { status = AO_SCAN_BAD_MTYPE; break; }  /* throws FpnnProtoError (:41-42) */
+        /* remainDataLen (:12): (int)(sizeof(Header) + BodyLen) - _curr, _curr == 12 */
+        length = (int64_t)(int32_t)(uint32_t)(12u + body) - 12;
+        if (length <= 0) { status = AO_SCAN_BAD_LENGTH; break; }          /* (:92, :106-110) */
+        if (12 + length > (int64_t)max_len) { status = AO_SCAN_TOO_LARGE; break; }  /* (:94-98) */
+        if (len - pos < 12 + (uint64_t)length) break;   /* body still incomplete */
+        if (f == max_frames) { status = AO_SCAN_FULL; break; }
+        off[f] = pos;
+        flen[f] = (uint32_t)(12 + length);
+        f++;
+        pos += 12 + (uint64_t)length;
+    }
+    res->frames = f;
+    res->status = status;
+    res->consumed = pos;
+}

@@ -195,3 +195,33 @@ def synth_bytes(nbytes: int, seed: int, offset: int = 0, threads: int = 8) -> np
 
 def synth_word(seed: int, i: int) -> int:
     return int(_plib().ao_synth_word(seed, i))
+
+
+# -- receive-side framing (restated, see aes_oracle.h) --------------------------------
+class _Scan(C.Structure):
+    _fields_ = [("frames", C.c_uint32), ("status", C.c_uint32), ("consumed", C.c_uint64)]
+
+
+SCAN_OK, SCAN_FULL, SCAN_TOO_LARGE, SCAN_BAD_MAGIC, SCAN_BAD_MTYPE, SCAN_BAD_LENGTH = range(6)
+
+
+def _scan(fn_name, data: bytes, max_len: int, max_frames: int):
+    lib = _plib()
+    fn = getattr(lib, fn_name)
+    fn.argtypes = [C.c_char_p, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
+                   C.POINTER(C.c_uint32), C.POINTER(_Scan)]
+    off = (C.c_uint64 * max(1, max_frames))()
+    ln = (C.c_uint32 * max(1, max_frames))()
+    res = _Scan()
+    fn(data, len(data), max_len, max_frames, off, ln, C.byref(res))
+    return [(int(off[i]), int(ln[i])) for i in range(res.frames)], int(res.status), int(res.consumed)
+
+
+def scan_package(data: bytes, max_len: int, max_frames: int):
+    """[(body_offset, n)], status, consumed for [htole32(n)][n] wire frames."""
+    return _scan("ao_scan_package", data, max_len, max_frames)
+
+
+def scan_stream(plain: bytes, max_len: int, max_frames: int):
+    """[(offset, message_length)], status, consumed for FPNN messages in stream plaintext."""
+    return _scan("ao_scan_stream", plain, max_len, max_frames)

@@ -7,17 +7,21 @@
 //   P <key> <iv> <data>            -> "<encrypt> <decrypt> <frame>"
 //   S <E|D> <key> <iv> <f1> .. <fn> -> "<out1> .. <outn>"      (StreamEncryptor)
 //   R <key> <iv> <data>            -> "<roundtrip-memcmp> <cipher>" (rijndael.h API)
+//   BP / BS ...                    as P / S, but queued on one fpnn::EncryptorBatch
+//   F                              flush the batch, then print the queued cases' lines
 // hex fields, "-" for an empty buffer.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "Encryptor.h"
+#include "EncryptorBatch.h"
 #include "rijndael.h"
 
 static std::vector<uint8_t> unhex(const std::string &h) {
@@ -37,13 +41,75 @@ static std::string hex(const uint8_t *p, size_t n) {
     return n ? s : "-";
 }
 
+// Cases queued on the batch: the encryptors and buffers live until the flush.
+struct Queued {
+    std::vector<std::unique_ptr<fpnn::Encryptor>> encs;
+    std::vector<std::unique_ptr<std::vector<uint8_t>>> bufs;
+    std::vector<std::unique_ptr<std::string>> strs;
+    // per case: a list of (buffer, length) or string outputs, printed space-separated
+    struct Out {
+        std::vector<uint8_t> *buf;
+        size_t n;
+        std::string *str;
+    };
+    std::vector<std::vector<Out>> lines;
+    std::vector<uint8_t> *keep(const std::vector<uint8_t> &v) {
+        bufs.emplace_back(new std::vector<uint8_t>(v));
+        bufs.back()->push_back(0);  // never empty: data() is a valid pointer
+        return bufs.back().get();
+    }
+};
+
 int main() {
     std::string line;
+    fpnn::EncryptorBatch batch;
+    Queued q;
     while (std::getline(std::cin, line)) {
         std::istringstream is(line);
         std::string kind;
         is >> kind;
-        if (kind == "P") {
+        if (kind == "BP") {  // PackageEncryptor calls through the batch
+            std::string k, v, d;
+            is >> k >> v >> d;
+            auto key = unhex(k), iv = unhex(v), data = unhex(d);
+            q.encs.emplace_back(new fpnn::PackageEncryptor(key.data(), key.size(), iv.data()));
+            fpnn::Encryptor *enc = q.encs.back().get();
+            std::vector<uint8_t> *src = q.keep(data), *a = q.keep(data), *b = q.keep(data);
+            batch.encrypt(enc, a->data(), src->data(), (int)data.size());
+            batch.decrypt(enc, b->data(), src->data(), (int)data.size());
+            q.strs.emplace_back(new std::string((const char *)data.data(), data.size()));
+            batch.encrypt(enc, q.strs.back().get());
+            q.lines.push_back({{a, data.size(), nullptr}, {b, data.size(), nullptr}, {nullptr, 0, q.strs.back().get()}});
+        } else if (kind == "BS") {  // StreamEncryptor calls through the batch
+            std::string dir, k, v, f;
+            is >> dir >> k >> v;
+            auto key = unhex(k), iv = unhex(v);
+            q.encs.emplace_back(new fpnn::StreamEncryptor(key.data(), key.size(), iv.data()));
+            fpnn::Encryptor *enc = q.encs.back().get();
+            std::vector<Queued::Out> outs;
+            while (is >> f) {
+                auto data = unhex(f);
+                std::vector<uint8_t> *src = q.keep(data), *o = q.keep(data);
+                if (dir == "E")
+                    batch.encrypt(enc, o->data(), src->data(), (int)data.size());
+                else
+                    batch.decrypt(enc, o->data(), src->data(), (int)data.size());
+                outs.push_back({o, data.size(), nullptr});
+            }
+            q.lines.push_back(outs);
+        } else if (kind == "F") {
+            batch.flush();
+            for (const auto &l : q.lines) {
+                std::string sep;
+                for (const auto &o : l) {
+                    std::cout << sep
+                              << (o.str ? hex((const uint8_t *)o.str->data(), o.str->size()) : hex(o.buf->data(), o.n));
+                    sep = " ";
+                }
+                std::cout << "\n";
+            }
+            q = Queued();
+        } else if (kind == "P") {
             std::string k, v, d;
             is >> k >> v >> d;
             auto key = unhex(k), iv = unhex(v), data = unhex(d);

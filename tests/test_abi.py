@@ -50,7 +50,11 @@ def test_cpp_encryptor_symbols_exported():
                 "fpnn::PackageEncryptor::decrypt(unsigned char*, unsigned char*, int)",
                 "fpnn::PackageEncryptor::encrypt(std::__cxx11::basic_string",
                 "fpnn::StreamEncryptor::encrypt(unsigned char*, unsigned char*, int)",
-                "fpnn::StreamEncryptor::decrypt(unsigned char*, unsigned char*, int)"):
+                "fpnn::StreamEncryptor::decrypt(unsigned char*, unsigned char*, int)",
+                "fpnn::EncryptorBatch::flush()",
+                "fpnn::EncryptorBatch::encrypt(fpnn::Encryptor*, std::__cxx11::basic_string",
+                "fpnn::EncryptorBatch::encrypt(fpnn::Encryptor*, unsigned char*, unsigned char*, int)",
+                "fpnn::EncryptorBatch::decrypt(fpnn::Encryptor*, unsigned char*, unsigned char*, int)"):
         assert sym in out, sym
 
 

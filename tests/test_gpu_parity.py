@@ -2,6 +2,7 @@
 reference's golden fixtures.  Bit-exact everywhere (byte work, no tolerance)."""
 import hashlib
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -12,6 +13,7 @@ import workloads as W
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
@@ -470,6 +472,46 @@ def test_cpp_dropin_matches_reference(golden, tmp_path):
     assert got == expect
 
 
+def test_cpp_encryptor_batch_matches_reference(golden, tmp_path, oracle):
+    """fpnn::EncryptorBatch (include/EncryptorBatch.h): the golden package/stream cases,
+    all queued on one batch across many encryptors and flushed at once, give the
+    reference's outputs; plus random many-connection cases checked against the oracle."""
+    from test_abi import build_dropin
+    exe = build_dropin(tmp_path)
+    lines, expect = [], []
+    for c in golden("package_cases.json"):
+        lines.append(f"BP {c['key']} {c['iv']} {c['in'] or '-'}")
+        expect.append(f"{c['encrypt'] or '-'} {c['decrypt'] or '-'} {c['frame']}")
+    for c in golden("stream_cases.json"):
+        lines.append(f"BS {'E' if c['encrypt'] else 'D'} {c['key']} {c['iv']} " +
+                     " ".join(f["in"] or "-" for f in c["frames"]))
+        expect.append(" ".join(f["out"] or "-" for f in c["frames"]))
+    lines.append("F")
+    rng = np.random.default_rng(31337)
+    for conn in range(300):  # a second flush: many connections, mixed key lengths
+        kl = (16, 24, 32)[conn % 3]
+        key, iv = rng.bytes(kl), rng.bytes(16)
+        if conn % 2:
+            data = rng.bytes(int(rng.integers(0, 3000)))
+            lines.append(f"BP {key.hex()} {iv.hex()} {data.hex() or '-'}")
+            expect.append(f"{oracle.package(key, iv, True, data).hex() or '-'} "
+                          f"{oracle.package(key, iv, False, data).hex() or '-'} {oracle.package_frame(key, iv, data).hex()}")
+        else:
+            enc = bool(conn % 4)
+            frames = [rng.bytes(int(rng.integers(0, 700))) for _ in range(int(rng.integers(1, 6)))]
+            outs, st_iv, st_pos = [], iv, 0
+            for f in frames:
+                o, st_iv, st_pos = oracle.cfb(key, enc, f, st_iv, st_pos)
+                outs.append(o.hex() or "-")
+            lines.append(f"BS {'E' if enc else 'D'} {key.hex()} {iv.hex()} " + " ".join(f.hex() or "-" for f in frames))
+            expect.append(" ".join(outs))
+    lines.append("F")
+    import subprocess
+    res = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout.strip().split("\n") == expect
+
+
 # --------------------------------------------------------------------------------------
 # many frames straight from host memory (fpnn_aes_package_host: gather -> pinned ->
 # pipelined H2D / kernel / D2H -> scatter)
@@ -544,3 +586,155 @@ def test_stream_host_frames(engine, oracle, keylen):
     for b, (f, _) in zip(bufs, frames):
         assert np.array_equal(b, f)
     assert np.array_equal(iv_d, iv_s) and np.array_equal(pos_d, pos_s)
+
+
+# --------------------------------------------------------------------------------------
+# receive side: wire framing on the device (fpnn_aes_package_recv / fpnn_aes_stream_recv)
+
+
+def _package_wire(rng, oracle, key, iv, nframes, max_len, partial, oversize):
+    wire, plain_bodies = b"", []
+    for j in range(nframes):
+        if oversize and j == 2:
+            wire += (max_len + 1 + int(rng.integers(0, 100))).to_bytes(4, "little") + rng.bytes(50)
+            return wire, plain_bodies
+        body = rng.bytes(int(rng.choice([0, 1, 16, int(rng.integers(0, max_len + 1))])))
+        plain_bodies.append(body)
+        wire += len(body).to_bytes(4, "little") + oracle.package(key, iv, True, body)
+    if partial:
+        body = rng.bytes(int(rng.integers(1, 600)))
+        full = len(body).to_bytes(4, "little") + oracle.package(key, iv, True, body)
+        wire += full[:int(rng.integers(1, len(full)))]
+    return wire, plain_bodies
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_package_recv_frames(engine, oracle, inplace):
+    import fpnn_amd
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as PO
+    rng = np.random.default_rng(2024 + inplace)
+    nconn, keylen, max_len, max_frames = 60, 32, 3000, 12
+    keys = rng.integers(0, 256, nconn * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nconn * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+    segs, bodies = [], []
+    for c in range(nconn):
+        k, v = keys[c * keylen:(c + 1) * keylen].tobytes(), ivs[c * 16:(c + 1) * 16].tobytes()
+        w, b = _package_wire(rng, oracle, k, v, int(rng.integers(0, 16)), max_len, partial=c % 3 == 1,
+                             oversize=c % 11 == 4)
+        segs.append(w)
+        bodies.append(b)
+    offs = np.cumsum([0] + [len(w) + 7 for w in segs[:-1]]).astype(np.int64)  # ragged, unaligned
+    total = int(offs[-1] + len(segs[-1]) + 7)
+    host = np.zeros(total, dtype=np.uint8)
+    for o, w in zip(offs, segs):
+        host[o:o + len(w)] = np.frombuffer(w, np.uint8)
+    inp = torch.from_numpy(host).to(DEV)
+    out = inp if inplace else torch.full_like(inp, 0xA5)
+    lens = torch.tensor([len(w) for w in segs], dtype=torch.int32, device=DEV)
+    slots = torch.arange(nconn, dtype=torch.int32, device=DEV)
+    foff, flen, scan = engine.package_recv(inp, out, nconn, ks, max_len, max_frames, in_off=torch.from_numpy(offs).to(DEV),
+                                           lens=lens, key_slot=slots)
+    torch.cuda.synchronize()
+    frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+    foff, flen, res = foff.cpu().numpy(), flen.cpu().numpy(), out.cpu().numpy()
+    for c in range(nconn):
+        exp_frames, exp_status, exp_consumed = PO.scan_package(segs[c], max_len, max_frames)
+        assert (frames[c], status[c], consumed[c]) == (len(exp_frames), exp_status, exp_consumed), c
+        for j, (bo, n) in enumerate(exp_frames):
+            assert (foff[c * max_frames + j], flen[c * max_frames + j]) == (bo, n)
+            got = res[offs[c] + bo: offs[c] + bo + n].tobytes()
+            assert got == bodies[c][j], (c, j)
+        if not inplace:  # nothing but complete bodies was written
+            mask = np.ones(len(segs[c]), bool)
+            for bo, n in exp_frames:
+                mask[bo:bo + n] = False
+            assert (res[offs[c]:offs[c] + len(segs[c])][mask] == 0xA5).all(), c
+    assert (status == PO.SCAN_FULL).any() and (status == PO.SCAN_TOO_LARGE).any()
+
+
+def _fpnn_message(rng, mtype, ss, psize):
+    hdr = b"FPNN" + bytes([1, 0x80, mtype, ss]) + psize.to_bytes(4, "little")
+    body = {1: psize + ss + 4, 2: psize + 4, 0: psize + ss}[mtype]
+    return hdr + rng.bytes(body)
+
+
+def test_stream_recv_messages(engine, oracle):
+    """Two receive calls per stream: the first ends mid-message, its plaintext tail is
+    carried in front of the second call's segment; malformed headers stop the scan with
+    the reference's verdict."""
+    import fpnn_amd
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as PO
+    rng = np.random.default_rng(99)
+    ns, keylen, max_len, max_frames = 40, 16, 6000, 64
+    keys = rng.integers(0, 256, ns * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, ns * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+    plains = []
+    for s in range(ns):
+        msgs = [_fpnn_message(rng, int(rng.integers(0, 3)), int(rng.integers(0, 30)), int(rng.integers(0, 2000)))
+                for _ in range(int(rng.integers(0, 12)))]
+        bad = s % 8
+        if bad == 1:
+            msgs.append(b"FPNX" + bytes(20))
+        elif bad == 2:
+            msgs.append(b"FPNN" + bytes([1, 0, 7, 0]) + bytes(8))
+        elif bad == 3:
+            msgs.append(b"FPNN" + bytes([1, 0, 0, 0]) + (0).to_bytes(4, "little"))  # BodyLen 0
+        elif bad == 4:
+            msgs.append(b"FPNN" + bytes([1, 0, 0, 0]) + (0x80000000).to_bytes(4, "little"))  # negative int
+        elif bad == 5:
+            msgs.append(_fpnn_message(rng, 2, 0, max_len))  # 12 + BodyLen > max_len
+        elif bad == 6:
+            msgs.append(b"FPNN" + bytes([1, 0, 2, 0]) + (0xFFFFFFFF).to_bytes(4, "little") + rng.bytes(3))  # wraps
+        plains.append(b"".join(msgs))
+    iv0 = ivs.reshape(ns, 16)
+    ciphers = [oracle.cfb(keys[s * keylen:(s + 1) * keylen].tobytes(), True, plains[s], iv0[s].tobytes(), 0)[0]
+               for s in range(ns)]
+    cut = [int(rng.integers(0, len(p) + 1)) for p in plains]
+    CARRY = max_len + 16
+    slot = CARRY + max(len(p) for p in plains) + 32
+    in_off = np.arange(ns, dtype=np.int64) * slot + CARRY
+    d_iv = torch.from_numpy(iv0.copy()).to(DEV)
+    d_pos = torch.zeros(ns, dtype=torch.int32, device=DEV)
+    slots = torch.arange(ns, dtype=torch.int32, device=DEV)
+    out = torch.zeros(ns * slot, dtype=torch.uint8, device=DEV)
+    carry = np.zeros(ns, dtype=np.int32)
+    for call in range(2):
+        parts = [c[:k] if call == 0 else c[k:] for c, k in zip(ciphers, cut)]
+        host = np.zeros(ns * slot, dtype=np.uint8)
+        for s, p in enumerate(parts):
+            host[in_off[s]:in_off[s] + len(p)] = np.frombuffer(p, np.uint8)
+        inp = torch.from_numpy(host).to(DEV)
+        foff, flen, scan = engine.stream_recv(inp, out, ns, ks, d_iv, d_pos, max_len, max_frames,
+                                              carry=torch.from_numpy(carry).to(DEV),
+                                              in_off=torch.from_numpy(in_off).to(DEV),
+                                              lens=torch.tensor([len(p) for p in parts], dtype=torch.int32, device=DEV),
+                                              key_slot=slots)
+        torch.cuda.synchronize()
+        frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+        foff, flen, res = foff.cpu().numpy(), flen.cpu().numpy(), out.cpu().numpy()
+        new_carry = np.zeros(ns, dtype=np.int32)
+        for s in range(ns):
+            start = 0 if call == 0 else cut[s] - int(carry[s])
+            region = plains[s][start:cut[s]] if call == 0 else plains[s][start:]
+            got_region = res[in_off[s] - carry[s]: in_off[s] - carry[s] + len(region)].tobytes()
+            assert got_region == region, (call, s)  # decrypted plaintext incl. the carried tail
+            exp_frames, exp_status, exp_consumed = PO.scan_stream(region, max_len, max_frames)
+            assert (frames[s], status[s], consumed[s]) == (len(exp_frames), exp_status, exp_consumed), (call, s)
+            for j, (o, n) in enumerate(exp_frames):
+                assert (foff[s * max_frames + j], flen[s * max_frames + j]) == (o, n)
+            if call == 0 and exp_status == PO.SCAN_OK:  # keep the incomplete message's plaintext
+                tail = region[exp_consumed:]
+                new_carry[s] = len(tail)
+                res[in_off[s] - len(tail): in_off[s]] = np.frombuffer(tail, np.uint8)
+        if call == 0:
+            out = torch.from_numpy(res).to(DEV)
+            carry = new_carry  # streams stopped by a bad header carry nothing
+    # after both calls the stream state equals the oracle's over the whole stream
+    for s in range(ns):
+        _, iv_end, pos_end = oracle.cfb(keys[s * keylen:(s + 1) * keylen].tobytes(), True, plains[s],
+                                        iv0[s].tobytes(), 0)
+        assert d_iv[s].cpu().numpy().tobytes() == iv_end and int(d_pos[s]) == pos_end

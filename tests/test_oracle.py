@@ -5,8 +5,13 @@
 2. Golden fixtures produced by the compiled reference (oracle/gen_golden.py).
 3. Live randomized comparison with oracle/_ref when it is built (this container).
 """
+import os
+import sys
+
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 FIPS_C1 = ("000102030405060708090a0b0c0d0e0f", "00112233445566778899aabbccddeeff", "69c4e0d86a7b0430d8cdb78070b4c55a")
 FIPS_C3 = ("000102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f", "00112233445566778899aabbccddeeff",
@@ -123,3 +128,34 @@ def test_port_speed_tracks_reference(oracle, ref_oracle):
             best[name] = min(best.get(name, 1e9), dt)
     ratio = best["reference"] / best["port"]  # port speed relative to the reference
     assert 0.6 < ratio < 1.7, ratio
+
+
+def test_framing_restatement_known_answers():
+    """The framing restatement on hand-built inputs whose verdicts follow from the
+    reference's code (core/EncryptedPackageReceiver.cpp:62-81,
+    core/EncryptedStreamReceiver.cpp:8-15,87-110, proto/FPMessage.cpp:27-44)."""
+    import struct
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as P
+    pk = struct.pack("<I", 3) + b"abc" + struct.pack("<I", 0) + struct.pack("<I", 5) + b"xy"
+    assert P.scan_package(pk, 100, 8) == ([(4, 3), (11, 0)], P.SCAN_OK, 11)
+    assert P.scan_package(pk, 100, 1) == ([(4, 3)], P.SCAN_FULL, 7)
+    assert P.scan_package(struct.pack("<I", 101) + bytes(200), 100, 8) == ([], P.SCAN_TOO_LARGE, 0)
+    assert P.scan_package(b"\x01\x00", 100, 8) == ([], P.SCAN_OK, 0)
+
+    def msg(mtype, ss, psize, body=None):
+        h = b"FPNN" + bytes([1, 0x80, mtype, ss]) + struct.pack("<I", psize)
+        return h + (bytes(body) if body is not None else b"")
+    two = msg(1, 3, 5, 5 + 3 + 4)   # TWOWAY: psize + ss + seq
+    ans = msg(2, 9, 5, 5 + 4)       # ANSWER: psize + seq (ss = status, not counted)
+    one = msg(0, 3, 5, 5 + 3)       # ONEWAY: psize + ss
+    st = two + ans + one
+    assert P.scan_stream(st, 1 << 23, 8) == ([(0, 24), (24, 21), (45, 20)], P.SCAN_OK, 65)
+    assert P.scan_stream(st[:-1], 1 << 23, 8) == ([(0, 24), (24, 21)], P.SCAN_OK, 45)
+    assert P.scan_stream(b"GET " + bytes(8), 1 << 23, 8)[1] == P.SCAN_BAD_MAGIC
+    assert P.scan_stream(msg(3, 0, 0), 1 << 23, 8)[1] == P.SCAN_BAD_MTYPE
+    assert P.scan_stream(msg(0, 0, 0), 1 << 23, 8)[1] == P.SCAN_BAD_LENGTH          # length 0 is rejected
+    assert P.scan_stream(msg(0, 0, 0x80000000), 1 << 23, 8)[1] == P.SCAN_BAD_LENGTH  # (int) < 0
+    assert P.scan_stream(msg(2, 0, 0xFFFFFFFF, 3), 1 << 23, 8) == ([(0, 15)], P.SCAN_OK, 15)  # uint32 wrap
+    assert P.scan_stream(msg(0, 0, 100), 111, 8)[1] == P.SCAN_TOO_LARGE             # 12 + 100 > 111
+    assert P.scan_stream(msg(0, 0, 100, 100), 112, 8) == ([(0, 112)], P.SCAN_OK, 112)
