@@ -81,17 +81,30 @@ struct Tables4 {
             return (J & 1) ? rotl32(v, 8) : v;
         }
     }
-    // S(byte j of w) at byte j: T0 entries hold S in bytes 1,2; T2 entries in bytes 0,3
+    // Raw final-round entry for byte j of w: S(byte j) sits at byte j of it (T0 entries
+    // hold S in bytes 1,2; T2 entries in bytes 0,3), the other bytes are junk.
     template <int J>
-    __device__ __forceinline__ uint32_t s(uint32_t w) const {
-        constexpr uint32_t mask = 0xffu << (8 * J);
+    __device__ __forceinline__ uint32_t sraw(uint32_t w) const {
         constexpr bool from_t2 = (J == 0 || J == 3);
         if (NT == 4) {
             const uint32_t base = from_t2 ? lb.lb1 : lb.lb0;
-            return lds_word(lds, __builtin_amdgcn_perm(base, w, sel(J)), 0) & mask;
+            return lds_word(lds, __builtin_amdgcn_perm(base, w, sel(J)), 0);
         } else {
-            return lds_word(lds, __builtin_amdgcn_perm(lb.lb0, w, sel(J)), from_t2 ? 128 : 0) & mask;
+            return lds_word(lds, __builtin_amdgcn_perm(lb.lb0, w, sel(J)), from_t2 ? 128 : 0);
         }
+    }
+    // S(byte j of w) at byte j, zero elsewhere
+    template <int J>
+    __device__ __forceinline__ uint32_t s(uint32_t w) const {
+        return sraw<J>(w) & (0xffu << (8 * J));
+    }
+    // Final-round output word: S(a.b0) | S(b.b1) << 8 | S(c.b2) << 16 | S(d.b3) << 24, ^ k.
+    // Two v_perm gather the four S bytes into disjoint halves, one v_bitop3 XORs them
+    // with the round key (3 VALU instead of 4 masks, 3 ORs and an XOR).
+    __device__ __forceinline__ uint32_t last(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+        const uint32_t lo = __builtin_amdgcn_perm(sraw<1>(b), sraw<0>(a), 0x0c0c0500u);
+        const uint32_t hi = __builtin_amdgcn_perm(sraw<3>(d), sraw<2>(c), 0x07020c0cu);
+        return xor3(lo, hi, k);
     }
 };
 
@@ -133,10 +146,10 @@ __device__ __forceinline__ uint4 aes_encrypt_block(uint4 in, const RoundKeys<NR>
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     uint4 o;
-    o.x = (T.template s<0>(s0) | T.template s<1>(s1) | T.template s<2>(s2) | T.template s<3>(s3)) ^ rk.k[4 * NR + 0];
-    o.y = (T.template s<0>(s1) | T.template s<1>(s2) | T.template s<2>(s3) | T.template s<3>(s0)) ^ rk.k[4 * NR + 1];
-    o.z = (T.template s<0>(s2) | T.template s<1>(s3) | T.template s<2>(s0) | T.template s<3>(s1)) ^ rk.k[4 * NR + 2];
-    o.w = (T.template s<0>(s3) | T.template s<1>(s0) | T.template s<2>(s1) | T.template s<3>(s2)) ^ rk.k[4 * NR + 3];
+    o.x = T.last(s0, s1, s2, s3, rk.k[4 * NR + 0]);
+    o.y = T.last(s1, s2, s3, s0, rk.k[4 * NR + 1]);
+    o.z = T.last(s2, s3, s0, s1, rk.k[4 * NR + 2]);
+    o.w = T.last(s3, s0, s1, s2, rk.k[4 * NR + 3]);
     return o;
 }
 

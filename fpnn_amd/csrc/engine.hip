@@ -384,7 +384,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         const uint64_t nb = ((uint64_t)b->uniform_len + 15) >> 4;
         const uint64_t total = nb * b->count;
         if (nb > 0 && total < (1ull << 32) && nb > 1) {
-            layout = LAYOUT_UNIFORM;
+            layout = (b->uniform_len & 15) == 0 && e->variant.dec_full ? LAYOUT_FULL : LAYOUT_UNIFORM;
             k.total_blocks = total;
             k.nb_uniform = (uint32_t)nb;
             k.magic = magic_for((uint32_t)nb);
@@ -414,7 +414,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // concurrently with K1 on the main stream.
     uint64_t bs_pkts = 0;
     const uint64_t nb_all = ((uint64_t)b->uniform_len + 15) >> 4;
-    if (layout == LAYOUT_UNIFORM && !inplace && km == KEY_UNIFORM && e->variant.bs_frac > 0.f &&
+    if (layout != LAYOUT_GENERAL && !inplace && km == KEY_UNIFORM && e->variant.bs_frac > 0.f &&
         (b->uniform_len & 511) == 0 && (b->stride & 15) == 0)
         bs_pkts = (uint64_t)((double)e->variant.bs_frac * (double)b->count + 0.5);
     if (bs_pkts > b->count) bs_pkts = b->count;
@@ -523,6 +523,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         const float f = (float)atof(v);
         e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
     }
+    if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;

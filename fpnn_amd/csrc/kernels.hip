@@ -31,7 +31,7 @@ struct Seg {
 template <int LAYOUT>
 __device__ __forceinline__ Seg get_seg(const KBatch &b, uint64_t s) {
     Seg g;
-    if (LAYOUT == LAYOUT_UNIFORM) {
+    if (LAYOUT != LAYOUT_GENERAL) {
         const uint64_t o = s * b.stride;
         g.in = b.in + o;
         g.out = b.out + o;
@@ -211,7 +211,7 @@ __device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32
         s0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s1), T.template t<2>(s2)), T.template t<3>(s3), rkq[r]);
     }
     const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
-    return (T.template s<0>(s0) | T.template s<1>(s1) | T.template s<2>(s2) | T.template s<3>(s3)) ^ rkq[NR];
+    return T.last(s0, s1, s2, s3, rkq[NR]);
 }
 
 typedef uint32_t __attribute__((aligned(1))) uint32_u;
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
 template <int LAYOUT>
 __device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64_t gblk, uint64_t total, uint64_t &s,
                                              uint32_t &bi) {
-    if (LAYOUT == LAYOUT_UNIFORM) {
+    if (LAYOUT != LAYOUT_GENERAL) {
         const uint32_t g32 = (uint32_t)(gblk < total ? gblk : total - 1);
         const uint32_t q = fast_div(g32, b.magic);
         s = q;
@@ -385,8 +385,14 @@ __device__ __forceinline__ void fetch_chunk(const KBatch &b, uint64_t c, uint64_
     ci.n0 = STREAM ? b.pos_snap[ci.s] : 0u;
     ci.slot = KM == KEY_UNIFORM ? 0u : ci.g.slot;
     ci.ivs = STREAM ? b.iv_snap[ci.s] : *reinterpret_cast<const uint4 *>(b.keys[ci.slot].iv);
-    ci.x = ci.valid ? load_cx(ci.g, ci.n0, ci.bi, ci.ivs) : make_uint4(0, 0, 0, 0);
     ci.xp0 = make_uint4(0, 0, 0, 0);
+    if (LAYOUT == LAYOUT_FULL) {  // whole blocks only: plain 16-B loads
+        ci.x = ci.valid ? load16(ci.g.in + 16ull * ci.bi) : make_uint4(0, 0, 0, 0);
+        if (lane == 0 && ci.bi != 0 && ci.valid)
+            ci.xp0 = INPLACE ? b.boundary[cc] : load16(ci.g.in + 16ull * (ci.bi - 1));
+        return;
+    }
+    ci.x = ci.valid ? load_cx(ci.g, ci.n0, ci.bi, ci.ivs) : make_uint4(0, 0, 0, 0);
     if (lane == 0 && ci.bi != 0 && ci.valid)
         ci.xp0 = INPLACE ? b.boundary[cc] : load_cx(ci.g, ci.n0, ci.bi - 1, ci.ivs);
 }
@@ -443,6 +449,10 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         for (int j = 0; j < U; j++) {
             const ChunkIn &c = ci[j];
             if (!c.valid) continue;
+            if (LAYOUT == LAYOUT_FULL) {
+                store16(c.g.out + 16ull * c.bi, c.x ^ ks[j]);
+                continue;
+            }
             store_cx(c.g, c.n0, c.bi, c.x ^ ks[j]);
             if (STREAM && (uint64_t)c.bi + 1 == seg_blocks(c.g.len, c.n0)) {  // last block: export (ivec, pos)
                 const uint32_t pos = (c.n0 + c.g.len) & 15u;
@@ -785,7 +795,9 @@ template <int NR, bool INPLACE, int NT>
 static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
 #define FPNN_DEC(L, K, S, NTX) \
     hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K)>), dim3(grid), dim3(kThreads), 0, st, b)
-    if (layout == LAYOUT_UNIFORM) {
+    if (layout == LAYOUT_FULL) {
+        FPNN_DEC(LAYOUT_FULL, KEY_UNIFORM, false, NT);
+    } else if (layout == LAYOUT_UNIFORM) {
         if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
     } else if (km == KEY_UNIFORM) {
         if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
@@ -827,7 +839,7 @@ static int grid_for(uint64_t items, int threads, int cap) {
 hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
                                 hipStream_t st) {
     const int grid = grid_for(nchunks, 256, 4096);
-    if (layout == LAYOUT_UNIFORM) {
+    if (layout != LAYOUT_GENERAL) {
         if (stream)
             hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, true>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
         else

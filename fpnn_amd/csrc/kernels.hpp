@@ -44,7 +44,10 @@ struct KBatch {
     const uint32_t *perm;
 };
 
-enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1 };
+// UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
+// uniform_len % 16 == 0 in package mode, so no block is partial (decrypt skips the
+// byte-granular head/tail paths).  GENERAL: offset/length/slot arrays.
+enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
 // Kernel build variant chosen per engine (defaults tuned on MI355X; overridable with
@@ -52,8 +55,9 @@ enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 struct Variant {
     float bs_frac = 0.0f;  // share of uniform package-decrypt packets given to the bitsliced K1b
     int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
-    int enc_chunk = 8;
-    int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c  // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
+    int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
+    int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
+    int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);

@@ -738,3 +738,52 @@ def test_stream_recv_messages(engine, oracle):
         _, iv_end, pos_end = oracle.cfb(keys[s * keylen:(s + 1) * keylen].tobytes(), True, plains[s],
                                         iv0[s].tobytes(), 0)
         assert d_iv[s].cpu().numpy().tobytes() == iv_end and int(d_pos[s]) == pos_end
+
+
+def test_udp_datagram_batches(engine, oracle):
+    """SURVEY.md 8f row 2, UDP v2 shape: MTU-sized datagrams of many connections (whole-
+    datagram package encryption, UDPEncryptor::packageEncrypt/Decrypt) and the
+    reinforced data stream (UDPEncryptor::dataEncrypt, a StreamEncryptor per
+    connection), as one device batch and as host frames."""
+    import fpnn_amd
+    rng = np.random.default_rng(1472)
+    nconn, n = 97, 3000
+    for keylen in (16, 32):  # non-reinforced / reinforced key length
+        keys = rng.integers(0, 256, nconn * keylen, dtype=np.uint8)
+        ivs = rng.integers(0, 256, nconn * 16, dtype=np.uint8)
+        ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+        lens = rng.choice([548, 1472, int(rng.integers(1, 1473))], n).astype(np.int32)
+        conn = rng.integers(0, nconn, n).astype(np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64))])
+        data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        exp = np.empty_like(data)
+        for i in range(n):
+            k = keys[conn[i] * keylen:(conn[i] + 1) * keylen].tobytes()
+            v = ivs[conn[i] * 16:(conn[i] + 1) * 16].tobytes()
+            exp[offs[i]:offs[i] + lens[i]] = np.frombuffer(
+                oracle.package(k, v, True, data[offs[i]:offs[i] + lens[i]].tobytes()), np.uint8)
+        d_in = torch.from_numpy(data).to(DEV)
+        d_out = torch.empty_like(d_in)
+        kw = dict(in_off=torch.from_numpy(offs).to(DEV), lens=torch.from_numpy(lens).to(DEV),
+                  key_slot=torch.from_numpy(conn).to(DEV))
+        engine.package_encrypt(d_in, d_out, n, ks, **kw)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_out.cpu().numpy(), exp)
+        dst = np.empty_like(data)
+        fr = np.zeros(n, dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
+        fr["src"] = data.ctypes.data + offs.astype(np.uint64)
+        fr["dst"] = dst.ctypes.data + offs.astype(np.uint64)
+        fr["len"] = lens
+        fr["key_slot"] = conn
+        engine.package_host_array(True, fr, ks)
+        assert np.array_equal(dst, exp)
+        # reinforced data stream: each connection's datagram payloads in send order
+        iv_s = ivs.reshape(nconn, 16).copy()
+        pos_s = np.zeros(nconn, dtype=np.uint32)
+        engine.stream_host_array(True, fr, ks, iv_s, pos_s)
+        st = {c: (ivs[c * 16:(c + 1) * 16].tobytes(), 0) for c in range(nconn)}
+        for i in range(n):
+            k = keys[conn[i] * keylen:(conn[i] + 1) * keylen].tobytes()
+            o, iv2, p2 = oracle.cfb(k, True, data[offs[i]:offs[i] + lens[i]].tobytes(), *st[conn[i]])
+            st[conn[i]] = (iv2, p2)
+            assert dst[offs[i]:offs[i] + lens[i]].tobytes() == o, i

@@ -3,7 +3,8 @@
 
 Each variant is an engine created under its own FPNN_AES_* environment; rounds
 alternate between variants; per-kernel HIP-event times are collected per round.
-Usage: python tools/ab.py [--rounds 8] [--variants "4,1 4,4 2,1 2,4"] [--keylen 32]
+Usage: python tools/ab.py [--rounds 8] [--variants "FPNN_AES_DEC_FULL=0;FPNN_AES_DEC_FULL=1"] [--keylen 32]
+(a variant is a comma-separated list of NAME=VALUE settings; variants are ';'-separated)
 """
 import argparse
 import json
@@ -23,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="4,1 4,4 2,1 2,4")
+    ap.add_argument("--variants", default="FPNN_AES_DEC_FULL=0;FPNN_AES_DEC_FULL=1")
     ap.add_argument("--packets", type=int, default=1 << 20)
     ap.add_argument("--length", type=int, default=1024)
     ap.add_argument("--keylen", type=int, default=32)
@@ -37,10 +38,15 @@ def main():
     cipher = torch.empty_like(plain)
     back = torch.empty_like(plain)
     variants = []
-    for v in args.variants.split():
-        t, c = v.split(",")
-        os.environ["FPNN_AES_TABLES"], os.environ["FPNN_AES_ENC_CHUNK"] = t, c
+    for v in args.variants.split(";"):
+        saved = dict(os.environ)
+        for kv in v.split(","):
+            if kv.strip():
+                k, val = kv.strip().split("=")
+                os.environ[k] = val
         e = fpnn_amd.Engine(0)
+        os.environ.clear()
+        os.environ.update(saved)
         ks = fpnn_amd.KeySet(e, key, len(key), iv)
         variants.append((v, e, ks))
     variants[0][1].fill_synthetic(plain, 2)
@@ -70,7 +76,7 @@ def main():
         out[v] = {k: {"median_ms": round(statistics.median(x), 4), "min_ms": round(min(x), 4),
                       "GiBs_median": round(P * L / (statistics.median(x) / 1e3) / 2**30, 1)}
                   for k, x in (("encrypt", enc), ("decrypt", dec))}
-    print(json.dumps({"P": P, "L": L, "keylen": args.keylen, "variants(tables,enc_chunk)": out}, indent=1))
+    print(json.dumps({"P": P, "L": L, "keylen": args.keylen, "variants": out}, indent=1))
 
 
 if __name__ == "__main__":

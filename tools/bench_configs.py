@@ -7,6 +7,7 @@ for DESIGN.md -- bench.py's single JSON line covers C2 only.
                                                       random 1 B..64 KiB frames = one call per frame round)
   C4  Zipf 64 B..64 KiB, 4 GiB, AES-256 package
   C5  65536 keys x 4 KiB AES-256, per-key IV
+  U1  1M x 1472 B UDP datagrams over 16384 connections, AES-128
 """
 import argparse
 import json
@@ -46,7 +47,7 @@ def gib(nbytes, sec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    ap.add_argument("--configs", default="C2,C3,C4,C5,U1")
     args = ap.parse_args()
     import fpnn_amd
     E, D = fpnn_amd.K_ENCRYPT, fpnn_amd.K_DECRYPT
@@ -165,6 +166,38 @@ def main():
                      "keyset_create_65536_keys_ms": round(kexp * 1e3, 2)}
         del a, b, r, ks2
         print(json.dumps({"C5": out["C5"]}), flush=True)
+
+    if "U1" in todo:
+        c = W.U1
+        P, L, NC = c["packets"], c["length"], c["connections"]
+        keys, ivs = W.many_keys(c)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), c["keylen"], ivs.tobytes())
+        slots = (torch.arange(P, dtype=torch.int32, device="cuda") % NC).contiguous()
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        kw = dict(stride=L, uniform_len=L, key_slot=slots)
+        we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, **kw), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
+        assert torch.equal(r, a)
+        src_h = a.cpu().numpy()
+        dst_h = np.empty_like(src_h)
+        fr = np.zeros(P, dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
+        fr["src"] = src_h.ctypes.data + np.arange(P, dtype=np.uint64) * L
+        fr["dst"] = dst_h.ctypes.data + np.arange(P, dtype=np.uint64) * L
+        fr["len"] = L
+        fr["key_slot"] = np.arange(P) % NC
+        eng.package_host_array(True, fr, ks)
+        t0 = time.perf_counter()
+        eng.package_host_array(True, fr, ks)
+        hb = time.perf_counter() - t0
+        assert np.array_equal(dst_h, b.cpu().numpy())
+        out["U1"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd),
+                     "encrypt_wall_GiBs": gib(P * L, we), "decrypt_wall_GiBs": gib(P * L, wd),
+                     "host_frames_encrypt_GiBs": gib(P * L, hb),
+                     "datagrams_per_s_encrypt_kernel": round(P / ke)}
+        del a, b, r
+        print(json.dumps({"U1": out["U1"]}), flush=True)
 
     if "C4" in todo:
         c = W.C4

@@ -26,7 +26,13 @@ C4 = dict(name="C4", mode="package", keylen=32, total_bytes=4 << 30, zipf_s=1.1,
           key_seed=1004, payload_seed=4, size_seed=4004, note="Zipf 64 B-64 KiB AES-256 package mode")
 C5 = dict(name="C5", mode="package", keylen=32, packets=65536, length=4096, key_seed=1005, payload_seed=5,
           note="65536 keys x 4 KiB AES-256, per-key IV")
-CONFIGS = {c["name"]: c for c in (C1, C2, C3, C4, C5)}
+# UDP v2 shape: MTU-sized datagrams (1472 = 1500 - IP - UDP headers,
+# core/UDP.v2/UDPIOBuffer.v2.h:14) of many connections, whole-datagram package encryption
+# (UDPEncryptor::packageEncrypt, core/UDP.v2/UDPCommon.v2.cpp:197-205), AES-128 (the
+# non-reinforced key length).  Datagram i belongs to connection i % connections.
+U1 = dict(name="U1", mode="package", keylen=16, packets=1 << 20, length=1472, connections=16384, key_seed=2001,
+          payload_seed=21, note="1M x 1472 B UDP datagrams over 16384 connections, AES-128 package mode")
+CONFIGS = {c["name"]: c for c in (C1, C2, C3, C4, C5, U1)}
 
 
 def _splitmix(x: np.ndarray) -> np.ndarray:
@@ -59,7 +65,7 @@ def single_key(cfg: dict):
 
 
 def many_keys(cfg: dict):
-    n = cfg.get("packets", cfg.get("streams"))
+    n = cfg.get("connections", cfg.get("packets", cfg.get("streams")))
     s = synth_bytes(48 * n, cfg["key_seed"]).reshape(n, 48)
     keys = np.ascontiguousarray(s[:, :cfg["keylen"]]).reshape(-1)
     ivs = np.ascontiguousarray(s[:, 32:48]).reshape(-1)
