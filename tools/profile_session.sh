@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/prof/$TAG
 mkdir -p "$OUT"
-BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --no-verify"}
+BENCH_ARGS=${BENCH_ARGS:-""}  # default: exactly the driver's `python bench.py`
 run() {  # run <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
@@ -21,6 +21,7 @@ if [ -n "$SLOW" ]; then
 fi
 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1 || true
 run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $BENCH_ARGS
+grep -E '^\{"metric"' "$OUT/trace.log" > "$OUT/bench_under_rocprof.json" || true
 PASSES=${PASSES:-"FETCH_SIZE|WRITE_SIZE|SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_LDS,SQ_INSTS_VALU,SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES|SQ_WAIT_INST_LDS,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,GRBM_GUI_ACTIVE"}
 i=0
 IFS="|" read -ra PGROUPS <<< "$PASSES"
