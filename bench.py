@@ -225,7 +225,7 @@ def main():
     # roofline for the dominant kernel: algorithmic bytes per launch
     alg_bytes = 2.0 * nbytes + 28.0 * P + 244.0 * 1
     kernels = {}
-    for name, n, ms in (("cfb_encrypt_chains", n_enc, ms_enc), ("cfb_decrypt_blocks", n_dec, ms_dec)):
+    for name, n, ms in (("cfb_encrypt_chains", n_enc, ms_enc), ("cfb_decrypt_dense", n_dec, ms_dec)):
         if n:
             avg_s = ms / n / 1e3
             ach = alg_bytes / avg_s / 1e9

@@ -153,6 +153,46 @@ __device__ __forceinline__ uint4 aes_encrypt_block(uint4 in, const RoundKeys<NR>
     return o;
 }
 
+// M independent blocks under one key, round-interleaved: round r of every block is
+// issued before round r+1 of any, in ONE basic block, so a wave has 16*M LDS lookups
+// in flight per round instead of 16 and the LDS pipe is fed while the VALU folds the
+// previous block's lookups.  (Separate aes_encrypt_block calls end up serialized by
+// the compiler when control flow sits between them.)
+template <int NR, int NT, int M>
+__device__ __forceinline__ void aes_encrypt_blocks(uint4 (&st)[M], const RoundKeys<NR> &rk, const Tables4<NT> &T) {
+    uint32_t s[M][4];
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+        s[m][0] = st[m].x ^ rk.k[0];
+        s[m][1] = st[m].y ^ rk.k[1];
+        s[m][2] = st[m].z ^ rk.k[2];
+        s[m][3] = st[m].w ^ rk.k[3];
+    }
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        uint32_t t[M][4];
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+                t[m][c] = xor3(xor3(T.template t<0>(s[m][c]), T.template t<1>(s[m][(c + 1) & 3]),
+                                    T.template t<2>(s[m][(c + 2) & 3])),
+                               T.template t<3>(s[m][(c + 3) & 3]), rk.k[4 * r + c]);
+        }
+#pragma unroll
+        for (int m = 0; m < M; m++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) s[m][c] = t[m][c];
+    }
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+        st[m].x = T.last(s[m][0], s[m][1], s[m][2], s[m][3], rk.k[4 * NR + 0]);
+        st[m].y = T.last(s[m][1], s[m][2], s[m][3], s[m][0], rk.k[4 * NR + 1]);
+        st[m].z = T.last(s[m][2], s[m][3], s[m][0], s[m][1], rk.k[4 * NR + 2]);
+        st[m].w = T.last(s[m][3], s[m][0], s[m][1], s[m][2], rk.k[4 * NR + 3]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 16-byte block helpers.  Interior blocks use (possibly unaligned) dwordx4 accesses;
 // edge blocks of a segment use byte accesses restricted to the segment so that no

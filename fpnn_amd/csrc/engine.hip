@@ -524,6 +524,11 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
     }
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
+    if (const char *v = getenv("FPNN_AES_DEC_IL")) {
+        const int c = atoi(v);
+        e->variant.dec_il = (c == 1 || c == 4) ? c : 2;
+    }
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;

@@ -16,6 +16,8 @@
 //   stream, not to memory; partial final blocks leave (ivec, pos) exactly as the
 //   reference's byte loop does.  Package mode is the special case n0 = 0,
 //   ivec = connection IV, state discarded (core/Encryptor.cpp:10-32).
+#include <type_traits>
+
 #include "aes_device.hpp"
 #include "kernels.hpp"
 
@@ -405,7 +407,7 @@ __device__ __forceinline__ uint4 readlane63(const uint4 &v) {
 // One wave step covers U consecutive 64-block chunks (U blocks per lane): the U loads go
 // out together, the U ciphers are independent (ILP for the LDS pipe), and a lane-0 block
 // whose predecessor sits in the previous chunk gets it from lane 63 by readlane.
-template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE, int NT, int U>
+template <int NR, int LAYOUT, int KM, bool STREAM, bool INPLACE, int NT, int U, int IL>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_blocks(KBatch b) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -425,14 +427,35 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
 #pragma unroll
         for (int j = 0; j < U; j++) fetch_chunk<LAYOUT, KM, STREAM, INPLACE>(b, st * U + j, total, lane, ci[j]);
         uint4 ks[U];
+        if (KM == KEY_UNIFORM) {
+            // All cipher inputs first (selects only, no lane-divergent branches), then
+            // the U ciphers round-interleaved in groups of IL in one basic block.
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const uint4 shr = wave_shr1(ci[j].x);  // C_{i-1} from the neighbouring lane
+                const uint4 l0 = j == 0 ? ci[0].xp0 : readlane63(ci[j - 1].x);
+                const uint4 xp = lane == 0 ? l0 : shr;
+                ks[j] = ci[j].bi == 0 ? ci[j].ivs : xp;
+            }
+#pragma unroll
+            for (int j = 0; j < U; j += IL) {
+                uint4 grp[IL];
+#pragma unroll
+                for (int m = 0; m < IL; m++) grp[m] = ks[j + m];
+                aes_encrypt_blocks<NR, NT, IL>(grp, rku, T);
+#pragma unroll
+                for (int m = 0; m < IL; m++) ks[j + m] = grp[m];
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                if (STREAM && ci[j].bi == 0 && ci[j].n0 != 0) ks[j] = ci[j].ivs;  // keystream already in the state
+        } else
 #pragma unroll
         for (int j = 0; j < U; j++) {
             uint4 xp = wave_shr1(ci[j].x);  // C_{i-1} from the neighbouring lane (all 64 lanes active)
             if (lane == 0) xp = j == 0 ? ci[0].xp0 : readlane63(ci[j - 1].x);
             const uint4 kin = ci[j].bi == 0 ? ci[j].ivs : xp;
-            if (KM == KEY_UNIFORM) {
-                ks[j] = aes_encrypt_block<NR, NT>(kin, rku, T);
-            } else {
+            {
                 const uint32_t slot0 = __builtin_amdgcn_readfirstlane(ci[j].slot);
                 const uint32_t my = ci[j].valid ? ci[j].slot : slot0;
                 if (__builtin_amdgcn_ballot_w64(my != slot0) == 0) {  // wave-uniform key: SGPR round keys
@@ -462,6 +485,134 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
             }
         }
     }
+}
+
+// K1d: K1 for DENSE whole-block uniform package batches -- packet i is the nb blocks
+// at in + i*16*nb (stride == length, length % 16 == 0, one key): the C2 shape and any
+// contiguous array of equal-size packets.  Block g then sits at in + 16*g, so a
+// 64-block chunk is one wave-uniform base address plus lane*16 (global_load saddr
+// form: no per-lane address arithmetic), and the CFB predecessor of lane 0 is a
+// wave-uniform value (the connection IV, lane 63 of the previous chunk by readlane,
+// or one scalar load).  C_{i-1} for lanes 1..63 is one DPP wave_shr:1 whose "old"
+// operand already holds lane 0's value.  Per 16-byte block this leaves ~16 VALU
+// besides the 340 of the cipher (K1: ~60).
+//   ALIGNED (nb % 64 == 0): packet starts fall only on lane 0, everything above is
+//   scalar.  Otherwise a lane whose block opens a packet (bi == 0) takes the IV by a
+//   per-lane select.
+template <bool ALIGNED>
+__device__ __forceinline__ uint32_t chunk_bi0(uint64_t c, uint32_t nb, uint64_t magic) {
+    // block-in-packet index of the chunk's first block (wave-uniform)
+    const uint32_t g = (uint32_t)(c << 6);  // total blocks < 2^32 (checked by the engine)
+    return g - nb * fast_div(g, magic);
+}
+
+template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_dense(KBatch b) {
+    static_assert(U % IL == 0, "IL-way interleave of U chunks");
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const uint32_t lane = threadIdx.x & 63u;
+    const RoundKeys<NR> rk = load_round_keys<NR>(b.keys);
+    const uint4 iv = *reinterpret_cast<const uint4 *>(b.keys[0].iv);
+    const uint64_t total = b.total_blocks;
+    const uint64_t nchunks = (total + 63) >> 6;
+    const uint64_t nsteps = (nchunks + U - 1) / U;
+    const uint32_t nb = b.nb_uniform;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t lane16 = lane * 16u;
+
+    // One step = U consecutive chunks.  FULL: all U chunks hold 64 valid blocks (no
+    // clamping, unconditional stores).  A StepBuf holds the step's ciphertext and lane
+    // 0's predecessor of its first chunk (the only fill that may need a load), loaded
+    // together.  With PF the step st + nwaves is loaded into the other buffer before
+    // this step's rounds (ping-pong, no register copies).
+    struct StepBuf {
+        uint4 x[U];
+        uint4 f;
+    };
+    auto load = [&](uint64_t st, StepBuf &D, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        // the fill first: the x loads are the newest, so a wait for them never covers
+        // more stores than necessary
+        const uint64_t c0 = FULL || st * U < nchunks ? st * U : nchunks - 1;
+        if (chunk_bi0<ALIGNED>(c0, nb, b.magic) == 0)  // wave-uniform
+            D.f = iv;
+        else
+            D.f = INPLACE ? b.boundary[c0] : *reinterpret_cast<const uint4 *>(b.in + (c0 << 10) - 16);
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t c = st * U + j;
+            const uint64_t cl = FULL || c < nchunks ? c : nchunks - 1;  // overhang: recompute the last chunk
+            uint32_t lo = lane16;
+            if (!FULL && !ALIGNED) {  // partial last chunk: clamp to the last block
+                const uint64_t left = total - (cl << 6);
+                if (left < 64) lo = min(lane, (uint32_t)left - 1u) * 16u;
+            }
+            D.x[j] = load16(b.in + (cl << 10) + lo);
+        }
+    };
+    auto step = [&](uint64_t st, StepBuf &X, StepBuf &NX, bool pref, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        if (!PF || !FULL) load(st, X, full_tag);
+        uint4 ks[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t c = st * U + j;
+            const uint64_t cl = FULL || c < nchunks ? c : nchunks - 1;
+            const uint32_t bi0 = chunk_bi0<ALIGNED>(cl, nb, b.magic);
+            // C_{i-1} of lane 0 (wave-uniform): IV at a packet start, else the block
+            // before the chunk (lane 63 of chunk j-1; for j = 0 loaded with the step)
+            const uint4 fill = j == 0 ? X.f : bi0 == 0 ? iv : readlane63(X.x[j - 1]);
+            uint4 kin = make_uint4(wave_shr1(X.x[j].x, fill.x), wave_shr1(X.x[j].y, fill.y),
+                                   wave_shr1(X.x[j].z, fill.z), wave_shr1(X.x[j].w, fill.w));
+            if (!ALIGNED) {  // lanes 1..63 that open a packet take the IV
+                const uint32_t r = bi0 + lane;
+                const uint32_t q = fast_div(r, b.magic);
+                if (lane != 0 && r == q * nb) kin = iv;
+            }
+            ks[j] = kin;
+        }
+        if (PF && FULL && pref) load(st + nwaves, NX, std::true_type{});
+#pragma unroll
+        for (int j = 0; j < U; j += IL) {
+            uint4 grp[IL];
+#pragma unroll
+            for (int m = 0; m < IL; m++) grp[m] = ks[j + m];
+            aes_encrypt_blocks<NR, NT, IL>(grp, rk, T);
+#pragma unroll
+            for (int m = 0; m < IL; m++) ks[j + m] = grp[m];
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t c = st * U + j;
+            if (!FULL) {
+                if (c >= nchunks) break;  // wave-uniform
+                if (!ALIGNED && (c << 6) + lane >= total) continue;
+            }
+            store16(b.out + (c << 10) + lane16, X.x[j] ^ ks[j]);
+        }
+    };
+    const uint64_t nfull = (total >> 6) / U;  // steps made of U whole chunks
+    uint64_t st = w0;
+    StepBuf ba, bb;
+    if (PF && st < nfull) {
+        load(st, ba, std::true_type{});
+        // Drain here: the loop header then only sees the back-edge state (prefetch
+        // loads followed by 4 stores) and waits with vmcnt(4), not vmcnt(0).
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        while (true) {
+            step(st, ba, bb, st + nwaves < nfull, std::true_type{});
+            st += nwaves;
+            if (st >= nfull) break;
+            step(st, bb, ba, st + nwaves < nfull, std::true_type{});
+            st += nwaves;
+            if (st >= nfull) break;
+        }
+    }
+    for (; st < nsteps; st += nwaves) step(st, ba, bb, false, std::false_type{});
 }
 
 // In-place decryption: save the ciphertext block that precedes every 64-block chunk
@@ -791,11 +942,23 @@ hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v,
 // (package mode, one key), 1 for stream / per-packet-key variants (they would spill).
 constexpr int dec_u(bool stream, int km) { return (!stream && km == KEY_UNIFORM) ? 4 : 1; }
 
-template <int NR, bool INPLACE, int NT>
-static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, hipStream_t st) {
+// Blocks round-interleaved per cipher call (divides dec_u): only the U = 4 variants vary.
+constexpr int dec_il(bool stream, int km, int il) { return dec_u(stream, km) == 4 ? il : 1; }
+
+template <int NR, bool INPLACE, int NT, int IL>
+static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int dense, int grid, hipStream_t st) {
 #define FPNN_DEC(L, K, S, NTX) \
-    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K)>), dim3(grid), dim3(kThreads), 0, st, b)
-    if (layout == LAYOUT_FULL) {
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K), dec_il(S, K, IL)>), dim3(grid), \
+                       dim3(kThreads), 0, st, b)
+    if (layout == LAYOUT_FULL && dense == 2 && b.nb_uniform % 64 == 0) {
+        hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, true, 4, IL, true>), dim3(grid), dim3(kThreads), 0, st, b);
+    } else if (layout == LAYOUT_FULL && dense == 2) {
+        hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, IL, true>), dim3(grid), dim3(kThreads), 0, st, b);
+    } else if (layout == LAYOUT_FULL && dense && b.nb_uniform % 64 == 0) {
+        hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, true, 4, IL, false>), dim3(grid), dim3(kThreads), 0, st, b);
+    } else if (layout == LAYOUT_FULL && dense) {
+        hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, IL, false>), dim3(grid), dim3(kThreads), 0, st, b);
+    } else if (layout == LAYOUT_FULL) {
         FPNN_DEC(LAYOUT_FULL, KEY_UNIFORM, false, NT);
     } else if (layout == LAYOUT_UNIFORM) {
         if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
@@ -811,11 +974,17 @@ template <int NR>
 static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, bool inplace, int grid,
                    hipStream_t st) {
     if (v.tables == 2) {
-        if (inplace) dec_launch<NR, true, 2>(b, layout, km, stream, grid, st);
-        else dec_launch<NR, false, 2>(b, layout, km, stream, grid, st);
+        if (inplace) dec_launch<NR, true, 2, 1>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+        else dec_launch<NR, false, 2, 1>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+    } else if (v.dec_il == 4) {
+        if (inplace) dec_launch<NR, true, 4, 4>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+        else dec_launch<NR, false, 4, 4>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+    } else if (v.dec_il == 2) {
+        if (inplace) dec_launch<NR, true, 4, 2>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+        else dec_launch<NR, false, 4, 2>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
     } else {
-        if (inplace) dec_launch<NR, true, 4>(b, layout, km, stream, grid, st);
-        else dec_launch<NR, false, 4>(b, layout, km, stream, grid, st);
+        if (inplace) dec_launch<NR, true, 4, 1>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
+        else dec_launch<NR, false, 4, 1>(b, layout, km, stream, b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0, grid, st);
     }
 }
 

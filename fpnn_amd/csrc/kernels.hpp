@@ -58,6 +58,8 @@ struct Variant {
     int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
+    int dec_il = 1;        // decrypt: blocks round-interleaved per cipher call (1, 2 or 4)
+    int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);

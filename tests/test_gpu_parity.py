@@ -255,6 +255,33 @@ def test_uniform_layout(engine, oracle, keylen, length):
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
+@pytest.mark.parametrize("length", [32, 48, 1008, 1024, 1040, 2048, 4096])
+@pytest.mark.parametrize("n", [64, 2501])
+def test_dense_layout(engine, oracle, keylen, length, n):
+    """Dense whole-block batches (stride == length, length % 16 == 0): the K1d decrypt
+    path -- chunk-aligned packets (length % 1 KiB == 0) and packet starts inside a
+    chunk, partial last chunk (n = 2501), in place and out of place.  The 64 guard
+    bytes after the batch must survive."""
+    rng = np.random.default_rng(length * 11 + keylen + n)
+    inp = rng.integers(0, 256, n * length + 64, dtype=np.uint8)
+    key, iv = rng.bytes(keylen), rng.bytes(16)
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, key, keylen, iv)
+    kb, ib = np.frombuffer(key, np.uint8).copy(), np.frombuffer(iv, np.uint8).copy()
+    for encrypt in (True, False):
+        exp = inp.copy()
+        oracle.package_batch(encrypt, inp, exp, n, stride=length, uniform_len=length, keys=kb, keylen=keylen,
+                             ivs=ib, threads=8)
+        for inplace in (False, True):
+            src = to_dev(inp)
+            dst = src if inplace else to_dev(inp)
+            fn = engine.package_encrypt if encrypt else engine.package_decrypt
+            fn(src, dst, n, ks, stride=length, uniform_len=length)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (encrypt, inplace)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
 def test_random_stream_batches(engine, oracle, keylen):
     """Many streams, several successive calls each with random lengths; outputs and the
     carried (iv, pos) state must follow the reference byte loop exactly."""

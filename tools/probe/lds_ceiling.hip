@@ -1,0 +1,165 @@
+// Compute-only ceiling of the T-table AES round function on one MI355X: the same LDS
+// image and round code as K1/K2 (aes_device.hpp), no HBM traffic.  Every lane runs
+// IL independent AES-256 chains for ITERS blocks each (output fed back as input), so
+// the measured blocks/s is what the LDS + VALU can do with nothing else in the way.
+// Also a pure lookup loop (perm + ds_read + xor, no AES structure) for the LDS rate.
+//   hipcc -O3 --offload-arch=gfx950 -I fpnn_amd/csrc tools/probe/lds_ceiling.hip -o tools/probe/lds_ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "aes_device.hpp"
+
+using namespace fpnn_aes;
+
+template <int IL>
+__global__ __launch_bounds__(1024, 1) void k_aes_only(const uint32_t *t0le, const DevKey *key, uint4 *out, int iters) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    lds_fill_tables<4>(lds4, t0le);
+    __syncthreads();
+    const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const RoundKeys<14> rk = load_round_keys<14>(key);
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 st[IL];
+#pragma unroll
+    for (int m = 0; m < IL; m++) st[m] = make_uint4(g, m, g * 7u, m * 13u);
+    for (int i = 0; i < iters; i++) aes_encrypt_blocks<14, 4, IL>(st, rk, T);
+    uint4 acc = st[0];
+#pragma unroll
+    for (int m = 1; m < IL; m++) acc = acc ^ st[m];
+    out[g] = acc;
+}
+
+// 16 lookups + 8 xor3 per "round", 4 independent words per lane (like one block).
+__global__ __launch_bounds__(1024, 1) void k_lookup_only(const uint32_t *t0le, uint32_t *out, int iters) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    lds_fill_tables<4>(lds4, t0le);
+    __syncthreads();
+    const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    uint32_t s0 = threadIdx.x, s1 = s0 * 3u, s2 = s0 * 5u, s3 = s0 * 9u;
+    for (int i = 0; i < iters; i++) {
+        const uint32_t t0 = xor3(xor3(T.t<0>(s0), T.t<1>(s1), T.t<2>(s2)), T.t<3>(s3), 1u);
+        const uint32_t t1 = xor3(xor3(T.t<0>(s1), T.t<1>(s2), T.t<2>(s3)), T.t<3>(s0), 2u);
+        const uint32_t t2 = xor3(xor3(T.t<0>(s2), T.t<1>(s3), T.t<2>(s0)), T.t<3>(s1), 3u);
+        const uint32_t t3 = xor3(xor3(T.t<0>(s3), T.t<1>(s0), T.t<2>(s1)), T.t<3>(s2), 4u);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s0 ^ s1 ^ s2 ^ s3;
+}
+
+
+// ---- LDS + vector-L1 (TCP) hybrid: R of the 16 lookups of a round go to a 4 KiB
+// global copy of T0..T3 through buffer_load (offset = byte << 2, table = imm offset).
+template <int J>
+__device__ __forceinline__ uint32_t tcp_t(__amdgpu_buffer_rsrc_t r, uint32_t w) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, ((w >> (8 * J)) & 0xffu) << 2, 0, 0) ;
+}
+
+template <int R, int J, int C>
+__device__ __forceinline__ uint32_t hyb(const Tables4<4> &T, __amdgpu_buffer_rsrc_t r, uint32_t w) {
+    // lookup slot k = J*4 + C taken by the TCP for k >= 16 - R (T3 first, then T2 ...)
+    constexpr int k = (3 - J) * 4 + C;
+    if (k < R) {
+        if (J == 0) return tcp_t<0>(r, w);
+        if (J == 1) return __builtin_amdgcn_raw_buffer_load_b32(r, ((w >> 8) & 0xffu) << 2, 1024, 0);
+        if (J == 2) return __builtin_amdgcn_raw_buffer_load_b32(r, ((w >> 16) & 0xffu) << 2, 2048, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(r, (w >> 24) << 2, 3072, 0);
+    }
+    return T.template t<J>(w);
+}
+
+template <int R, int IL>
+__global__ __launch_bounds__(1024, 1) void k_hybrid(const uint32_t *t0le, const uint32_t *gt, uint4 *out, int iters) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    lds_fill_tables<4>(lds4, t0le);
+    __syncthreads();
+    const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)gt, 0, 4096, 0x00020000);
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t s[IL][4];
+#pragma unroll
+    for (int m = 0; m < IL; m++) { s[m][0] = g; s[m][1] = g * 3u + m; s[m][2] = g * 5u; s[m][3] = g * 9u + m; }
+    for (int i = 0; i < iters; i++) {
+        uint32_t t[IL][4];
+#pragma unroll
+        for (int m = 0; m < IL; m++) {
+            t[m][0] = xor3(xor3(hyb<R, 0, 0>(T, rs, s[m][0]), hyb<R, 1, 0>(T, rs, s[m][1]), hyb<R, 2, 0>(T, rs, s[m][2])), hyb<R, 3, 0>(T, rs, s[m][3]), 1u);
+            t[m][1] = xor3(xor3(hyb<R, 0, 1>(T, rs, s[m][1]), hyb<R, 1, 1>(T, rs, s[m][2]), hyb<R, 2, 1>(T, rs, s[m][3])), hyb<R, 3, 1>(T, rs, s[m][0]), 2u);
+            t[m][2] = xor3(xor3(hyb<R, 0, 2>(T, rs, s[m][2]), hyb<R, 1, 2>(T, rs, s[m][3]), hyb<R, 2, 2>(T, rs, s[m][0])), hyb<R, 3, 2>(T, rs, s[m][1]), 3u);
+            t[m][3] = xor3(xor3(hyb<R, 0, 3>(T, rs, s[m][3]), hyb<R, 1, 3>(T, rs, s[m][0]), hyb<R, 2, 3>(T, rs, s[m][1])), hyb<R, 3, 3>(T, rs, s[m][2]), 4u);
+        }
+#pragma unroll
+        for (int m = 0; m < IL; m++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) s[m][c] = t[m][c];
+    }
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < IL; m++) acc = acc ^ make_uint4(s[m][0], s[m][1], s[m][2], s[m][3]);
+    out[g] = acc;
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+int main() {
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    uint32_t *d_t0;
+    DevKey *d_key;
+    uint4 *d_out;
+    CK(hipMalloc(&d_t0, 1024));
+    CK(hipMemcpy(d_t0, kTables.t0le, 1024, hipMemcpyHostToDevice));
+    DevKey hk{};
+    for (int i = 0; i < 60; i++) hk.rk[i] = 0x01020304u * (i + 1);
+    CK(hipMalloc(&d_key, sizeof(DevKey)));
+    CK(hipMemcpy(d_key, &hk, sizeof(DevKey), hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_out, (size_t)cus * 1024 * 16));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    const int iters = 2048;
+    auto run = [&](const char *name, auto launch, double blocks, double lookups) {
+        launch();
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int r = 0; r < 5; r++) {
+            CK(hipEventRecord(a));
+            launch();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            if (ms < best) best = ms;
+        }
+        // lookups/clk/CU at the nominal 2.4 GHz and implied clock if LDS ran at 32/clk
+        const double lps = lookups / (best * 1e-3);
+        printf("{\"kernel\": \"%s\", \"ms\": %.3f, \"payload_GBs\": %.1f, \"lookups_per_ns_per_cu\": %.2f, "
+               "\"lds_bound_clock_GHz_at_32_per_clk\": %.3f}\n",
+               name, best, blocks * 16 / (best * 1e-3) / 1e9, lps / 1e9 / cus, lps / cus / 32 / 1e9);
+    };
+    const double lanes = (double)cus * 1024;
+    run("aes_only_il1", [&] { hipLaunchKernelGGL(k_aes_only<1>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters); },
+        lanes * iters, lanes * iters * 224);
+    run("aes_only_il2", [&] { hipLaunchKernelGGL(k_aes_only<2>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters / 2); },
+        lanes * iters, lanes * iters * 224);
+    run("aes_only_il4", [&] { hipLaunchKernelGGL(k_aes_only<4>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters / 4); },
+        lanes * iters, lanes * iters * 224);
+    run("lookup_only", [&] { hipLaunchKernelGGL(k_lookup_only, dim3(cus), dim3(1024), 0, 0, d_t0, (uint32_t *)d_out, iters * 14); },
+        lanes * iters, lanes * iters * 224);
+
+    uint32_t *d_gt;
+    CK(hipMalloc(&d_gt, 4096));
+    {
+        uint32_t h[1024];
+        for (int k = 0; k < 4; k++)
+            for (int x = 0; x < 256; x++) h[256 * k + x] = (kTables.t0le[x] << (8 * k)) | (k ? kTables.t0le[x] >> (32 - 8 * k) : 0);
+        CK(hipMemcpy(d_gt, h, 4096, hipMemcpyHostToDevice));
+    }
+#define HYB(R, IL) run("hybrid_r" #R "_il" #IL, [&] { hipLaunchKernelGGL((k_hybrid<R, IL>), dim3(cus), dim3(1024), 0, 0, d_t0, d_gt, d_out, iters * 14 / IL); }, lanes * iters, lanes * iters * 224)
+    HYB(0, 2); HYB(1, 2); HYB(2, 2); HYB(3, 2); HYB(4, 2); HYB(6, 2); HYB(8, 2); HYB(16, 2);
+    HYB(2, 4); HYB(4, 4);
+    CK(hipGetLastError());
+    return 0;
+}
