@@ -389,6 +389,18 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.nb_uniform = (uint32_t)nb;
             k.magic = magic_for((uint32_t)nb);
         }
+    } else if (!stream && km == KEY_LANE && !b->in_off && !b->out_off && !b->len && e->variant.dec_dense &&
+               b->uniform_len && b->uniform_len % 1024 == 0 && b->stride == b->uniform_len) {
+        // dense packets of whole 64-block chunks, one key slot each (C5): K1d with a
+        // wave-uniform key per step
+        const uint64_t nb = b->uniform_len >> 4;
+        const uint64_t total = nb * b->count;
+        if (total < (1ull << 32)) {
+            layout = LAYOUT_FULL;
+            k.total_blocks = total;
+            k.nb_uniform = (uint32_t)nb;
+            k.magic = magic_for((uint32_t)nb);
+        }
     }
     if (layout == LAYOUT_GENERAL) {
         const uint64_t nwg = (b->count + 1023) / 1024;
@@ -525,10 +537,6 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     }
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
-    if (const char *v = getenv("FPNN_AES_DEC_IL")) {
-        const int c = atoi(v);
-        e->variant.dec_il = (c == 1 || c == 4) ? c : 2;
-    }
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;

@@ -46,7 +46,9 @@ struct KBatch {
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
 // uniform_len % 16 == 0 in package mode, so no block is partial (decrypt skips the
-// byte-granular head/tail paths).  GENERAL: offset/length/slot arrays.
+// byte-granular head/tail paths); with KEY_LANE, FULL also means dense (stride ==
+// uniform_len), uniform_len % 1024 == 0 and key_slot[] holding one slot per packet.
+// GENERAL: offset/length/slot arrays.
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
@@ -58,7 +60,6 @@ struct Variant {
     int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
-    int dec_il = 1;        // decrypt: blocks round-interleaved per cipher call (1, 2 or 4)
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
 };
 

@@ -281,6 +281,31 @@ def test_dense_layout(engine, oracle, keylen, length, n):
             assert np.array_equal(to_host(dst), exp), (encrypt, inplace)
 
 
+@pytest.mark.parametrize("length", [1024, 2048, 3072, 4096])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_dense_keyed_layout(engine, oracle, length, inplace):
+    """Dense packets of whole 1 KiB chunks with one key slot each (the C5 shape): K1d
+    with a wave-uniform key per step (U = 4, 2 or 1 chunks), mixed key lengths."""
+    rng = np.random.default_rng(length + inplace)
+    n, nkeys = 777, 97
+    inp = rng.integers(0, 256, n * length + 64, dtype=np.uint8)
+    for keylen in (16, 32):
+        keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+        ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+        slots = rng.integers(0, nkeys, n).astype(np.int32)
+        ks = keyset(engine, keys, keylen, ivs)
+        for encrypt in (True, False):
+            exp = inp.copy()
+            oracle.package_batch(encrypt, inp, exp, n, stride=length, uniform_len=length,
+                                 key_slot=slots.astype(np.uint32), keys=keys, keylen=keylen, ivs=ivs, threads=8)
+            src = to_dev(inp)
+            dst = src if inplace else to_dev(inp)
+            fn = engine.package_encrypt if encrypt else engine.package_decrypt
+            fn(src, dst, n, ks, stride=length, uniform_len=length, key_slot=to_dev(slots))
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (keylen, encrypt)
+
+
 @pytest.mark.parametrize("keylen", [16, 32])
 def test_random_stream_batches(engine, oracle, keylen):
     """Many streams, several successive calls each with random lengths; outputs and the

@@ -26,7 +26,8 @@ import workloads as W  # noqa: E402
 
 def timed(eng, which, fn, reps):
     import fpnn_amd
-    fn()  # warm
+    for _ in range(3):  # warm (clocks ramp; the first calls grow scratch buffers)
+        fn()
     torch.cuda.synchronize()
     eng.reset_stats()
     eng.set_timing(True)
