@@ -4,7 +4,7 @@
 // sizing, choosing the kernel variant (uniform vs general layout, uniform vs
 // per-packet keys, package vs stream, in-place) and queuing it on the engine's
 // HIP stream.  There is no CPU cipher in this library: every byte of payload is
-// transformed by the HIP kernels in kernels.hip.
+// transformed by the HIP kernels in k_encrypt.hip / k_decrypt.hip.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

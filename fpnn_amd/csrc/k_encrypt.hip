@@ -1,0 +1,342 @@
+// k_encrypt.hip -- CFB-128 encryption kernels for gfx950 (see segments.hpp for the
+// segment semantics and aes_device.hpp for the LDS T-table round function).
+//   K2  k_cfb_encrypt_chains : one lane per packet / stream chain.
+//        C_i = P_i ^ E(C_{i-1}) is serial inside a chain (base/rijndael.c:1176-1185),
+//        so parallelism is across packets (package mode) or streams (stream mode).
+//   K2c k_cfb_encrypt_coop   : one lane quad per chain (few / long / ragged chains).
+//   Both are persistent: workgroups walk the chains with a grid stride.
+#include "segments.hpp"
+
+namespace fpnn_aes {
+
+// ---------------------------------------------------------------------------
+// K2: encryption, one lane per chain.
+
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT, int CH>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_encrypt_chains(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+
+    RoundKeys<NR> rku;
+    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        RoundKeys<NR> rk;
+        if (KM == KEY_UNIFORM)
+            rk = rku;
+        else
+            rk = load_round_keys<NR>(key);
+
+        uint4 iv;
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = ld_state_iv(b.iv_state + 16 * s);
+            n = b.pos_state[s];
+        } else {
+            iv = *reinterpret_cast<const uint4 *>(key->iv);
+        }
+        const uint8_t *p = g.in;
+        uint8_t *q = g.out;
+        uint32_t rem = g.len;
+
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
+            q[0] = (uint8_t)rem;
+            q[1] = (uint8_t)(rem >> 8);
+            q[2] = (uint8_t)(rem >> 16);
+            q[3] = (uint8_t)(rem >> 24);
+            q += 4;
+        }
+
+        if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = (int)n, hi = (int)(n + take);
+            const uint4 o = load_bytes(p - n, lo, hi) ^ iv;
+            store_bytes(q - n, o, lo, hi);
+            iv = select_bytes(byte_mask(lo, hi), o, iv);
+            p += take;
+            q += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+
+        const uint32_t nfull = rem >> 4;
+        uint32_t i = 0;
+        if (CH > 1 && nfull >= CH) {
+            // CH-block chunks (CH*16 = 64 or 128 bytes): a chunk's loads and its stores
+            // each go out back to back, so every cache line is read and written whole
+            // while it is in L2; the next chunk's loads are in flight during this
+            // chunk's rounds.  (Two alternating buffers with unconditional loads, which
+            // avoid the copy and the conservative waits below, measured 1.3 % slower.)
+            uint4 a[CH], c[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = load16(p + 16 * j);
+            for (; i + CH <= nfull; i += CH) {
+                const bool more = i + 2 * CH <= nfull;
+                uint4 nx[CH];
+#pragma unroll
+                for (int j = 0; j < CH; j++) nx[j] = more ? load16(p + 16 * (CH + j)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ a[j];
+                    c[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < CH; j++) store16(q + 16 * j, c[j]);
+#pragma unroll
+                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                p += 16 * CH;
+                q += 16 * CH;
+            }
+        }
+        uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
+        for (; i < nfull; i++) {
+            const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
+            iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            store16(q, iv);
+            pt = pn;
+            p += 16;
+            q += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
+            const uint4 ks = aes_encrypt_block<NR, NT>(iv, rk, T);
+            const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
+            store_bytes(q, o, 0, (int)rem);
+            iv = select_bytes(byte_mask(0, (int)rem), o, ks);
+            n = rem;
+        }
+        if (STREAM) {
+            *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = iv;
+            b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2c: encryption, one lane QUAD per chain.  Lane q of the quad owns state column q:
+// per round it fetches the other three columns from its quad neighbours with DPP
+// quad_perm (VALU only), then does the 4 T-table lookups of its output column.  A
+// chain therefore issues 4 LDS reads per round instead of 16 -- 4x the lanes per
+// chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
+// lane instead of 60.  Used when chains are few (streams) or long/ragged.
+
+template <int SHIFT>  // value held by lane (q + SHIFT) & 3 of this lane's quad
+__device__ __forceinline__ uint32_t quad_from(uint32_t v) {
+    constexpr int ctl = ((0 + SHIFT) & 3) | (((1 + SHIFT) & 3) << 2) | (((2 + SHIFT) & 3) << 4) | (((3 + SHIFT) & 3) << 6);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctl, 0xf, 0xf, false);
+}
+
+template <int NR, int NT>
+__device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32_t *rkq, const Tables4<NT> &T) {
+    uint32_t s0 = sq ^ rkq[0];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
+        s0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s1), T.template t<2>(s2)), T.template t<3>(s3), rkq[r]);
+    }
+    const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
+    return T.last(s0, s1, s2, s3, rkq[NR]);
+}
+
+typedef uint32_t __attribute__((aligned(1))) uint32_u;
+
+// bytes [lo, hi) of this lane's word (word covers block bytes [4q, 4q+4))
+__device__ __forceinline__ uint32_t load_word_bytes(const uint8_t *p, int lo, int hi) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) w |= (uint32_t)p[j] << (8 * j);
+    return w;
+}
+
+__device__ __forceinline__ void store_word_bytes(uint8_t *p, uint32_t w, int lo, int hi) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) p[j] = (uint8_t)(w >> (8 * j));
+}
+
+__device__ __forceinline__ uint32_t word_mask(int lo, int hi) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) m |= (j >= lo && j < hi) ? (0xffu << (8 * j)) : 0u;
+    return m;
+}
+
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const int q = (int)(threadIdx.x & 3u);
+    constexpr int CH = 8;
+
+    const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; t < b.count; t += nquads) {
+        const uint64_t s = b.perm ? b.perm[t] : t;  // longest chains first (ragged batches)
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        uint32_t rkq[NR + 1];
+#pragma unroll
+        for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+
+        uint32_t iv;  // this lane's word of the 16-byte feedback register
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            n = b.pos_state[s];
+        } else {
+            iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
+        }
+        const uint8_t *p = g.in;
+        uint8_t *o = g.out;
+        uint32_t rem = g.len;
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
+            if (q == 0) store_word_bytes(o, rem, 0, 4);
+            o += 4;
+        }
+        const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+        if (STREAM && n != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
+            if (lo < hi) {
+                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
+                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (iv & ~m);
+            }
+            p += take;
+            o += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+        const uint32_t nfull = rem >> 4;
+        uint32_t i = 0;
+        if (nfull >= CH) {
+            uint32_t a[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo);
+            for (; i + CH <= nfull; i += CH) {
+                const bool more = i + 2 * CH <= nfull;
+                uint32_t nx[CH], c[CH];
+#pragma unroll
+                for (int j = 0; j < CH; j++) nx[j] = more ? *reinterpret_cast<const uint32_u *>(p + 16 * (CH + j) + wlo) : 0u;
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
+                    c[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
+#pragma unroll
+                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                p += 16 * CH;
+                o += 16 * CH;
+            }
+        }
+        for (; i < nfull; i++) {
+            const uint32_t pt = *reinterpret_cast<const uint32_u *>(p + wlo);
+            iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ pt;
+            *reinterpret_cast<uint32_u *>(o + wlo) = iv;
+            p += 16;
+            o += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const int lo = 0, hi = min((int)rem, wlo + 4) - wlo;
+            if (hi > lo) {
+                const uint32_t c = load_word_bytes(p + wlo, lo, hi) ^ ks;
+                store_word_bytes(o + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (ks & ~m);
+            } else {
+                iv = ks;
+            }
+            n = rem;
+        }
+        if (STREAM) {
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
+            if (q == 0) b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (runtime -> template dispatch)
+
+// Variant selection.  Per-packet keys need ~100 VGPRs of round keys, so they always
+// use the 4-table layout (one workgroup per CU); uniform-key variants take the
+// layout the engine asks for.
+template <int NR, int NT, int CH>
+static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads,
+                       hipStream_t st) {
+#define FPNN_ENC(L, K, S, NTX) \
+    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
+    } else {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false, 4);
+    }
+#undef FPNN_ENC
+}
+
+template <int NR>
+static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid, int threads,
+                   hipStream_t st) {
+    if (v.tables == 2) {
+        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, threads, st);
+    } else {
+        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, threads, st);
+        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, threads, st);
+    }
+}
+
+template <int NR>
+static void coop_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads, hipStream_t st) {
+#define FPNN_COOP(L, K, S) \
+    hipLaunchKernelGGL((k_cfb_encrypt_coop<NR, L, K, S, 4>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, false);
+    }
+#undef FPNN_COOP
+}
+
+hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                               int threads, hipStream_t st) {
+    switch (nrounds) {
+        case 10: coop_nr<10>(b, layout, km, stream, grid, threads, st); break;
+        case 12: coop_nr<12>(b, layout, km, stream, grid, threads, st); break;
+        case 14: coop_nr<14>(b, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }
+
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, int grid, int threads, hipStream_t st) {
+    switch (nrounds) {
+        case 10: enc_nr<10>(b, v, layout, km, stream, grid, threads, st); break;
+        case 12: enc_nr<12>(b, v, layout, km, stream, grid, threads, st); break;
+        case 14: enc_nr<14>(b, v, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace fpnn_aes

@@ -1,0 +1,281 @@
+// k_support.hip -- small gfx950 kernels around the cipher: the ragged decrypt block
+// map (scan + tile map), the longest-first encrypt ordering, device key expansion
+// and the synthetic payload generator.
+#include "segments.hpp"
+
+namespace fpnn_aes {
+
+// ---------------------------------------------------------------------------
+// General-layout block map: exclusive scan of per-segment block counts.
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+template <bool STREAM>
+__device__ __forceinline__ uint64_t nblocks_of(const KBatch &b, uint64_t s) {
+    if (s >= b.count) return 0;
+    const uint32_t len = b.len ? b.len[s] : b.uniform_len;
+    return seg_blocks(len, STREAM ? b.pos_snap[s] : 0u);
+}
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) {
+        const uint64_t add = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    total = sh[kScanThreads - 1];
+    const uint64_t incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(kScanThreads) void k_scan_local(KBatch b, uint64_t *bstart, uint64_t *wg_sums) {
+    __shared__ uint64_t sh[kScanThreads];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint64_t v[kScanItems], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = nblocks_of<STREAM>(b, base + k);
+        sum += v[k];
+    }
+    uint64_t total;
+    uint64_t run = block_exclusive_scan(sum, sh, total);
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        if (base + k < b.count) bstart[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 0) wg_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_sums(uint64_t *wg_sums, uint64_t nwg, uint64_t *bstart,
+                                                            uint64_t count, uint64_t *total_out) {
+    __shared__ uint64_t sh[kScanThreads];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nwg; base += kScanThreads) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nwg ? wg_sums[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(v, sh, tot);
+        if (i < nwg) wg_sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        bstart[count] = carry;
+        *total_out = carry;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_add(uint64_t *bstart, const uint64_t *wg_sums, uint64_t count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) bstart[i] += wg_sums[i / kScanTile];
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(kScanThreads) void k_tile_map(KBatch b, const uint64_t *bstart, uint64_t *tile_first,
+                                                           uint64_t nchunks) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0) tile_first[nchunks] = b.count ? b.count - 1 : 0;
+    if (s >= b.count) return;
+    const uint64_t nb = nblocks_of<STREAM>(b, s);
+    if (!nb) return;
+    const uint64_t first = bstart[s], last = first + nb - 1;
+    for (uint64_t t = (first + 63) >> 6; (t << 6) <= last; t++) tile_first[t] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Length ordering for ragged encrypt batches: counting sort into 128 descending
+// quarter-octave buckets of the block count (order inside a bucket is arbitrary; it
+// only affects speed, never results).
+
+constexpr int kBuckets = 128;
+
+template <bool STREAM>
+__device__ __forceinline__ uint32_t length_bucket(const KBatch &b, uint64_t s) {
+    const uint64_t nb = nblocks_of<STREAM>(b, s) + 1;  // >= 1
+    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
+    const int lz = 31 - __builtin_clz(x);
+    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
+    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);  // descending length
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts) {
+    __shared__ uint32_t h[kBuckets];
+    if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[length_bucket<STREAM>(b, s)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
+    __shared__ uint32_t sh[kBuckets];
+    const int t = threadIdx.x;
+    sh[t] = counts[t];
+    __syncthreads();
+    for (int off = 1; off < kBuckets; off <<= 1) {
+        const uint32_t add = t >= off ? sh[t - off] : 0u;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    cursor[t] = sh[t] - counts[t];  // exclusive
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm, uint64_t per_wg) {
+    __shared__ uint32_t cnt[kBuckets], base[kBuckets];
+    if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * per_wg;
+    const uint64_t hi = lo + per_wg < b.count ? lo + per_wg : b.count;
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) atomicAdd(&cnt[length_bucket<STREAM>(b, s)], 1u);
+    __syncthreads();
+    if (threadIdx.x < kBuckets) {
+        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]) : 0u;
+        cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
+        const uint32_t k = length_bucket<STREAM>(b, s);
+        perm[base[k] + atomicAdd(&cnt[k], 1u)] = (uint32_t)s;
+    }
+}
+
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st) {
+    uint32_t *cursor = counts + kBuckets;
+    hipError_t e = hipMemsetAsync(counts, 0, kBuckets * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)((b.count + 255) / 256 < 1024 ? (b.count + 255) / 256 : 1024);
+    if (stream)
+        hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
+    else
+        hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor);
+    const uint64_t per_wg = 4096;
+    const unsigned sgrid = (unsigned)((b.count + per_wg - 1) / per_wg);
+    if (stream)
+        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+    else
+        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Key expansion on the device (one lane per key; base/rijndael.c:712-799).
+
+__global__ __launch_bounds__(256) void k_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs,
+                                                     uint32_t count, const uint8_t *sbox_g, DevKey *out) {
+    __shared__ uint8_t sbox[256];
+    sbox[threadIdx.x] = sbox_g[threadIdx.x];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint8_t *key = keys + (uint64_t)i * keylen;
+    const int nk = (int)keylen / 4, nr = nk + 6;
+    uint32_t w[60];
+    for (int k = 0; k < nk; k++)
+        w[k] = ((uint32_t)key[4 * k] << 24) | ((uint32_t)key[4 * k + 1] << 16) | ((uint32_t)key[4 * k + 2] << 8) |
+               key[4 * k + 3];
+    auto sub = [&](uint32_t t) {
+        return ((uint32_t)sbox[t >> 24] << 24) | ((uint32_t)sbox[(t >> 16) & 0xff] << 16) |
+               ((uint32_t)sbox[(t >> 8) & 0xff] << 8) | sbox[t & 0xff];
+    };
+    uint32_t rcon = 1;
+    for (int k = nk; k < 4 * (nr + 1); k++) {
+        uint32_t t = w[k - 1];
+        if (k % nk == 0) {
+            t = sub((t << 8) | (t >> 24)) ^ (rcon << 24);
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0)) & 0xff;
+        } else if (nk > 6 && k % nk == 4) {
+            t = sub(t);
+        }
+        w[k] = w[k - nk] ^ t;
+    }
+    DevKey *d = out + i;
+    for (int k = 0; k < 60; k++) d->rk[k] = k < 4 * (nr + 1) ? __builtin_bswap32(w[k]) : 0u;
+    d->nrounds = (uint32_t)nr;
+    d->keylen = keylen;
+    d->reserved[0] = d->reserved[1] = 0;
+    for (int k = 0; k < 16; k++) d->iv[k] = ivs ? ivs[16 * (uint64_t)i + k] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic payload: counter-based splitmix64 (same definition as oracle/aes_oracle.c).
+
+__device__ __forceinline__ uint64_t synth_word(uint64_t seed, uint64_t i) {
+    uint64_t z = i + seed * 0xD1B54A32D192ED03ULL;
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t off) {
+    const uint64_t w0 = off >> 3, w1 = (off + nbytes + 7) >> 3;
+    const bool aligned = (((uintptr_t)dst - off) & 7) == 0;
+    for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w1;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = synth_word(seed, w);
+        const uint64_t lo = w << 3;
+        if (aligned && lo >= off && lo + 8 <= off + nbytes) {
+            *reinterpret_cast<uint64_t *>(dst + (lo - off)) = v;
+        } else {
+            for (int k = 0; k < 8; k++) {
+                const uint64_t a = lo + k;
+                if (a >= off && a < off + nbytes) dst[a - off] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,
+                                 hipStream_t st) {
+    const uint64_t nwg = (b.count + kScanTile - 1) / kScanTile;
+    if (nwg) {
+        if (stream)
+            hipLaunchKernelGGL((k_scan_local<true>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
+        else
+            hipLaunchKernelGGL((k_scan_local<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
+    }
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, st, wg_sums, nwg, bstart, b.count, total);
+    if (b.count)
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((b.count + kScanThreads - 1) / kScanThreads)),
+                           dim3(kScanThreads), 0, st, bstart, wg_sums, b.count);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first, uint64_t nchunks,
+                           hipStream_t st) {
+    const unsigned grid = (unsigned)((b.count + kScanThreads) / kScanThreads);
+    if (stream)
+        hipLaunchKernelGGL((k_tile_map<true>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
+    else
+        hipLaunchKernelGGL((k_tile_map<false>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
+                              const uint8_t *sbox, DevKey *out, hipStream_t st) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_expand_keys, dim3((count + 255) / 256), dim3(256), 0, st, keys, keylen, ivs, count, sbox, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, int grid,
+                                 hipStream_t st) {
+    if (!nbytes) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_synthetic, dim3(grid), dim3(256), 0, st, dst, nbytes, seed, byte_offset);
+    return hipGetLastError();
+}
+
+}  // namespace fpnn_aes

@@ -1,5 +1,5 @@
 // kernels.hpp -- internal launch interface between the C-ABI (engine.hip) and the
-// HIP kernels (kernels.hip).  Not installed; the public boundary is include/fpnn_aes.h.
+// HIP kernels (k_encrypt.hip, k_decrypt.hip, k_support.hip).  Not installed; the public boundary is include/fpnn_aes.h.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -1,0 +1,114 @@
+// segments.hpp -- device-side view of a batch shared by the encrypt and decrypt
+// kernels: segment lookup, stream-aligned block loads/stores with the reference's
+// exact (ivec, pos) byte semantics, and the uniform/general block locator.
+//
+//   Segments follow the reference's exact byte semantics (rijndael_cfb_encrypt's
+//   (ivec, pos) carry): a stream segment that starts at CFB position n0 != 0 first
+//   consumes the keystream bytes ivec[n0..15]; block alignment is relative to the
+//   stream, not to memory; partial final blocks leave (ivec, pos) exactly as the
+//   reference's byte loop does.  Package mode is the special case n0 = 0,
+//   ivec = connection IV, state discarded (core/Encryptor.cpp:10-32).
+#pragma once
+
+#include <type_traits>
+
+#include "aes_device.hpp"
+#include "kernels.hpp"
+
+namespace fpnn_aes {
+
+struct Seg {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t len;
+    uint32_t slot;
+};
+
+template <int LAYOUT>
+__device__ __forceinline__ Seg get_seg(const KBatch &b, uint64_t s) {
+    Seg g;
+    if (LAYOUT != LAYOUT_GENERAL) {
+        const uint64_t o = s * b.stride;
+        g.in = b.in + o;
+        g.out = b.out + o;
+        g.len = b.uniform_len;
+        g.slot = 0;
+    } else {
+        const uint64_t io = b.in_off ? b.in_off[s] : s * b.stride;
+        const uint64_t oo = b.out_off ? b.out_off[s] : io;
+        g.in = b.in + io;
+        g.out = b.out + oo;
+        g.len = b.len ? b.len[s] : b.uniform_len;
+        g.slot = b.key_slot ? b.key_slot[s] : 0u;
+    }
+    return g;
+}
+
+__device__ __forceinline__ uint4 ld_state_iv(const uint8_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+
+// Virtual (stream-aligned) block `bi` of a segment that starts at CFB position n0:
+// bytes j < n0 of block 0 come from the carried ivec (they are the ciphertext bytes
+// already consumed, base/rijndael.c:1182,1195), data bytes from the segment.
+__device__ __forceinline__ uint4 load_cx(const Seg &g, uint32_t n0, uint32_t bi, const uint4 &ivs) {
+    const int64_t vlo = 16 * (int64_t)bi;
+    const int lo = bi == 0 ? (int)n0 : 0;
+    const int64_t hi64 = (int64_t)n0 + g.len - vlo;
+    const int hi = hi64 > 16 ? 16 : (int)hi64;
+    const uint8_t *base = g.in + (vlo - (int64_t)n0);
+    if (lo == 0 && hi == 16) return load16(base);
+    uint4 d = load_bytes(base, lo, hi);
+    if (lo != 0) d = select_bytes(byte_mask(0, lo), ivs, d);
+    return d;
+}
+
+__device__ __forceinline__ void store_cx(const Seg &g, uint32_t n0, uint32_t bi, const uint4 &v) {
+    const int64_t vlo = 16 * (int64_t)bi;
+    const int lo = bi == 0 ? (int)n0 : 0;
+    const int64_t hi64 = (int64_t)n0 + g.len - vlo;
+    const int hi = hi64 > 16 ? 16 : (int)hi64;
+    uint8_t *base = g.out + (vlo - (int64_t)n0);
+    if (lo == 0 && hi == 16)
+        store16(base, v);
+    else
+        store_bytes(base, v, lo, hi);
+}
+
+__device__ __forceinline__ uint64_t seg_blocks(uint32_t len, uint32_t n0) {
+    return len ? ((uint64_t)n0 + len + 15) >> 4 : 0;
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64_t gblk, uint64_t total, uint64_t &s,
+                                             uint32_t &bi) {
+    if (LAYOUT != LAYOUT_GENERAL) {
+        const uint32_t g32 = (uint32_t)(gblk < total ? gblk : total - 1);
+        const uint32_t q = fast_div(g32, b.magic);
+        s = q;
+        bi = g32 - q * b.nb_uniform;
+    } else {
+        const uint64_t gg = gblk < total ? gblk : total - 1;
+        uint64_t lo = b.tile_first[c], hi = b.tile_first[c + 1];
+        while (lo < hi) {  // largest s in [lo, hi] with bstart[s] <= gg
+            const uint64_t mid = (lo + hi + 1) >> 1;
+            if (b.bstart[mid] <= gg)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        s = lo;
+        bi = (uint32_t)(gg - b.bstart[lo]);
+    }
+}
+
+__device__ __forceinline__ uint4 readlane63(const uint4 &v) {
+    return make_uint4(__builtin_amdgcn_readlane(v.x, 63), __builtin_amdgcn_readlane(v.y, 63),
+                      __builtin_amdgcn_readlane(v.z, 63), __builtin_amdgcn_readlane(v.w, 63));
+}
+
+inline int grid_for(uint64_t items, int threads, int cap) {
+    uint64_t g = (items + threads - 1) / threads;
+    if (g < 1) g = 1;
+    return (int)(g > (uint64_t)cap ? cap : g);
+}
+
+}  // namespace fpnn_aes
