@@ -181,6 +181,8 @@ struct fpnn_aes_engine {
     uint64_t cap_snap_pos = 0;
     uint32_t *d_perm = nullptr;  // ragged encrypt: longest-first order
     uint64_t cap_perm = 0;
+    uint32_t *d_next = nullptr;  // K2q work-queue counter (one word)
+    uint64_t cap_next = 0;
     uint32_t *d_buckets = nullptr;  // 2 x 128 counters
     uint64_t cap_buckets = 0;
     uint64_t *d_fr_off = nullptr;  // package receive: absolute body offset per frame slot
@@ -334,8 +336,15 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.perm = e->d_perm;
         }
         EventPair *ev;
+        // ragged and more chains than quads: a work queue balances them (with fewer
+        // chains every quad holds at most one and the grid stride is cheaper)
+        const bool queue = b->len && (e->variant.queue == 2 || (e->variant.queue == 1 && lanes > full_chip));
+        if (queue && (rc = grow(e->d_next, e->cap_next, 1))) return rc;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-        HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
+        if (queue)
+            HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));
+        else
+            HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
         return timing_end(e, ev);
     }
     // One lane per chain.  Workgroup size: the smallest power of two (>= one wave) that
@@ -530,6 +539,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
     if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
+    if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_BITSLICE_FRAC")) {
         const float f = (float)atof(v);
@@ -579,6 +589,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_snap_iv);
     (void)hipFree(e->d_snap_pos);
     (void)hipFree(e->d_perm);
+    (void)hipFree(e->d_next);
     (void)hipFree(e->d_buckets);
     (void)hipFree(e->d_fr_off);
     (void)hipFree(e->d_fr_slot);

@@ -3,8 +3,9 @@
 //   K2  k_cfb_encrypt_chains : one lane per packet / stream chain.
 //        C_i = P_i ^ E(C_{i-1}) is serial inside a chain (base/rijndael.c:1176-1185),
 //        so parallelism is across packets (package mode) or streams (stream mode).
-//   K2c k_cfb_encrypt_coop   : one lane quad per chain (few / long / ragged chains).
-//   Both are persistent: workgroups walk the chains with a grid stride.
+//   K2c k_cfb_encrypt_coop   : one lane quad per chain (few / long chains).
+//   K2q k_cfb_encrypt_queue  : K2c with a work queue (many ragged chains).
+//   All are persistent: workgroups walk the chains with a grid stride or the queue.
 #include "segments.hpp"
 
 namespace fpnn_aes {
@@ -268,6 +269,133 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
 }
 
 // ---------------------------------------------------------------------------
+// K2q: K2c's quad-per-chain cipher with a work queue instead of a grid stride.
+// Chains are visited longest first (perm[]); a quad that finishes its chain takes the
+// next one from a global counter at once, so lanes of a wave never wait for the
+// longest chain of their wave (greedy longest-processing-time scheduling).  The loop
+// body is one step of up to CH blocks of whatever chain each quad holds; the wave
+// leaves the loop when no quad has work.  Used for ragged batches (C4, U1 with mixed
+// sizes) where a static chain-to-lane assignment leaves most lanes idle.
+template <int NR, int KM, bool STREAM, int NT>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uint32_t *next) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const int q = (int)(threadIdx.x & 3u);
+    const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+    constexpr int CH = 8;
+    const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+
+    uint32_t rkq[NR + 1];
+    if (KM == KEY_UNIFORM) {
+#pragma unroll
+        for (int r = 0; r <= NR; r++) rkq[r] = b.keys[0].rk[4 * r + q];
+    }
+    // per-quad chain state
+    uint64_t s = 0;
+    const uint8_t *p = nullptr;
+    uint8_t *o = nullptr;
+    uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
+    bool active = false;
+
+    auto begin = [&](uint64_t t) {  // take chain perm[t] (t < count), run its head
+        s = b.perm ? b.perm[t] : t;
+        const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        if (KM != KEY_UNIFORM) {
+#pragma unroll
+            for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+        }
+        if (STREAM) {
+            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            n = b.pos_state[s];
+        } else {
+            iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
+            n = 0;
+        }
+        p = g.in;
+        o = g.out;
+        uint32_t rem = g.len;
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
+            if (q == 0) store_word_bytes(o, rem, 0, 4);
+            o += 4;
+        }
+        if (STREAM && n != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
+            if (lo < hi) {
+                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
+                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (iv & ~m);
+            }
+            p += take;
+            o += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+        nfull = rem >> 4;
+        tail = rem & 15u;
+        active = true;
+    };
+    auto finish = [&]() {  // partial final block and the stream state
+        if (tail) {
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const int hi = min((int)tail, wlo + 4) - wlo;
+            if (hi > 0) {
+                const uint32_t c = load_word_bytes(p + wlo, 0, hi) ^ ks;
+                store_word_bytes(o + wlo, c, 0, hi);
+                const uint32_t m = word_mask(0, hi);
+                iv = (c & m) | (ks & ~m);
+            } else {
+                iv = ks;
+            }
+            n = tail;
+        }
+        if (STREAM) {
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
+            if (q == 0) b.pos_state[s] = n;
+        }
+    };
+    // first chain: the quad's own index; later ones from the counter (which counts
+    // from nquads on)
+    const uint64_t t0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    if (t0 < b.count) begin(t0);
+    while (__builtin_amdgcn_ballot_w64(active) != 0) {
+        if (active && nfull > 0) {
+            // (prefetching the next chunk during this one's rounds measured no gain:
+            // 16 waves per CU already hide the load latency)
+            const uint32_t k = nfull < CH ? nfull : CH;
+            uint32_t a[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = j < (int)k ? *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo) : 0u;
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                if (j < (int)k) {
+                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
+                    a[j] = iv;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < CH; j++)
+                if (j < (int)k) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = a[j];
+            p += 16 * k;
+            o += 16 * k;
+            nfull -= k;
+        } else if (active) {
+            finish();
+            uint32_t t = 0;
+            if (q == 0) t = atomicAdd(next, 1u);
+            // broadcast the quad leader's ticket (DPP quad_perm 0,0,0,0)
+            t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x00, 0xf, 0xf, false) + (uint32_t)nquads;
+            active = false;
+            if (t < b.count) begin(t);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers (runtime -> template dispatch)
 
 // Variant selection.  Per-packet keys need ~100 VGPRs of round keys, so they always
@@ -313,6 +441,31 @@ static void coop_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int
         if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, false);
     }
 #undef FPNN_COOP
+}
+
+template <int NR>
+static void queue_nr(const KBatch &b, KeyMode km, bool stream, int grid, int threads, uint32_t *next, hipStream_t st) {
+#define FPNN_QUEUE(K, S) \
+    hipLaunchKernelGGL((k_cfb_encrypt_queue<NR, K, S, 4>), dim3(grid), dim3(threads), 0, st, b, next)
+    if (km == KEY_UNIFORM) {
+        if (stream) FPNN_QUEUE(KEY_UNIFORM, true); else FPNN_QUEUE(KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_QUEUE(KEY_LANE, true); else FPNN_QUEUE(KEY_LANE, false);
+    }
+#undef FPNN_QUEUE
+}
+
+hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool stream, int grid, int threads,
+                                uint32_t *next, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(next, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess) return err;
+    switch (nrounds) {
+        case 10: queue_nr<10>(b, km, stream, grid, threads, next, st); break;
+        case 12: queue_nr<12>(b, km, stream, grid, threads, next, st); break;
+        case 14: queue_nr<14>(b, km, stream, grid, threads, next, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,

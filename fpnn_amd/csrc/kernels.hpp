@@ -59,6 +59,7 @@ struct Variant {
     int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
     int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
+    int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
 };
@@ -98,6 +99,10 @@ hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v,
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st);
+// K2q: K2c with a work queue (a quad takes the next chain as soon as it is done);
+// next = one device word of scratch (zeroed here, on the stream).
+hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool stream, int grid, int threads,
+                                uint32_t *next, hipStream_t st);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
 // (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);

@@ -49,3 +49,25 @@ def engine():
     yield eng
     eng.sync()
     eng.close()
+
+
+@pytest.fixture(scope="session")
+def queue_engine():
+    """An engine that always uses the K2q work-queue encrypt for ragged batches
+    (by default it only does so when chains outnumber the chip's lane quads)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a machine without a HIP device")
+    import fpnn_amd
+    old = os.environ.get("FPNN_AES_QUEUE")
+    os.environ["FPNN_AES_QUEUE"] = "2"
+    try:
+        eng = fpnn_amd.Engine(0)
+    finally:
+        if old is None:
+            del os.environ["FPNN_AES_QUEUE"]
+        else:
+            os.environ["FPNN_AES_QUEUE"] = old
+    yield eng
+    eng.sync()
+    eng.close()

@@ -125,7 +125,9 @@ def test_golden_cfb_cases_stream_batch(engine, golden):
                 assert int(poso[i]) == c["pos_out"]
 
 
-def test_golden_package_cases(engine, golden):
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+def test_golden_package_cases(request, golden, eng_kind):
+    engine = request.getfixturevalue(eng_kind)
     import fpnn_amd
     cases = golden("package_cases.json")
     for c in cases:  # per-call drop-in surface
@@ -205,7 +207,9 @@ def make_ragged(rng, n, max_len, align_gap=True):
 @pytest.mark.parametrize("keylen", [16, 24, 32])
 @pytest.mark.parametrize("nkeys", [1, 7])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_random_package_batch(engine, oracle, keylen, nkeys, inplace):
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind):
+    engine = request.getfixturevalue(eng_kind)
     rng = np.random.default_rng(1000 * keylen + 10 * nkeys + inplace)
     n = 700
     lens, offs = make_ragged(rng, n, 3000)
@@ -307,9 +311,11 @@ def test_dense_keyed_layout(engine, oracle, length, inplace):
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_random_stream_batches(engine, oracle, keylen):
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+def test_random_stream_batches(request, oracle, keylen, eng_kind):
     """Many streams, several successive calls each with random lengths; outputs and the
     carried (iv, pos) state must follow the reference byte loop exactly."""
+    engine = request.getfixturevalue(eng_kind)
     rng = np.random.default_rng(500 + keylen)
     S = 333
     keys = rng.integers(0, 256, S * keylen, dtype=np.uint8)
