@@ -254,8 +254,13 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// Same with 0 into lane 0 (bound_ctrl: no "old" register to materialise).
+__device__ __forceinline__ uint32_t wave_shr1_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
+}
+
 __device__ __forceinline__ uint4 wave_shr1(const uint4 &v) {
-    return make_uint4(wave_shr1(v.x, 0u), wave_shr1(v.y, 0u), wave_shr1(v.z, 0u), wave_shr1(v.w, 0u));
+    return make_uint4(wave_shr1_zero(v.x), wave_shr1_zero(v.y), wave_shr1_zero(v.z), wave_shr1_zero(v.w));
 }
 
 // floor(g / d) for g, d < 2^32 with magic = ceil(2^64 / d)

@@ -126,10 +126,13 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 // chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
 // lane instead of 60.  Used when chains are few (streams) or long/ragged.
 
-template <int SHIFT>  // value held by lane (q + SHIFT) & 3 of this lane's quad
+// value held by lane (q + SHIFT) & 3 of this lane's quad.  bound_ctrl: every lane has a
+// source under quad_perm, so no "old" value is needed (update_dpp with old = 0 costs a
+// v_mov per call to materialise it -- 3 of the 12 VALU of a K2c round).
+template <int SHIFT>
 __device__ __forceinline__ uint32_t quad_from(uint32_t v) {
     constexpr int ctl = ((0 + SHIFT) & 3) | (((1 + SHIFT) & 3) << 2) | (((2 + SHIFT) & 3) << 4) | (((3 + SHIFT) & 3) << 6);
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctl, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctl, 0xf, 0xf, true);
 }
 
 template <int NR, int NT>
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
             uint32_t t = 0;
             if (q == 0) t = atomicAdd(next, 1u);
             // broadcast the quad leader's ticket (DPP quad_perm 0,0,0,0)
-            t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, 0x00, 0xf, 0xf, false) + (uint32_t)nquads;
+            t = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) + (uint32_t)nquads;
             active = false;
             if (t < b.count) begin(t);
         }
