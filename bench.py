@@ -121,7 +121,36 @@ def cpu_baseline(plain_host: np.ndarray, P: int, L: int, key: bytes, iv: bytes, 
                       f"{t:.2f} s wall = {t * threads:.1f} s of CPU work; matches GPU output: {ok}",
             "single_core": {"value": round(2.0 * n1 * L / t1 / 2**30, 4), "cores": 1,
                             "sample": f"first {n1} packets, {t1:.2f} s"},
+            "openssl_aesni": openssl_baseline(plain_host, P, L, key, iv, threads, gpu_cipher),
             "cpu_model": _cpu_model()}
+
+
+def openssl_baseline(plain_host, P, L, key, iv, threads, gpu_cipher, target_s=1.0):
+    """The stronger CPU comparator SURVEY.md 8(d) names: the same package-mode work
+    through the host's OpenSSL EVP cfb128 (AES-NI) -- oracle/libossl_cfb.so, built by
+    `make -C oracle ossl`.  None when it was not built."""
+    import ctypes as C
+    lib_path = os.path.join(ROOT, "oracle", "libossl_cfb.so")
+    if not os.path.exists(lib_path):
+        return None
+    lib = C.CDLL(lib_path)
+    f = lib.ossl_time_package_roundtrip
+    u8 = C.POINTER(C.c_uint8)
+    f.argtypes = [u8, u8, u8, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t, C.c_char_p, C.c_int, C.c_int]
+    f.restype = C.c_double
+    ptr = lambda a: a.ctypes.data_as(u8)  # noqa: E731
+    n = min(P, 65536)
+    tmp, out = np.empty(n * L, np.uint8), np.empty(n * L, np.uint8)
+    t = f(ptr(plain_host), ptr(tmp), ptr(out), n, L, key, len(key), iv, threads, 1)
+    if t <= 0:
+        return None
+    n = int(min(P, max(n, n * target_s / t)))
+    tmp, out = np.empty(n * L, np.uint8), np.empty(n * L, np.uint8)
+    t = f(ptr(plain_host), ptr(tmp), ptr(out), n, L, key, len(key), iv, threads, 1)
+    ok = bool(np.array_equal(tmp, gpu_cipher[:n * L])) and bool(np.array_equal(out, plain_host[:n * L]))
+    return {"value": round(2.0 * n * L / t / 2**30, 3), "unit": "GiB/s", "cores": threads,
+            "sample": f"{n} x {L} B packets, EVP_aes_256_cfb128 encrypt then decrypt per packet (IV reset per "
+                      f"packet), {threads} threads, {t:.2f} s; matches GPU output: {ok}"}
 
 
 def _cpu_model():

@@ -159,3 +159,30 @@ def test_framing_restatement_known_answers():
     assert P.scan_stream(msg(2, 0, 0xFFFFFFFF, 3), 1 << 23, 8) == ([(0, 15)], P.SCAN_OK, 15)  # uint32 wrap
     assert P.scan_stream(msg(0, 0, 100), 111, 8)[1] == P.SCAN_TOO_LARGE             # 12 + 100 > 111
     assert P.scan_stream(msg(0, 0, 100, 100), 112, 8) == ([(0, 112)], P.SCAN_OK, 112)
+
+
+def test_openssl_comparator_matches_oracle(oracle):
+    """The bench's OpenSSL EVP cfb128 comparator (oracle/openssl_cfb.c) computes the same
+    package-mode bytes as the restatement (so its timing is of the same work)."""
+    import ctypes as C
+    lib_path = os.path.join(ROOT, "oracle", "libossl_cfb.so")
+    if not os.path.exists(lib_path):
+        pytest.skip("oracle/libossl_cfb.so not built (make -C oracle ossl; needs libcrypto)")
+    lib = C.CDLL(lib_path)
+    f = lib.ossl_time_package_roundtrip
+    u8 = C.POINTER(C.c_uint8)
+    f.argtypes = [u8, u8, u8, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t, C.c_char_p, C.c_int, C.c_int]
+    f.restype = C.c_double
+    rng = np.random.default_rng(77)
+    for keylen, L in ((16, 1000), (24, 17), (32, 1024)):
+        n = 300
+        key, iv = rng.bytes(keylen), rng.bytes(16)
+        inp = rng.integers(0, 256, n * L, dtype=np.uint8)
+        tmp, out = np.empty_like(inp), np.empty_like(inp)
+        assert f(inp.ctypes.data_as(u8), tmp.ctypes.data_as(u8), out.ctypes.data_as(u8), n, L, key, keylen, iv,
+                 4, 1) > 0
+        exp = inp.copy()
+        oracle.package_batch(True, inp, exp, n, stride=L, uniform_len=L, keys=np.frombuffer(key, np.uint8).copy(),
+                             keylen=keylen, ivs=np.frombuffer(iv, np.uint8).copy())
+        assert np.array_equal(tmp, exp)
+        assert np.array_equal(out, inp)
