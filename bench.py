@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1], "C2"): 1 M x 1 KiB random payloads, AES-256
 package mode, one connection key/IV.  One step = encrypt the whole batch (K2,
-one lane per packet chain) + decrypt it back (K1, one lane per 16-byte block),
+one lane per packet chain) + decrypt it back (K1d, one lane per 16-byte block),
 inputs resident in HBM before timing starts.
 
 value = payload bytes processed by all ranks (P*L encrypted + P*L decrypted per
