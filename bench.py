@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time pinned H2D + kernels + D2H (for DESIGN.md)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL; default) or gloo (rehearsal)")
+    ap.add_argument("--workload", choices=["C2", "C4", "C5"], default="C2",
+                    help="C2 = the bench line (default); C4 / C5 = the BASELINE.json sharded configs")
     ap.add_argument("--only", choices=["encrypt", "decrypt"], default=None,
                     help="profiling aid: run one direction only (not a bench line)")
     return ap.parse_args()
@@ -69,6 +71,15 @@ def dist_setup(args):
         else:
             dist.init_process_group(args.dist_backend)
     return world, rank, dev
+
+
+def sum_over_ranks(value: int, world: int, device=None) -> int:
+    if world <= 1:
+        return int(value)
+    import torch.distributed as dist
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
 
 
 def barrier(world):
@@ -189,35 +200,100 @@ def pcie_rate(eng, ks, P, L, steps=3):
             "note": "host pinned -> H2D -> kernel -> D2H per direction, serialized on one stream", "roundtrip_ok": ok}
 
 
+def setup_c2(args, eng, world, rank):
+    """C2 (the bench line): P x L uniform packets per rank, one key; weak scaling."""
+    import fpnn_amd
+    from fpnn_amd.sharding import shard_range
+    P, L = args.packets, args.length
+    cfg = W.C2
+    key, iv = W.single_key(cfg)
+    ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+    # the global batch is world * P packets; this rank owns a contiguous packet range
+    # of it (no collective on the data path)
+    first, last = shard_range(P * world, world, rank)
+    assert last - first == P
+    plain = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+    eng.fill_synthetic(plain, cfg["payload_seed"], byte_offset=first * L)
+    kw = dict(stride=L, uniform_len=L)
+    desc = {"workload": "C2: 1M x 1 KiB AES-256 package-mode CFB encrypt+decrypt per GPU",
+            "packets_per_gpu": P, "payload_bytes": L, "key_bits": 256, "mode": "package",
+            "global_packets": P * world, "parallelism": f"packet-shard x{world}"}
+    digest = "C2" if (world == 1 and P == cfg["packets"] and L == cfg["length"]) else None
+    return dict(plain=plain, ks=ks, kw=kw, P=P, nkeys=1, scaling="weak", config=desc, digest=digest,
+                data="synthetic (counter splitmix64 payload, seed 2; key/IV from seed 1002)",
+                key=key, iv=iv, L=L, uniform=True)
+
+
+def setup_c4(args, eng, world, rank):
+    """C4: one global Zipf batch (64 B - 64 KiB, 4 GiB), byte-balanced contiguous packet
+    ranges per rank; strong scaling (the global batch is fixed)."""
+    import fpnn_amd
+    from fpnn_amd.sharding import shard_range
+    cfg = W.C4
+    sizes = W.zipf_sizes(cfg).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1])]).astype(np.int64)
+    first, last = shard_range(len(sizes), world, rank, sizes)
+    lo = int(offs[first])
+    nbytes = int(offs[last - 1] + sizes[last - 1] - lo) if last > first else 0
+    key, iv = W.single_key(cfg)
+    ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+    plain = torch.empty(max(1, nbytes), dtype=torch.uint8, device="cuda")
+    eng.fill_synthetic(plain[:nbytes], cfg["payload_seed"], byte_offset=lo, nbytes=nbytes)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda")  # noqa: E731
+    kw = dict(in_off=d(offs[first:last] - lo), lens=d(sizes[first:last].astype(np.int32)))
+    desc = {"workload": "C4: Zipf(1.1) 64 B-64 KiB packets, 4 GiB global, AES-256 package-mode encrypt+decrypt",
+            "packets_this_rank": last - first, "global_packets": len(sizes), "global_bytes": int(sizes.sum()),
+            "key_bits": 256, "mode": "package", "parallelism": f"byte-balanced packet-shard x{world}"}
+    return dict(plain=plain[:nbytes], ks=ks, kw=kw, P=last - first, nkeys=1, scaling="strong", config=desc,
+                digest=None, data="synthetic (splitmix64 payload seed 4, Zipf sizes seed 4004, key/IV seed 1004)",
+                key=key, iv=iv, L=None, uniform=False)
+
+
+def setup_c5(args, eng, world, rank):
+    """C5: 65 536 packets x 4 KiB, each with its own key and IV; the key table is
+    replicated, packets split evenly (8 GPUs x 8 192 keys); strong scaling."""
+    import fpnn_amd
+    from fpnn_amd.sharding import shard_range
+    cfg = W.C5
+    Pg, L = cfg["packets"], cfg["length"]
+    keys, ivs = W.many_keys(cfg)
+    ks = fpnn_amd.KeySet(eng, keys.tobytes(), cfg["keylen"], ivs.tobytes())
+    first, last = shard_range(Pg, world, rank)
+    P = last - first
+    plain = torch.empty(max(1, P * L), dtype=torch.uint8, device="cuda")
+    eng.fill_synthetic(plain[:P * L], cfg["payload_seed"], byte_offset=first * L, nbytes=P * L)
+    slots = torch.arange(first, last, dtype=torch.int32, device="cuda")
+    kw = dict(stride=L, uniform_len=L, key_slot=slots)
+    desc = {"workload": "C5: 65536 keys x 4 KiB AES-256 package-mode encrypt+decrypt, per-key IV",
+            "packets_this_rank": P, "global_packets": Pg, "payload_bytes": L, "key_bits": 256, "mode": "package",
+            "parallelism": f"packet-shard x{world} (key table replicated)"}
+    digest = "C5" if world == 1 else None
+    return dict(plain=plain[:P * L], ks=ks, kw=kw, P=P, nkeys=Pg, scaling="strong", config=desc, digest=digest,
+                data="synthetic (splitmix64 payload seed 5; keys/IVs seed 1005)", key=None, iv=None, L=L,
+                uniform=False)
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     import fpnn_amd
-    from fpnn_amd.sharding import max_over_ranks, shard_range
+    from fpnn_amd.sharding import max_over_ranks
 
-    P, L = args.packets, args.length
-    cfg = W.C2
-    key, iv = W.single_key(cfg)
     eng = fpnn_amd.Engine(local)  # queues on torch's current stream of this device
-    ks = fpnn_amd.KeySet(eng, key, len(key), iv)
-    nbytes = P * L
-    # weak scaling: the global batch is world * P packets; this rank owns a contiguous
-    # packet range of it (no collective on the data path)
-    first, last = shard_range(P * world, world, rank)
-    assert last - first == P
-    plain = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    eng.fill_synthetic(plain, cfg["payload_seed"], byte_offset=first * L)
+    job = {"C2": setup_c2, "C4": setup_c4, "C5": setup_c5}[args.workload](args, eng, world, rank)
+    plain, ks, kw, P = job["plain"], job["ks"], job["kw"], job["P"]
+    nbytes = plain.numel()
     cipher = torch.empty_like(plain)
     back = torch.empty_like(plain)
 
     def step():
         if args.only != "decrypt":
-            eng.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L)
+            eng.package_encrypt(plain, cipher, P, ks, **kw)
         if args.only != "encrypt":
-            eng.package_decrypt(cipher, back, P, ks, stride=L, uniform_len=L)
+            eng.package_decrypt(cipher, back, P, ks, **kw)
 
     if args.only == "decrypt":
-        eng.package_encrypt(plain, cipher, P, ks, stride=L, uniform_len=L)
+        eng.package_encrypt(plain, cipher, P, ks, **kw)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -236,25 +312,28 @@ def main():
     elapsed = max_over_ranks(elapsed, world, "cuda" if args.dist_backend == "nccl" else None)
     n_enc, ms_enc = eng.kernel_stats(fpnn_amd.K_ENCRYPT)
     n_dec, ms_dec = eng.kernel_stats(fpnn_amd.K_DECRYPT)
+    total_bytes = sum_over_ranks(nbytes, world, "cuda" if args.dist_backend == "nccl" else None)
 
     verify = {}
     if not args.no_verify:
         if args.only is None:
             verify["roundtrip_ok"] = bool(torch.equal(back, plain))
-        if rank == 0 and P == cfg["packets"] and L == cfg["length"]:
+        if rank == 0 and job["digest"]:
             with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
-                gold = json.load(f)["C2"]
+                gold = json.load(f)[job["digest"]]
             verify["cipher_sha256_matches_reference"] = \
                 hashlib.sha256(cipher.cpu().numpy()).hexdigest() == gold["cipher_sha256"]
 
     directions = 2 if args.only is None else 1
-    payload = float(directions) * nbytes * world * args.steps
+    payload = float(directions) * total_bytes * args.steps
     value = payload / elapsed / 2**30
 
     # roofline for the dominant kernel: algorithmic bytes per launch
-    alg_bytes = 2.0 * nbytes + 28.0 * P + 244.0 * 1
+    alg_bytes = 2.0 * nbytes + 28.0 * P + 244.0 * job["nkeys"]
     kernels = {}
-    for name, n, ms in (("cfb_encrypt_chains", n_enc, ms_enc), ("cfb_decrypt_dense", n_dec, ms_dec)):
+    names = {"C2": ("cfb_encrypt_chains", "cfb_decrypt_dense"), "C4": ("cfb_encrypt_queue", "cfb_decrypt_blocks"),
+             "C5": ("cfb_encrypt_coop", "cfb_decrypt_dense")}[args.workload]
+    for name, n, ms in ((names[0], n_enc, ms_enc), (names[1], n_dec, ms_dec)):
         if n:
             avg_s = ms / n / 1e3
             ach = alg_bytes / avg_s / 1e9
@@ -262,19 +341,19 @@ def main():
                              "payload_GiBs": round(nbytes / avg_s / 2**30, 2)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     ach = kernels[dom]["achieved_GBs"]
-    traffic = load_traffic(dom)
+    traffic = load_traffic(dom) if args.workload == "C2" else None  # the committed PMC summary is of C2
     roofline = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
                 "alg_bytes_per_launch": int(alg_bytes), "kernels": kernels}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and job["uniform"]:
         host_plain = plain.cpu().numpy()
-        cpu = cpu_baseline(host_plain, P, L, key, iv, args.cpu_seconds, cipher.cpu().numpy())
+        cpu = cpu_baseline(host_plain, P, job["L"], job["key"], job["iv"], args.cpu_seconds, cipher.cpu().numpy())
 
     extra = {}
-    if args.pcie and rank == 0:
-        extra["pcie_inclusive"] = pcie_rate(eng, ks, P, L)
+    if args.pcie and rank == 0 and job["uniform"]:
+        extra["pcie_inclusive"] = pcie_rate(eng, ks, P, job["L"])
 
     if rank == 0:
         line = {
@@ -286,13 +365,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": job["scaling"],
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (counter splitmix64 payload, seed 2; key/IV from seed 1002)",
-            "config": {"workload": "C2: 1M x 1 KiB AES-256 package-mode CFB encrypt+decrypt per GPU",
-                       "packets_per_gpu": P, "payload_bytes": L, "key_bits": 256, "mode": "package",
-                       "global_packets": P * world, "parallelism": f"packet-shard x{world}"},
+            "data": job["data"],
+            "config": job["config"],
             "roofline": roofline,
             "cpu_baseline": cpu,
             "verify": verify,

@@ -31,6 +31,26 @@ __global__ __launch_bounds__(1024, 1) void k_aes_only(const uint32_t *t0le, cons
     out[g] = acc;
 }
 
+// The 2-table image (T0, T2: 64 KiB) lets two 1024-thread workgroups share a CU
+// (8 waves per SIMD) at the price of rotations for T1 / T3.
+template <int IL>
+__global__ __launch_bounds__(1024, 2) void k_aes_only_nt2(const uint32_t *t0le, const DevKey *key, uint4 *out, int iters) {
+    __shared__ uint4 lds4[Lds<2>::kBytes / 16];
+    lds_fill_tables<2>(lds4, t0le);
+    __syncthreads();
+    const Tables4<2> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const RoundKeys<14> rk = load_round_keys<14>(key);
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 st[IL];
+#pragma unroll
+    for (int m = 0; m < IL; m++) st[m] = make_uint4(g, m, g * 7u, m * 13u);
+    for (int i = 0; i < iters; i++) aes_encrypt_blocks<14, 2, IL>(st, rk, T);
+    uint4 acc = st[0];
+#pragma unroll
+    for (int m = 1; m < IL; m++) acc = acc ^ st[m];
+    out[g] = acc;
+}
+
 // 16 lookups + 8 xor3 per "round", 4 independent words per lane (like one block).
 __global__ __launch_bounds__(1024, 1) void k_lookup_only(const uint32_t *t0le, uint32_t *out, int iters) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
@@ -145,6 +165,12 @@ int main() {
     run("aes_only_il2", [&] { hipLaunchKernelGGL(k_aes_only<2>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters / 2); },
         lanes * iters, lanes * iters * 224);
     run("aes_only_il4", [&] { hipLaunchKernelGGL(k_aes_only<4>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters / 4); },
+        lanes * iters, lanes * iters * 224);
+    CK(hipFree(d_out));
+    CK(hipMalloc(&d_out, (size_t)2 * cus * 1024 * 16));
+    run("aes_only_nt2_2wg", [&] { hipLaunchKernelGGL(k_aes_only_nt2<1>, dim3(2 * cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters / 2); },
+        lanes * iters, lanes * iters * 224);
+    run("aes_only_nt2_1wg", [&] { hipLaunchKernelGGL(k_aes_only_nt2<1>, dim3(cus), dim3(1024), 0, 0, d_t0, d_key, d_out, iters); },
         lanes * iters, lanes * iters * 224);
     run("lookup_only", [&] { hipLaunchKernelGGL(k_lookup_only, dim3(cus), dim3(1024), 0, 0, d_t0, (uint32_t *)d_out, iters * 14); },
         lanes * iters, lanes * iters * 224);
