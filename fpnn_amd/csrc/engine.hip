@@ -399,9 +399,10 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.magic = magic_for((uint32_t)nb);
         }
     } else if (!stream && km == KEY_LANE && !b->in_off && !b->out_off && !b->len && e->variant.dec_dense &&
-               b->uniform_len && b->uniform_len % 1024 == 0 && b->stride == b->uniform_len) {
-        // dense packets of whole 64-block chunks, one key slot each (C5): K1d with a
-        // wave-uniform key per step
+               b->uniform_len >= 32 && b->uniform_len % 16 == 0 && b->stride == b->uniform_len) {
+        // dense whole-block packets, one key slot each: K1d with a wave-uniform key per
+        // step when packets are whole 64-block chunks (C5), K1k with per-lane keys
+        // otherwise (U1)
         const uint64_t nb = b->uniform_len >> 4;
         const uint64_t total = nb * b->count;
         if (total < (1ull << 32)) {

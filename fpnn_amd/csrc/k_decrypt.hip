@@ -274,6 +274,73 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     for (; st < nsteps; st += nwaves) step(st, ba, bb, false, std::false_type{});
 }
 
+// K1k: K1d's dense addressing with one key slot per packet and packets that do NOT
+// fall on chunk boundaries (UDP datagrams of many connections: 1472-B packets, the U1
+// shape).  A chunk then mixes packets, so round keys are per lane (VGPRs, loaded per
+// step from the lane's key slot); everything else is K1d: packet / block-in-packet by
+// one multiply-high, no segment arrays, the step's ciphertext and key slots prefetched
+// one step ahead (ping-pong), lane 0's predecessor loaded with them.
+template <int NR, bool INPLACE, int NT>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_lanekey(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t total = b.total_blocks;
+    const uint64_t nchunks = (total + 63) >> 6;
+    const uint32_t nb = b.nb_uniform;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+
+    struct Buf {
+        uint4 x, f;  // this lane's block; lane 0's predecessor (when the chunk opens mid-packet)
+        uint32_t slot;
+    };
+    // lane's global block (clamped into the batch for the partial last chunk)
+    auto gblock = [&](uint64_t c) {
+        const uint64_t g = (c << 6) + lane;
+        return (uint32_t)(g < total ? g : total - 1);
+    };
+    auto load = [&](uint64_t c, Buf &D) {
+        const uint32_t bi0 = chunk_bi0<false>(c, nb, b.magic);
+        if (bi0 != 0)  // wave-uniform
+            D.f = INPLACE ? b.boundary[c] : *reinterpret_cast<const uint4 *>(b.in + (c << 10) - 16);
+        const uint32_t g = gblock(c);
+        D.x = load16(b.in + 16ull * g);
+        D.slot = b.key_slot[fast_div(g, b.magic)];
+    };
+    auto step = [&](uint64_t c, Buf &X, Buf &NX, bool pref) {
+        const uint32_t g = gblock(c);
+        const uint32_t bi = g - nb * fast_div(g, b.magic);
+        const RoundKeys<NR> rk = load_round_keys<NR>(b.keys + X.slot);
+        const uint4 ivl = *reinterpret_cast<const uint4 *>(b.keys[X.slot].iv);
+        // C_{i-1}: lane l-1's block (DPP); lane 0 gets its IV at a packet start, else the
+        // block before the chunk; a lane that opens a packet takes its own IV
+        uint4 kin = X.x;
+        const uint4 fill = bi == 0 ? ivl : X.f;
+        kin = make_uint4(wave_shr1(X.x.x, fill.x), wave_shr1(X.x.y, fill.y), wave_shr1(X.x.z, fill.z),
+                         wave_shr1(X.x.w, fill.w));
+        if (lane != 0 && bi == 0) kin = ivl;
+        if (pref) load(c + nwaves, NX);
+        const uint4 ks = aes_encrypt_block<NR, NT>(kin, rk, T);
+        if ((c << 6) + lane < total) store16(b.out + 16ull * ((c << 6) + lane), X.x ^ ks);
+    };
+    uint64_t c = w0;
+    if (c >= nchunks) return;
+    Buf ba, bb;
+    load(c, ba);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the loop header then sees only the back edge
+    while (true) {
+        step(c, ba, bb, c + nwaves < nchunks);
+        c += nwaves;
+        if (c >= nchunks) break;
+        step(c, bb, ba, c + nwaves < nchunks);
+        c += nwaves;
+        if (c >= nchunks) break;
+    }
+}
+
 // In-place decryption: save the ciphertext block that precedes every 64-block chunk
 // before any wave overwrites it.
 template <int LAYOUT, bool STREAM>
@@ -304,7 +371,9 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
 #define FPNN_DENSE(AL, U, PF, KEYED) \
     hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
-    if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet
+    if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
+        hipLaunchKernelGGL((k_cfb_decrypt_lanekey<NR, INPLACE, 4>), dim3(grid), dim3(kThreads), 0, st, b);
+    } else if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet
         const uint32_t nbc = b.nb_uniform / 64;
         if (nbc % 4 == 0) FPNN_DENSE(true, 4, true, true);
         else if (nbc % 2 == 0) FPNN_DENSE(true, 2, true, true);

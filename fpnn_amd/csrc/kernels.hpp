@@ -47,7 +47,8 @@ struct KBatch {
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
 // uniform_len % 16 == 0 in package mode, so no block is partial (decrypt skips the
 // byte-granular head/tail paths); with KEY_LANE, FULL also means dense (stride ==
-// uniform_len), uniform_len % 1024 == 0 and key_slot[] holding one slot per packet.
+// uniform_len) with key_slot[] holding one slot per packet (K1d keyed when
+// uniform_len % 1024 == 0, else K1k).
 // GENERAL: offset/length/slot arrays.
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };

@@ -285,11 +285,13 @@ def test_dense_layout(engine, oracle, keylen, length, n):
             assert np.array_equal(to_host(dst), exp), (encrypt, inplace)
 
 
-@pytest.mark.parametrize("length", [1024, 2048, 3072, 4096])
+@pytest.mark.parametrize("length", [32, 48, 1040, 1472, 1024, 2048, 3072, 4096])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_dense_keyed_layout(engine, oracle, length, inplace):
-    """Dense packets of whole 1 KiB chunks with one key slot each (the C5 shape): K1d
-    with a wave-uniform key per step (U = 4, 2 or 1 chunks), mixed key lengths."""
+    """Dense packets with one key slot each.  Whole 1 KiB chunks (the C5 shape): K1d
+    with a wave-uniform key per step (U = 4, 2 or 1 chunks); other lengths (the U1
+    shape): K1k with per-lane keys and packets starting inside chunks.  Mixed key
+    lengths, a partial last chunk (777 packets)."""
     rng = np.random.default_rng(length + inplace)
     n, nkeys = 777, 97
     inp = rng.integers(0, 256, n * length + 64, dtype=np.uint8)
