@@ -67,31 +67,34 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
         const uint32_t nfull = rem >> 4;
         uint32_t i = 0;
-        if (CH > 1 && nfull >= CH) {
-            // CH-block chunks (CH*16 = 64 or 128 bytes): a chunk's loads and its stores
+        // Per-lane AES-256 round keys (60 VGPRs) leave room for 4-block chunks only.
+        constexpr int C = (KM == KEY_LANE && NR == 14 && CH > 4) ? 4 : CH;
+        if (C > 1 && nfull >= C) {
+            // C-block chunks (C*16 = 64 or 128 bytes): a chunk's loads and its stores
             // each go out back to back, so every cache line is read and written whole
             // while it is in L2; the next chunk's loads are in flight during this
-            // chunk's rounds.  (Two alternating buffers with unconditional loads, which
-            // avoid the copy and the conservative waits below, measured 1.3 % slower.)
-            uint4 a[CH], c[CH];
+            // chunk's rounds.  Ciphertext overwrites the chunk's plaintext registers.
+            // (Two alternating buffers with unconditional loads, which avoid the copy
+            // and the conservative waits below, measured 1.3 % slower.)
+            uint4 a[C];
 #pragma unroll
-            for (int j = 0; j < CH; j++) a[j] = load16(p + 16 * j);
-            for (; i + CH <= nfull; i += CH) {
-                const bool more = i + 2 * CH <= nfull;
-                uint4 nx[CH];
+            for (int j = 0; j < C; j++) a[j] = load16(p + 16 * j);
+            for (; i + C <= nfull; i += C) {
+                const bool more = i + 2 * C <= nfull;
+                uint4 nx[C];
 #pragma unroll
-                for (int j = 0; j < CH; j++) nx[j] = more ? load16(p + 16 * (CH + j)) : make_uint4(0, 0, 0, 0);
+                for (int j = 0; j < C; j++) nx[j] = more ? load16(p + 16 * (C + j)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-                for (int j = 0; j < CH; j++) {
+                for (int j = 0; j < C; j++) {
                     iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ a[j];
-                    c[j] = iv;
+                    a[j] = iv;
                 }
 #pragma unroll
-                for (int j = 0; j < CH; j++) store16(q + 16 * j, c[j]);
+                for (int j = 0; j < C; j++) store16(q + 16 * j, a[j]);
 #pragma unroll
-                for (int j = 0; j < CH; j++) a[j] = nx[j];
-                p += 16 * CH;
-                q += 16 * CH;
+                for (int j = 0; j < C; j++) a[j] = nx[j];
+                p += 16 * C;
+                q += 16 * C;
             }
         }
         uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
