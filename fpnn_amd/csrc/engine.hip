@@ -173,6 +173,8 @@ struct fpnn_aes_engine {
     uint64_t cap_wgsums = 0;
     uint64_t *d_tile = nullptr;
     uint64_t cap_tile = 0;
+    uint64_t *d_mask = nullptr;  // contiguous ragged decrypt: segment-start bits per chunk
+    uint64_t cap_mask = 0;
     uint4 *d_boundary = nullptr;
     uint64_t cap_boundary = 0;
     uint4 *d_snap_iv = nullptr;  // stream-decrypt state snapshot
@@ -189,7 +191,7 @@ struct fpnn_aes_engine {
     uint64_t cap_fr_off = 0;
     uint32_t *d_fr_slot = nullptr;  // package receive: key slot per frame slot
     uint64_t cap_fr_slot = 0;
-    uint64_t *d_total = nullptr;
+    uint64_t *d_total = nullptr;  // [0] ragged block total, [1] non-contiguous segments
     uint64_t *h_total = nullptr;  // pinned
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
@@ -418,13 +420,25 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
         HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         uint64_t total = total_hint;
+        // Package mode, one key, and the host has to wait for the total anyway: also ask
+        // whether the segments are contiguous whole blocks, which K1d decrypts with
+        // dense addressing and a start-bit mask instead of a per-lane segment search.
+        const bool try_dense = !stream && km == KEY_UNIFORM && total == kNoHint && e->variant.dec_dense;
+        if (try_dense) HIP_TRY(launch_contig_check(k, e->d_total + 1, e->stream));
+        bool contiguous = false;
         if (total == kNoHint) {
-            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
             HIP_TRY(hipStreamSynchronize(e->stream));
-            total = *e->h_total;
+            total = e->h_total[0];
+            contiguous = try_dense && e->h_total[1] == 0;
         }
         if (!total) return FPNN_AES_OK;
         const uint64_t nchunks = (total + 63) >> 6;
+        if (contiguous) {
+            if ((rc = grow(e->d_mask, e->cap_mask, nchunks))) return rc;
+            HIP_TRY(launch_start_mask(k, e->d_bstart, e->d_mask, nchunks, e->stream));
+            k.start_mask = e->d_mask;
+        }
         if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
         HIP_TRY(launch_tile_map(k, stream, e->d_bstart, e->d_tile, nchunks, e->stream));
         k.total_blocks = total;
@@ -566,8 +580,8 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         err = hipMemcpy(e->d_tables, kTables.t0le, 1024, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1024, kTables.sbox, 256, hipMemcpyHostToDevice);
         if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
-        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), sizeof(uint64_t));
-        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), sizeof(uint64_t), 0);
+        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), 2 * sizeof(uint64_t));  // total, contiguity
+        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), 2 * sizeof(uint64_t), 0);
         if (err != hipSuccess) { rc = hip_fail(err, "alloc(total)"); break; }
     } while (0);
     if (rc) {
@@ -586,6 +600,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_bstart);
     (void)hipFree(e->d_wgsums);
     (void)hipFree(e->d_tile);
+    (void)hipFree(e->d_mask);
     (void)hipFree(e->d_boundary);
     (void)hipFree(e->d_snap_iv);
     (void)hipFree(e->d_snap_pos);

@@ -157,10 +157,11 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 //   KEYED: one key per packet (key_slot[] with the dense layout, chunk-aligned packets:
 //   the C5 shape).  A step's U chunks never straddle two packets (U divides nb/64), so
 //   the step's key is wave-uniform: slot and round keys are scalar loads per step.
-template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED>
+template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED, bool RAGGED = false>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_dense(KBatch b) {
     static_assert(U % IL == 0, "IL-way interleave of U chunks");
     static_assert(!KEYED || ALIGNED, "per-packet keys need chunk-aligned packets");
+    static_assert(!RAGGED || (!ALIGNED && !KEYED), "ragged batches use the start mask");
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -183,6 +184,15 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t lane16 = lane * 16u;
+    // RAGGED: contiguous segments from in_off[0] (out_off[0]); packet starts come from
+    // the per-chunk bit mask built by the scan (bit l of start_mask[c]: block 64c + l
+    // opens a segment)
+    const uint64_t off0 = RAGGED && b.in_off ? b.in_off[0] : 0;
+    const uint8_t *inb = b.in + off0;
+    uint8_t *outb = b.out + (RAGGED && b.out_off ? b.out_off[0] : off0);
+    auto starts = [&](uint64_t c) -> uint64_t { return ((__attribute__((address_space(4))) const uint64_t *)b.start_mask)[c]; };
+    // wave-uniform: does the chunk's first block open a packet?
+    auto opens = [&](uint64_t c) -> bool { return RAGGED ? (starts(c) & 1ull) != 0 : chunk_bi0<ALIGNED>(c, nb, b.magic) == 0; };
 
     // One step = U consecutive chunks.  FULL: all U chunks hold 64 valid blocks (no
     // clamping, unconditional stores).  A StepBuf holds the step's ciphertext and lane
@@ -198,8 +208,8 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         // the fill first: the x loads are the newest, so a wait for them never covers
         // more stores than necessary
         const uint64_t c0 = FULL || st * U < nchunks ? st * U : nchunks - 1;
-        if (chunk_bi0<ALIGNED>(c0, nb, b.magic) != 0)  // wave-uniform; at a packet start the IV is used
-            D.f = INPLACE ? b.boundary[c0] : *reinterpret_cast<const uint4 *>(b.in + (c0 << 10) - 16);
+        if (!opens(c0))  // wave-uniform; at a packet start the IV is used
+            D.f = INPLACE ? b.boundary[c0] : *reinterpret_cast<const uint4 *>(inb + (c0 << 10) - 16);
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const uint64_t c = st * U + j;
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 const uint64_t left = total - (cl << 6);
                 if (left < 64) lo = min(lane, (uint32_t)left - 1u) * 16u;
             }
-            D.x[j] = load16(b.in + (cl << 10) + lo);
+            D.x[j] = load16(inb + (cl << 10) + lo);
         }
     };
     auto step = [&](uint64_t st, StepBuf &X, StepBuf &NX, bool pref, auto full_tag) {
@@ -221,13 +231,16 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         for (int j = 0; j < U; j++) {
             const uint64_t c = st * U + j;
             const uint64_t cl = FULL || c < nchunks ? c : nchunks - 1;
-            const uint32_t bi0 = chunk_bi0<ALIGNED>(cl, nb, b.magic);
+            const uint64_t m = RAGGED ? starts(cl) : 0;
+            const uint32_t bi0 = RAGGED ? (uint32_t)(~m & 1ull) : chunk_bi0<ALIGNED>(cl, nb, b.magic);
             // C_{i-1} of lane 0 (wave-uniform): IV at a packet start, else the block
             // before the chunk (lane 63 of chunk j-1; for j = 0 loaded with the step)
             const uint4 fill = bi0 == 0 ? iv : j == 0 ? X.f : readlane63(X.x[j - 1]);
             uint4 kin = make_uint4(wave_shr1(X.x[j].x, fill.x), wave_shr1(X.x[j].y, fill.y),
                                    wave_shr1(X.x[j].z, fill.z), wave_shr1(X.x[j].w, fill.w));
-            if (!ALIGNED) {  // lanes 1..63 that open a packet take the IV
+            if (RAGGED) {  // lanes 1..63 that open a packet take the IV
+                if (lane != 0 && ((m >> lane) & 1ull)) kin = iv;
+            } else if (!ALIGNED) {
                 const uint32_t r = bi0 + lane;
                 const uint32_t q = fast_div(r, b.magic);
                 if (lane != 0 && r == q * nb) kin = iv;
@@ -251,7 +264,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 if (c >= nchunks) break;  // wave-uniform
                 if (!ALIGNED && (c << 6) + lane >= total) continue;
             }
-            store16(b.out + (c << 10) + lane16, X.x[j] ^ ks[j]);
+            store16(outb + (c << 10) + lane16, X.x[j] ^ ks[j]);
         }
     };
     const uint64_t nfull = (total >> 6) / U;  // steps made of U whole chunks
@@ -368,10 +381,15 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
 #define FPNN_DEC(L, K, S, NTX) \
     hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K), 1>), dim3(grid), dim3(kThreads), \
                        0, st, b)
+#define FPNN_DENSE_R() \
+    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, 1, true, false, true>), dim3(grid), \
+                       dim3(kThreads), 0, st, b)
 #define FPNN_DENSE(AL, U, PF, KEYED) \
     hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
-    if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
+    if (layout == LAYOUT_GENERAL && b.start_mask) {  // contiguous whole-block segments, one key
+        FPNN_DENSE_R();
+    } else if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
         hipLaunchKernelGGL((k_cfb_decrypt_lanekey<NR, INPLACE, 4>), dim3(grid), dim3(kThreads), 0, st, b);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet
         const uint32_t nbc = b.nb_uniform / 64;
@@ -391,6 +409,7 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
     } else {
         if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, false, 4);
     }
+#undef FPNN_DENSE_R
 #undef FPNN_DENSE
 #undef FPNN_DEC
 }

@@ -238,6 +238,50 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
     }
 }
 
+__device__ __forceinline__ uint64_t seg_off(const KBatch &b, uint64_t s, const uint64_t *off) {
+    return off ? off[s] : s * b.stride;
+}
+
+__global__ __launch_bounds__(256) void k_contig_check(KBatch b, uint64_t *bad) {
+    uint32_t n = 0;
+    const uint64_t in0 = seg_off(b, 0, b.in_off);
+    const uint64_t out0 = b.out_off ? b.out_off[0] : in0;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t len = b.len ? b.len[s] : b.uniform_len;
+        const uint64_t io = seg_off(b, s, b.in_off);
+        bool ok = (len & 15u) == 0;
+        if (s + 1 < b.count) ok = ok && seg_off(b, s + 1, b.in_off) == io + len;
+        if (b.out_off) ok = ok && b.out_off[s] - out0 == io - in0;
+        n += ok ? 0u : 1u;
+    }
+    if (n) atomicAdd(reinterpret_cast<unsigned long long *>(bad), (unsigned long long)n);
+}
+
+__global__ __launch_bounds__(256) void k_start_mask(KBatch b, const uint64_t *bstart, uint64_t *mask) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = bstart[s];
+        if (bstart[s + 1] > g)  // non-empty
+            atomicOr(reinterpret_cast<unsigned long long *>(mask + (g >> 6)), 1ull << (g & 63));
+    }
+}
+
+hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(bad, 0, sizeof(uint64_t), st);
+    if (err != hipSuccess) return err;
+    if (b.count) hipLaunchKernelGGL(k_contig_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, uint64_t nchunks,
+                             hipStream_t st) {
+    hipError_t err = hipMemsetAsync(mask, 0, nchunks * sizeof(uint64_t), st);
+    if (err != hipSuccess) return err;
+    if (b.count) hipLaunchKernelGGL(k_start_mask, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, mask);
+    return hipGetLastError();
+}
+
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,
                                  hipStream_t st) {
     const uint64_t nwg = (b.count + kScanTile - 1) / kScanTile;

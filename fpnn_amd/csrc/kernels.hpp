@@ -42,6 +42,9 @@ struct KBatch {
     const uint32_t *pos_snap;
     // encrypt of ragged batches: segment visiting order (longest first), or null
     const uint32_t *perm;
+    // decrypt of contiguous ragged batches (K1d ragged): bit l of start_mask[c] set when
+    // block 64c + l opens a segment; null otherwise
+    const uint64_t *start_mask;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
@@ -119,6 +122,13 @@ hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uin
 // ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
+// Package-mode decrypt of a general layout: counts the segments that break "contiguous
+// whole blocks" (len % 16 != 0, a gap or overlap to the next segment, out_off not a
+// shifted copy of in_off) into *bad (zeroed here).
+hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st);
+// start_mask[nchunks] (zeroed here): one bit per block that opens a non-empty segment.
+hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, uint64_t nchunks,
+                             hipStream_t st);
 hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first,
                            uint64_t nchunks, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,

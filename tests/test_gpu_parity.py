@@ -285,6 +285,47 @@ def test_dense_layout(engine, oracle, keylen, length, n):
             assert np.array_equal(to_host(dst), exp), (encrypt, inplace)
 
 
+@pytest.mark.parametrize("layout", ["contiguous", "shifted_out", "inplace", "one_gap", "odd_len"])
+def test_contiguous_ragged_decrypt(engine, oracle, layout):
+    """Ragged package batches whose segments are back to back in whole 16-byte blocks
+    (the C4 shape): the decrypt runs K1d with the segment-start mask.  'one_gap' and
+    'odd_len' break contiguity and must fall back to K1 with the same results."""
+    rng = np.random.default_rng(["contiguous", "shifted_out", "inplace", "one_gap", "odd_len"].index(layout) + 90)
+    n = 3001
+    lens = (rng.integers(0, 257, n) * 16).astype(np.int64)
+    lens[rng.random(n) < 0.05] = 0
+    lens[:3] = (16, 1024, 0)
+    if layout == "odd_len":
+        lens[1500] += 5
+    base = 48  # the batch does not start at the buffer start
+    offs = base + np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    if layout == "one_gap":
+        offs[2000:] += 32
+    total = int(offs[-1] + lens[-1] + 64)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    key, iv = rng.bytes(32), rng.bytes(16)
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, key, 32, iv)
+    kb, ib = np.frombuffer(key, np.uint8).copy(), np.frombuffer(iv, np.uint8).copy()
+    out_offs = offs + 96 if layout == "shifted_out" else offs
+    exp = np.zeros(total + 96, dtype=np.uint8) if layout == "shifted_out" else inp.copy()
+    oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=out_offs.astype(np.uint64),
+                         lens=lens.astype(np.uint32), keys=kb, keylen=32, ivs=ib, threads=8)
+    src = to_dev(inp)
+    if layout == "inplace":
+        dst = src
+    elif layout == "shifted_out":
+        dst = dev_u8(total + 96)
+    else:
+        dst = to_dev(inp)
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+    if layout == "shifted_out":
+        kw["out_off"] = to_dev(out_offs)
+    engine.package_decrypt(src, dst, n, ks, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(dst), exp)
+
+
 @pytest.mark.parametrize("length", [32, 48, 1040, 1472, 1024, 2048, 3072, 4096])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_dense_keyed_layout(engine, oracle, length, inplace):
