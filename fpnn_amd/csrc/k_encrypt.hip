@@ -138,16 +138,34 @@ __device__ __forceinline__ uint32_t quad_from(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctl, 0xf, 0xf, true);
 }
 
+// XOR of a and the value b holds in lane (q + SHIFT) & 3: one v_xor_b32 with a DPP
+// quad_perm source (the mov_dpp folds into the xor).
+template <int SHIFT>
+__device__ __forceinline__ uint32_t xor_quad_from(uint32_t a, uint32_t b) {
+    return a ^ quad_from<SHIFT>(b);
+}
+
+// Round structure: lane q looks up ITS OWN four bytes -- T0[b0] feeds output column q,
+// T1[b1] column q-1, T2[b2] column q-2, T3[b3] column q-3 -- and the quad then sums
+// the contributions with DPP-sourced XORs.  Per lane and round: 4 v_perm + 4 ds_read
+// + 3 DPP ops + 1 v_bitop3 = 8 VALU, and every DPP operand is an LDS result or a round
+// key, never a fresh VALU result, so no hazard wait states (moving the state words to
+// the neighbours first costs 9 VALU plus an s_nop per round).
 template <int NR, int NT>
 __device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32_t *rkq, const Tables4<NT> &T) {
     uint32_t s0 = sq ^ rkq[0];
 #pragma unroll
     for (int r = 1; r < NR; r++) {
-        const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
-        s0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s1), T.template t<2>(s2)), T.template t<3>(s3), rkq[r]);
+        const uint32_t t0 = T.template t<0>(s0), t1 = T.template t<1>(s0), t2 = T.template t<2>(s0),
+                       t3 = T.template t<3>(s0);
+        // three independent DPP ops whose other operand is an LDS result or a round key
+        // (a chain of DPP xors would need 2 wait states between them), then one xor3
+        s0 = xor3(xor_quad_from<1>(t0, t1), xor_quad_from<2>(rkq[r], t2), quad_from<3>(t3));
     }
-    const uint32_t s1 = quad_from<1>(s0), s2 = quad_from<2>(s0), s3 = quad_from<3>(s0);
-    return T.last(s0, s1, s2, s3, rkq[NR]);
+    // final round: S(byte j) of the own word, masked to byte j, summed the same way
+    const uint32_t m0 = T.template sraw<0>(s0) & 0x000000ffu, m1 = T.template sraw<1>(s0) & 0x0000ff00u,
+                   m2 = T.template sraw<2>(s0) & 0x00ff0000u, m3 = T.template sraw<3>(s0) & 0xff000000u;
+    return xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(rkq[NR], m2), quad_from<3>(m3));
 }
 
 typedef uint32_t __attribute__((aligned(1))) uint32_u;
