@@ -123,9 +123,9 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
 // ---------------------------------------------------------------------------
 // K2c: encryption, one lane QUAD per chain.  Lane q of the quad owns state column q:
-// per round it fetches the other three columns from its quad neighbours with DPP
-// quad_perm (VALU only), then does the 4 T-table lookups of its output column.  A
-// chain therefore issues 4 LDS reads per round instead of 16 -- 4x the lanes per
+// per round it does the 4 T-table lookups of its own 4 bytes and the quad sums the
+// contributions with DPP quad_perm (VALU only; aes_encrypt_column below).  A chain
+// therefore issues 4 LDS reads per lane and round instead of 16 -- 4x the lanes per
 // chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
 // lane instead of 60.  Used when chains are few (streams) or long/ragged.
 
@@ -294,13 +294,41 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
 
 // ---------------------------------------------------------------------------
 // K2q: K2c's quad-per-chain cipher with a work queue instead of a grid stride.
-// Chains are visited longest first (perm[]); a quad that finishes its chain takes the
+// Chains are visited longest first (perm[]); a quad that finishes a chain takes the
 // next one from a global counter at once, so lanes of a wave never wait for the
-// longest chain of their wave (greedy longest-processing-time scheduling).  The loop
-// body is one step of up to CH blocks of whatever chain each quad holds; the wave
-// leaves the loop when no quad has work.  Used for ragged batches (C4, U1 with mixed
-// sizes) where a static chain-to-lane assignment leaves most lanes idle.
-template <int NR, int KM, bool STREAM, int NT>
+// longest chain of their wave (greedy longest-processing-time scheduling).  Each quad
+// can carry S chains ("slots") whose ciphers run round-interleaved (a K2c round has
+// only 4 lookups in flight per lane).  S = 2 measured 35 % slower on C4: the longest
+// chains, which set the end of the launch, then advance at half speed.  The launcher
+// uses S = 1.  The loop body is one step of up to CH blocks of every slot;
+// a block past a slot's chain end is computed but not committed (a select, not a
+// branch, so the two ciphers stay in one basic block).  The wave leaves the loop when
+// no slot of any quad has work.  Used for ragged batches with more chains than quads
+// (C4), where a static chain-to-lane assignment leaves most lanes idle.
+template <int NR, int NT, int S>
+__device__ __forceinline__ void aes_encrypt_columns(uint32_t (&sq)[S], const uint32_t (&rkq)[S][NR + 1],
+                                                    const Tables4<NT> &T) {
+    uint32_t st[S];
+#pragma unroll
+    for (int k = 0; k < S; k++) st[k] = sq[k] ^ rkq[k][0];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+            const uint32_t t0 = T.template t<0>(st[k]), t1 = T.template t<1>(st[k]), t2 = T.template t<2>(st[k]),
+                           t3 = T.template t<3>(st[k]);
+            st[k] = xor3(xor_quad_from<1>(t0, t1), xor_quad_from<2>(rkq[k][r], t2), quad_from<3>(t3));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+        const uint32_t m0 = T.template sraw<0>(st[k]) & 0x000000ffu, m1 = T.template sraw<1>(st[k]) & 0x0000ff00u,
+                       m2 = T.template sraw<2>(st[k]) & 0x00ff0000u, m3 = T.template sraw<3>(st[k]) & 0xff000000u;
+        sq[k] = xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(rkq[k][NR], m2), quad_from<3>(m3));
+    }
+}
+
+template <int NR, int KM, bool STREAM, int NT, int S>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uint32_t *next) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -311,110 +339,149 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
     constexpr int CH = 8;
     const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
 
-    uint32_t rkq[NR + 1];
+    uint32_t rkq[S][NR + 1];
     if (KM == KEY_UNIFORM) {
 #pragma unroll
-        for (int r = 0; r <= NR; r++) rkq[r] = b.keys[0].rk[4 * r + q];
+        for (int r = 0; r <= NR; r++) {
+            const uint32_t w = b.keys[0].rk[4 * r + q];
+#pragma unroll
+            for (int k = 0; k < S; k++) rkq[k][r] = w;
+        }
     }
-    // per-quad chain state
-    uint64_t s = 0;
-    const uint8_t *p = nullptr;
-    uint8_t *o = nullptr;
-    uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
-    bool active = false;
+    // per-slot chain state
+    uint64_t sid[S];
+    const uint8_t *p[S];
+    uint8_t *o[S];
+    uint32_t nfull[S], tail[S], n[S], iv[S];
+    bool active[S];
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+        sid[k] = 0; p[k] = nullptr; o[k] = nullptr;
+        nfull[k] = tail[k] = n[k] = iv[k] = 0;
+        active[k] = false;
+    }
 
-    auto begin = [&](uint64_t t) {  // take chain perm[t] (t < count), run its head
-        s = b.perm ? b.perm[t] : t;
+    auto begin = [&](int k, uint64_t t) {  // slot k takes chain perm[t] (t < count), runs its head
+        const uint64_t s = b.perm ? b.perm[t] : t;
+        sid[k] = s;
         const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
         const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
         if (KM != KEY_UNIFORM) {
 #pragma unroll
-            for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+            for (int r = 0; r <= NR; r++) rkq[k][r] = key->rk[4 * r + q];
         }
+        uint32_t v, pos;
         if (STREAM) {
-            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
-            n = b.pos_state[s];
+            v = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            pos = b.pos_state[s];
         } else {
-            iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
-            n = 0;
+            v = reinterpret_cast<const uint32_t *>(key->iv)[q];
+            pos = 0;
         }
-        p = g.in;
-        o = g.out;
+        const uint8_t *pp = g.in;
+        uint8_t *oo = g.out;
         uint32_t rem = g.len;
         if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
-            if (q == 0) store_word_bytes(o, rem, 0, 4);
-            o += 4;
+            if (q == 0) store_word_bytes(oo, rem, 0, 4);
+            oo += 4;
         }
-        if (STREAM && n != 0 && rem != 0) {  // rest of the partially used keystream block
-            const uint32_t take = rem < 16 - n ? rem : 16 - n;
-            const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
+        if (STREAM && pos != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - pos ? rem : 16 - pos;
+            const int lo = max((int)pos, wlo) - wlo, hi = min((int)(pos + take), wlo + 4) - wlo;
             if (lo < hi) {
-                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
-                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t c = load_word_bytes(pp - pos + wlo, lo, hi) ^ v;
+                store_word_bytes(oo - pos + wlo, c, lo, hi);
                 const uint32_t m = word_mask(lo, hi);
-                iv = (c & m) | (iv & ~m);
+                v = (c & m) | (v & ~m);
             }
-            p += take;
-            o += take;
+            pp += take;
+            oo += take;
             rem -= take;
-            n = (n + take) & 15u;
+            pos = (pos + take) & 15u;
         }
-        nfull = rem >> 4;
-        tail = rem & 15u;
-        active = true;
+        iv[k] = v;
+        n[k] = pos;
+        p[k] = pp;
+        o[k] = oo;
+        nfull[k] = rem >> 4;
+        tail[k] = rem & 15u;
+        active[k] = true;
     };
-    auto finish = [&]() {  // partial final block and the stream state
-        if (tail) {
-            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
-            const int hi = min((int)tail, wlo + 4) - wlo;
+    auto finish = [&](int k) {  // partial final block and the stream state
+        if (tail[k]) {
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv[k], rkq[k], T);
+            const int hi = min((int)tail[k], wlo + 4) - wlo;
             if (hi > 0) {
-                const uint32_t c = load_word_bytes(p + wlo, 0, hi) ^ ks;
-                store_word_bytes(o + wlo, c, 0, hi);
+                const uint32_t c = load_word_bytes(p[k] + wlo, 0, hi) ^ ks;
+                store_word_bytes(o[k] + wlo, c, 0, hi);
                 const uint32_t m = word_mask(0, hi);
-                iv = (c & m) | (ks & ~m);
+                iv[k] = (c & m) | (ks & ~m);
             } else {
-                iv = ks;
+                iv[k] = ks;
             }
-            n = tail;
+            n[k] = tail[k];
         }
         if (STREAM) {
-            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
-            if (q == 0) b.pos_state[s] = n;
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * sid[k])[q] = iv[k];
+            if (q == 0) b.pos_state[sid[k]] = n[k];
         }
     };
-    // first chain: the quad's own index; later ones from the counter (which counts
-    // from nquads on)
+    // first chains: slot k of quad i takes chain k * nquads + i; later ones come from
+    // the counter (which counts from S * nquads on)
     const uint64_t t0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-    if (t0 < b.count) begin(t0);
-    while (__builtin_amdgcn_ballot_w64(active) != 0) {
-        if (active && nfull > 0) {
-            // (prefetching the next chunk during this one's rounds measured no gain:
-            // 16 waves per CU already hide the load latency)
-            const uint32_t k = nfull < CH ? nfull : CH;
-            uint32_t a[CH];
 #pragma unroll
-            for (int j = 0; j < CH; j++) a[j] = j < (int)k ? *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo) : 0u;
+    for (int k = 0; k < S; k++)
+        if (t0 + k * nquads < b.count) begin(k, t0 + k * nquads);
+    while (true) {
+        bool any = false;
 #pragma unroll
-            for (int j = 0; j < CH; j++) {
-                if (j < (int)k) {
-                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
-                    a[j] = iv;
-                }
+        for (int k = 0; k < S; k++) any = any || active[k];
+        if (__builtin_amdgcn_ballot_w64(any) == 0) break;
+        // slots whose chain has no whole block left: finish it, take the next chain
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+            if (active[k] && nfull[k] == 0) {
+                finish(k);
+                uint32_t t = 0;
+                if (q == 0) t = atomicAdd(next, 1u);
+                // broadcast the quad leader's ticket (DPP quad_perm 0,0,0,0)
+                t = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) + (uint32_t)(S * nquads);
+                active[k] = false;
+                if (t < b.count) begin(k, t);
             }
+        }
+        uint32_t kk[S];
+        uint32_t a[S][CH];
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+            kk[k] = active[k] ? (nfull[k] < CH ? nfull[k] : CH) : 0u;
 #pragma unroll
             for (int j = 0; j < CH; j++)
-                if (j < (int)k) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = a[j];
-            p += 16 * k;
-            o += 16 * k;
-            nfull -= k;
-        } else if (active) {
-            finish();
-            uint32_t t = 0;
-            if (q == 0) t = atomicAdd(next, 1u);
-            // broadcast the quad leader's ticket (DPP quad_perm 0,0,0,0)
-            t = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) + (uint32_t)nquads;
-            active = false;
-            if (t < b.count) begin(t);
+                a[k][j] = j < (int)kk[k] ? *reinterpret_cast<const uint32_u *>(p[k] + 16 * j + wlo) : 0u;
+        }
+        // (a quad with no work in any slot still runs the rounds: its results are
+        // dropped like those of blocks past a chain's end)
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            uint32_t e[S];
+#pragma unroll
+            for (int k = 0; k < S; k++) e[k] = iv[k];
+            aes_encrypt_columns<NR, NT, S>(e, rkq, T);
+#pragma unroll
+            for (int k = 0; k < S; k++) {
+                const uint32_t c = e[k] ^ a[k][j];  // C_i = P_i ^ E(C_{i-1})
+                iv[k] = j < (int)kk[k] ? c : iv[k];
+                a[k][j] = c;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < S; k++) {
+#pragma unroll
+            for (int j = 0; j < CH; j++)
+                if (j < (int)kk[k]) *reinterpret_cast<uint32_u *>(o[k] + 16 * j + wlo) = a[k][j];
+            p[k] += 16 * kk[k];
+            o[k] += 16 * kk[k];
+            nfull[k] -= kk[k];
         }
     }
 }
@@ -468,9 +535,10 @@ static void coop_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int
 }
 
 template <int NR>
-static void queue_nr(const KBatch &b, KeyMode km, bool stream, int grid, int threads, uint32_t *next, hipStream_t st) {
-#define FPNN_QUEUE(K, S) \
-    hipLaunchKernelGGL((k_cfb_encrypt_queue<NR, K, S, 4>), dim3(grid), dim3(threads), 0, st, b, next)
+static void queue_nr(const KBatch &b, KeyMode km, bool stream, int grid, int threads, uint32_t *next,
+                     hipStream_t st) {
+#define FPNN_QUEUE(K, STR) \
+    hipLaunchKernelGGL((k_cfb_encrypt_queue<NR, K, STR, 4, 1>), dim3(grid), dim3(threads), 0, st, b, next)
     if (km == KEY_UNIFORM) {
         if (stream) FPNN_QUEUE(KEY_UNIFORM, true); else FPNN_QUEUE(KEY_UNIFORM, false);
     } else {
