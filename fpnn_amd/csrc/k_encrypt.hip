@@ -328,7 +328,7 @@ __device__ __forceinline__ void aes_encrypt_columns(uint32_t (&sq)[S], const uin
     }
 }
 
-template <int NR, int KM, bool STREAM, int NT, int S>
+template <int NR, int KM, bool STREAM, int NT, int S, bool FIRST_PRIO = true>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uint32_t *next) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -426,9 +426,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
             if (q == 0) b.pos_state[sid[k]] = n[k];
         }
     };
-    // first chains: slot k of quad i takes chain k * nquads + i; later ones come from
-    // the counter (which counts from S * nquads on)
-    const uint64_t t0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    // First chains: the longest (perm[] order) are dealt round-robin over the
+    // workgroups -- quad j of workgroup w takes chain j * gridDim.x + w -- so the few
+    // longest chains, which set the end of the launch, sit on different CUs and in the
+    // first wave of each; that wave runs at raised priority so its chain's rounds are
+    // not queued behind the 15 other waves' (the critical path of a greedy schedule
+    // is its longest job).  Later chains come from the counter (from S * nquads on).
+    const uint64_t t0 = (uint64_t)(threadIdx.x >> 2) * gridDim.x + blockIdx.x;
+    if (FIRST_PRIO && threadIdx.x < 64) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int k = 0; k < S; k++)
         if (t0 + k * nquads < b.count) begin(k, t0 + k * nquads);
