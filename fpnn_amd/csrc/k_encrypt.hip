@@ -450,9 +450,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
                 uint32_t t = 0;
                 if (q == 0) t = atomicAdd(next, 1u);
                 // broadcast the quad leader's ticket (DPP quad_perm 0,0,0,0)
-                t = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) + (uint32_t)(S * nquads);
+                const uint64_t tt = (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) +
+                                    (uint64_t)S * nquads;  // 64-bit: no wrap near count = 2^32 - 1
                 active[k] = false;
-                if (t < b.count) begin(k, t);
+                if (tt < b.count) begin(k, tt);
             }
         }
         uint32_t kk[S];
