@@ -8,6 +8,7 @@ for DESIGN.md -- bench.py's single JSON line covers C2 only.
   C4  Zipf 64 B..64 KiB, 4 GiB, AES-256 package
   C5  65536 keys x 4 KiB AES-256, per-key IV
   U1  1M x 1472 B UDP datagrams over 16384 connections, AES-128
+  R1  the receive path: 16384 connections x 64 wire frames, fpnn_aes_package_recv (8f row 3)
 """
 import argparse
 import json
@@ -48,7 +49,7 @@ def gib(nbytes, sec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--configs", default="C2,C3,C4,C5,U1")
+    ap.add_argument("--configs", default="C2,C3,C4,C5,U1,R1")
     args = ap.parse_args()
     import fpnn_amd
     E, D = fpnn_amd.K_ENCRYPT, fpnn_amd.K_DECRYPT
@@ -295,6 +296,42 @@ def main():
                      "note": "encrypt = 4096 serial CFB chains (one lane each, latency bound); "
                              "decrypt parallel per block"}
         print(json.dumps({"C3": out["C3"]}), flush=True)
+    if "R1" in todo:
+        # The receive path: 16384 connection buffers, each holding 64
+        # package-mode wire frames (htole32(len) + 1 KiB ciphertext, the form
+        # PackageEncryptor::encrypt(std::string*) sends) = 1 GiB of bodies; one
+        # fpnn_aes_package_recv call finds the frames on the device and decrypts them.
+        NC, F, L = 16384, 64, 1024
+        key, iv = W.single_key(W.C2)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        P = NC * F
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, 7)
+        wire = torch.empty(P * (L + 4), dtype=torch.uint8, device="cuda")
+        in_off = torch.arange(P, dtype=torch.int64, device="cuda") * L
+        out_off = torch.arange(P, dtype=torch.int64, device="cuda") * (L + 4)
+        lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
+        eng.package_encrypt(a, wire, P, ks, in_off=in_off, out_off=out_off, lens=lens, wire_prefix=True)
+        conn_off = torch.arange(NC, dtype=torch.int64, device="cuda") * (F * (L + 4))
+        conn_len = torch.full((NC,), F * (L + 4), dtype=torch.int32, device="cuda")
+        plain = torch.empty_like(wire)
+
+        def recv():
+            return eng.package_recv(wire, plain, NC, ks, 8 << 20, F, in_off=conn_off, lens=conn_len)
+
+        wr, kr, _ = timed(eng, D, recv, args.reps)
+        foff, flen, scan = recv()
+        torch.cuda.synchronize()
+        body = plain.view(P, L + 4)[:, 4:]
+        assert torch.equal(body.reshape(-1), a), "R1 receive-path plaintext differs"
+        out["R1"] = {"frames": P, "body_bytes": P * L, "recv_wall_GiBs": gib(P * L, wr),
+                     "decrypt_kernel_GiBs": gib(P * L, kr),
+                     "note": "fpnn_aes_package_recv over 16384 connections x 64 wire frames (4-byte LE length + 1 KiB): "
+                             "device frame scan + decrypt of the bodies at their frame offsets (wall includes the scan "
+                             "and the host sync for the block total)"}
+        del a, wire, plain
+        print(json.dumps({"R1": out["R1"]}), flush=True)
+
     print(json.dumps({"configs": out}))
 
 
