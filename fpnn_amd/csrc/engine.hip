@@ -512,7 +512,8 @@ const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
 
 const char *fpnn_aes_version(void) {
     return "fpnn_aes 0.1 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
-           "K1 lane-per-block decrypt, K2 lane-per-chain encrypt)";
+           "decrypt: K1d dense/keyed/ragged, K1k lane keys, K1 general, one lane per block; "
+           "encrypt: K2 lane per chain, K2c/K2q quad per chain)";
 }
 
 int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen) {
