@@ -385,7 +385,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.iv_snap = e->d_snap_iv;
         k.pos_snap = e->d_snap_pos;
     }
-    const bool inplace = b->in == b->out && b->out_off == nullptr;
+    bool inplace = b->in == b->out && b->out_off == nullptr;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     // Uniform layout: every segment has the same block count, known on the host.
     // (Stream mode only when there is a single segment, whose position the caller
@@ -412,6 +412,29 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.total_blocks = total;
             k.nb_uniform = (uint32_t)nb;
             k.magic = magic_for((uint32_t)nb);
+        }
+    } else if (stream && km == KEY_LANE && !b->len && e->variant.dec_dense && b->uniform_len >= 1024 &&
+               b->uniform_len % 1024 == 0 && (b->in_off || (!b->out_off && b->stride == b->uniform_len)) &&
+               ((uint64_t)b->uniform_len >> 4) * b->count < (1ull << 32)) {
+        // dense stream decrypt, one key slot per stream, whole 64-block chunks (C3): when
+        // every stream is at CFB position 0 and (offset arrays) stream s sits at s * L
+        // (checked on the device; one host sync), it is K1d keyed with the streams'
+        // carried IVs, and the new state is each stream's last ciphertext block (written
+        // first: the decrypt may run in place)
+        HIP_TRY(launch_pos_check(k, e->d_total + 1, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->h_total + 1, e->d_total + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (e->h_total[1] == 0) {
+            const uint64_t nb = b->uniform_len >> 4;
+            k.in_off = k.out_off = nullptr;
+            k.stride = b->uniform_len;
+            inplace = b->in == b->out;  // out_off may repeat in_off
+            HIP_TRY(launch_stream_dense_state(k, e->stream));
+            layout = LAYOUT_FULL;
+            k.total_blocks = nb * b->count;
+            k.nb_uniform = (uint32_t)nb;
+            k.magic = magic_for((uint32_t)nb);
+            k.seg_iv = e->d_snap_iv;
         }
     }
     if (layout == LAYOUT_GENERAL) {

@@ -224,7 +224,14 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     };
     auto step = [&](uint64_t st, StepBuf &X, StepBuf &NX, bool pref, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
-        if (KEYED) set_key(((ConstU32 *)b.key_slot)[fast_div((uint32_t)((st * U) << 6), b.magic)]);
+        if (KEYED) {
+            const uint32_t pkt = fast_div((uint32_t)((st * U) << 6), b.magic);
+            set_key(((ConstU32 *)b.key_slot)[pkt]);
+            if (b.seg_iv) {  // dense stream decrypt: the stream's carried IV (wave-uniform)
+                ConstU32 *ivp = (ConstU32 *)(b.seg_iv + pkt);
+                iv = make_uint4(ivp[0], ivp[1], ivp[2], ivp[3]);
+            }
+        }
         if (!PF || !FULL) load(st, X, full_tag);
         uint4 ks[U];
 #pragma unroll

@@ -267,6 +267,47 @@ __global__ __launch_bounds__(256) void k_start_mask(KBatch b, const uint64_t *bs
     }
 }
 
+// Dense stream decrypt: streams whose CFB position is not 0 (their first block is
+// partial, so K1d's whole-block addressing does not apply) or, with offset arrays,
+// that do not sit at s * uniform_len.
+__global__ __launch_bounds__(256) void k_pos_check(KBatch b, uint64_t *bad) {
+    uint32_t n = 0;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = s * b.uniform_len;
+        bool ok = b.pos_snap[s] == 0u;
+        if (b.in_off) ok = ok && b.in_off[s] == o;
+        if (b.out_off) ok = ok && b.out_off[s] == o;
+        n += ok ? 0u : 1u;
+    }
+    if (n) atomicAdd(reinterpret_cast<unsigned long long *>(bad), (unsigned long long)n);
+}
+
+// Dense stream decrypt, every position 0 and whole blocks: the state each stream leaves
+// is (its last ciphertext block, 0) -- base/rijndael.c:1171-1201 ends a whole block with
+// ivec = that block and pos = 0.  Runs before the decrypt (which may overwrite the
+// ciphertext in place); the decrypt reads the incoming IVs from the snapshot.
+__global__ __launch_bounds__(256) void k_stream_dense_state(KBatch b) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 last = *reinterpret_cast<const uint4 *>(b.in + s * b.stride + b.uniform_len - 16);
+        *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = last;
+        b.pos_state[s] = 0u;
+    }
+}
+
+hipError_t launch_pos_check(const KBatch &b, uint64_t *bad, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(bad, 0, sizeof(uint64_t), st);
+    if (err != hipSuccess) return err;
+    if (b.count) hipLaunchKernelGGL(k_pos_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st) {
+    if (b.count) hipLaunchKernelGGL(k_stream_dense_state, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b);
+    return hipGetLastError();
+}
+
 hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st) {
     hipError_t err = hipMemsetAsync(bad, 0, sizeof(uint64_t), st);
     if (err != hipSuccess) return err;

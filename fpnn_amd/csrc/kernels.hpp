@@ -45,6 +45,9 @@ struct KBatch {
     // decrypt of contiguous ragged batches (K1d ragged): bit l of start_mask[c] set when
     // block 64c + l opens a segment; null otherwise
     const uint64_t *start_mask;
+    // K1d keyed: per-packet IV (dense stream decrypt with every position 0: the
+    // snapshot of iv_state); null = the key slot's IV (package mode)
+    const uint4 *seg_iv;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
@@ -127,6 +130,10 @@ hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart,
 // shifted copy of in_off) into *bad (zeroed here).
 hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st);
 // start_mask[nchunks] (zeroed here): one bit per block that opens a non-empty segment.
+// Stream decrypt of a dense whole-block batch: *bad (zeroed here) = streams whose
+// pos_snap is not 0; then, when it is 0, the new (iv, pos) state of every stream.
+hipError_t launch_pos_check(const KBatch &b, uint64_t *bad, hipStream_t st);
+hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st);
 hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, uint64_t nchunks,
                              hipStream_t st);
 hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first,

@@ -388,6 +388,49 @@ def test_random_stream_batches(request, oracle, keylen, eng_kind):
             assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h), (encrypt, call)
 
 
+@pytest.mark.parametrize("length", [1024, 3072, 4096])
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("arrays", [False, True])
+def test_dense_stream_decrypt(engine, oracle, length, inplace, arrays):
+    """Dense stream decrypt (the C3 shape: one key slot per stream, stride = length,
+    whole 1 KiB chunks).  Calls where every stream sits at CFB position 0 run K1d keyed
+    with the streams' carried IVs and write (last ciphertext block, 0) as the new state;
+    a call with one stream mid-block falls back to K1.  With `arrays` the batch comes as
+    offset arrays (in_off = s * length, checked on the device).  Output and (iv, pos)
+    state must follow the reference byte loop (base/rijndael.c:1171-1201) call after call."""
+    rng = np.random.default_rng(length + 7 * inplace + 13 * arrays)
+    S = 333  # partial last chunk of the batch is irrelevant (whole chunks), odd stream count
+    for keylen in (16, 32):
+        keys = rng.integers(0, 256, S * keylen, dtype=np.uint8)
+        ivs = rng.integers(0, 256, S * 16, dtype=np.uint8)
+        ks = keyset(engine, keys, keylen, ivs)
+        slots = rng.permutation(S).astype(np.uint32)
+        iv_h, pos_h = ivs.copy(), np.zeros(S, dtype=np.uint32)
+        iv_d, pos_d = to_dev(iv_h), to_dev(pos_h.astype(np.int32))
+        offs = (np.arange(S, dtype=np.uint64) * length)
+        lens = np.full(S, length, dtype=np.uint32)
+        for call in range(4):
+            if call == 2:  # one stream mid-block: the K1 fallback, then back to dense
+                pos_h[S // 2] = 7
+                pos_d[S // 2] = 7
+            inp = rng.integers(0, 256, S * length, dtype=np.uint8)
+            exp = inp.copy()
+            oracle.stream_batch(False, inp, exp, S, in_off=offs, out_off=offs, lens=lens, key_slot=slots,
+                                keys=keys, keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
+            src = to_dev(inp)
+            dst = src if inplace else to_dev(inp)
+            lay = dict(in_off=to_dev(offs.astype(np.int64))) if arrays else dict(stride=length)
+            engine.stream_decrypt(src, dst, S, ks, iv_d, pos_d, uniform_len=length,
+                                  key_slot=to_dev(slots.astype(np.int32)), **lay)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp), (keylen, call)
+            assert np.array_equal(to_host(iv_d), iv_h), (keylen, call)
+            assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h), (keylen, call)
+            if call == 2:  # realign that stream for the last (dense) call
+                pos_h[S // 2] = 0
+                pos_d[S // 2] = 0
+
+
 @pytest.mark.parametrize("encrypt", [True, False])
 def test_long_stream_segments(engine, oracle, encrypt):
     """Few streams, segments of many 64-block chunks: every wave of a segment must see
