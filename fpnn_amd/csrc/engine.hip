@@ -175,6 +175,8 @@ struct fpnn_aes_engine {
     uint64_t cap_tile = 0;
     uint64_t *d_mask = nullptr;  // contiguous ragged decrypt: segment-start bits per chunk
     uint64_t cap_mask = 0;
+    int32_t *d_blk_delta = nullptr, *d_chunk_delta = nullptr;  // gapped ragged decrypt
+    uint64_t cap_blk_delta = 0, cap_chunk_delta = 0;
     uint4 *d_boundary = nullptr;
     uint64_t cap_boundary = 0;
     uint4 *d_snap_iv = nullptr;  // stream-decrypt state snapshot
@@ -447,19 +449,29 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // whether the segments are contiguous whole blocks, which K1d decrypts with
         // dense addressing and a start-bit mask instead of a per-lane segment search.
         const bool try_dense = !stream && km == KEY_UNIFORM && total == kNoHint && e->variant.dec_dense;
-        if (try_dense) HIP_TRY(launch_contig_check(k, e->d_total + 1, e->stream));
-        bool contiguous = false;
+        if (try_dense) HIP_TRY(launch_contig_check(k, e->d_bstart, e->d_total + 1, e->stream));
+        bool contiguous = false, gapped = false;
         if (total == kNoHint) {
-            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
             HIP_TRY(hipStreamSynchronize(e->stream));
             total = e->h_total[0];
             contiguous = try_dense && e->h_total[1] == 0;
+            // whole-block segments with gaps between them (wire frames: 4-byte length
+            // prefixes): K1d ragged with a per-segment address delta
+            gapped = try_dense && !contiguous && e->h_total[2] == 0 && e->variant.dec_gapped && total < (1ull << 32);
         }
         if (!total) return FPNN_AES_OK;
         const uint64_t nchunks = (total + 63) >> 6;
-        if (contiguous) {
+        if (contiguous || gapped) {
             if ((rc = grow(e->d_mask, e->cap_mask, nchunks))) return rc;
-            HIP_TRY(launch_start_mask(k, e->d_bstart, e->d_mask, nchunks, e->stream));
+            if (gapped) {
+                if ((rc = grow(e->d_blk_delta, e->cap_blk_delta, total))) return rc;
+                if ((rc = grow(e->d_chunk_delta, e->cap_chunk_delta, nchunks))) return rc;
+                k.blk_delta = e->d_blk_delta;
+                k.chunk_delta = e->d_chunk_delta;
+            }
+            HIP_TRY(launch_start_mask(k, e->d_bstart, e->d_mask, k.blk_delta ? e->d_blk_delta : nullptr,
+                                      e->d_chunk_delta, nchunks, e->stream));
             k.start_mask = e->d_mask;
         }
         if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
@@ -585,6 +597,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
     }
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_DEC_GAPPED")) e->variant.dec_gapped = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
@@ -604,8 +617,8 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         err = hipMemcpy(e->d_tables, kTables.t0le, 1024, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1024, kTables.sbox, 256, hipMemcpyHostToDevice);
         if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
-        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), 2 * sizeof(uint64_t));  // total, contiguity
-        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), 2 * sizeof(uint64_t), 0);
+        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), 4 * sizeof(uint64_t));  // total, contiguity, gapped
+        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), 4 * sizeof(uint64_t), 0);
         if (err != hipSuccess) { rc = hip_fail(err, "alloc(total)"); break; }
     } while (0);
     if (rc) {
@@ -625,6 +638,8 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_wgsums);
     (void)hipFree(e->d_tile);
     (void)hipFree(e->d_mask);
+    (void)hipFree(e->d_blk_delta);
+    (void)hipFree(e->d_chunk_delta);
     (void)hipFree(e->d_boundary);
     (void)hipFree(e->d_snap_iv);
     (void)hipFree(e->d_snap_pos);

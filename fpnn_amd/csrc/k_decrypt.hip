@@ -157,11 +157,17 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 //   KEYED: one key per packet (key_slot[] with the dense layout, chunk-aligned packets:
 //   the C5 shape).  A step's U chunks never straddle two packets (U divides nb/64), so
 //   the step's key is wave-uniform: slot and round keys are scalar loads per step.
-template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED, bool RAGGED = false>
+//   GAPPED (with RAGGED): whole-block segments with gaps between them (wire frames behind
+//   4-byte length prefixes).  Block g of segment s sits at in + in_off[0] + 16 g + d_s:
+//   a lane takes d_s from blk_delta at its segment's start bit in the chunk, or, before
+//   the chunk's first start bit, from chunk_delta[c] (wave-uniform).
+template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED, bool RAGGED = false,
+          bool GAPPED = false>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_dense(KBatch b) {
     static_assert(U % IL == 0, "IL-way interleave of U chunks");
     static_assert(!KEYED || ALIGNED, "per-packet keys need chunk-aligned packets");
     static_assert(!RAGGED || (!ALIGNED && !KEYED), "ragged batches use the start mask");
+    static_assert(!GAPPED || RAGGED, "the gapped form is a ragged batch");
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -202,6 +208,10 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     struct StepBuf {
         uint4 x[U];
         uint4 f;
+        int32_t d[U];  // GAPPED: the lane's segment address delta per chunk
+    };
+    auto cdelta = [&](uint64_t c) -> int64_t {
+        return GAPPED ? (int64_t)((__attribute__((address_space(4))) const int32_t *)b.chunk_delta)[c] : 0;
     };
     auto load = [&](uint64_t st, StepBuf &D, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         // more stores than necessary
         const uint64_t c0 = FULL || st * U < nchunks ? st * U : nchunks - 1;
         if (!opens(c0))  // wave-uniform; at a packet start the IV is used
-            D.f = INPLACE ? b.boundary[c0] : *reinterpret_cast<const uint4 *>(inb + (c0 << 10) - 16);
+            D.f = INPLACE ? b.boundary[c0] : load16(inb + (c0 << 10) - 16 + cdelta(c0));  // any byte alignment
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const uint64_t c = st * U + j;
@@ -219,7 +229,16 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 const uint64_t left = total - (cl << 6);
                 if (left < 64) lo = min(lane, (uint32_t)left - 1u) * 16u;
             }
-            D.x[j] = load16(inb + (cl << 10) + lo);
+            int64_t dl = 0;
+            if (GAPPED) {  // the delta of the segment holding the lane's (clamped) block
+                const uint32_t lc = lo >> 4;
+                const uint64_t below = starts(cl) & (lc == 63 ? ~0ull : (2ull << lc) - 1ull);
+                const uint32_t p = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+                const int32_t bd = b.blk_delta[(cl << 6) + p];
+                D.d[j] = below ? bd : (int32_t)cdelta(cl);
+                dl = D.d[j];
+            }
+            D.x[j] = load16(inb + (cl << 10) + lo + dl);
         }
     };
     auto step = [&](uint64_t st, StepBuf &X, StepBuf &NX, bool pref, auto full_tag) {
@@ -271,7 +290,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 if (c >= nchunks) break;  // wave-uniform
                 if (!ALIGNED && (c << 6) + lane >= total) continue;
             }
-            store16(outb + (c << 10) + lane16, X.x[j] ^ ks[j]);
+            store16(outb + (c << 10) + lane16 + (GAPPED ? (int64_t)X.d[j] : 0), X.x[j] ^ ks[j]);
         }
     };
     const uint64_t nfull = (total >> 6) / U;  // steps made of U whole chunks
@@ -388,14 +407,14 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
 #define FPNN_DEC(L, K, S, NTX) \
     hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K), 1>), dim3(grid), dim3(kThreads), \
                        0, st, b)
-#define FPNN_DENSE_R() \
-    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, 1, true, false, true>), dim3(grid), \
+#define FPNN_DENSE_R(G) \
+    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, 1, true, false, true, G>), dim3(grid), \
                        dim3(kThreads), 0, st, b)
 #define FPNN_DENSE(AL, U, PF, KEYED) \
     hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
-    if (layout == LAYOUT_GENERAL && b.start_mask) {  // contiguous whole-block segments, one key
-        FPNN_DENSE_R();
+    if (layout == LAYOUT_GENERAL && b.start_mask) {  // contiguous (or gapped) whole-block segments, one key
+        if (b.blk_delta) FPNN_DENSE_R(true); else FPNN_DENSE_R(false);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
         hipLaunchKernelGGL((k_cfb_decrypt_lanekey<NR, INPLACE, 4>), dim3(grid), dim3(kThreads), 0, st, b);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet

@@ -242,28 +242,50 @@ __device__ __forceinline__ uint64_t seg_off(const KBatch &b, uint64_t s, const u
     return off ? off[s] : s * b.stride;
 }
 
-__global__ __launch_bounds__(256) void k_contig_check(KBatch b, uint64_t *bad) {
-    uint32_t n = 0;
+// bad[0]: segments that break "contiguous whole blocks"; bad[1]: non-empty segments
+// that also rule out the gapped form (K1d ragged with a per-segment offset delta): a
+// partial last block, out_off not a shifted copy of in_off, or a delta
+// (in_off[s] - in_off[0] - 16 bstart[s]) outside int32.  Empty segments never count
+// for bad[1] (their offsets are not read).
+__global__ __launch_bounds__(256) void k_contig_check(KBatch b, const uint64_t *bstart, uint64_t *bad) {
+    uint32_t n = 0, h = 0;
     const uint64_t in0 = seg_off(b, 0, b.in_off);
     const uint64_t out0 = b.out_off ? b.out_off[0] : in0;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
          s += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t len = b.len ? b.len[s] : b.uniform_len;
         const uint64_t io = seg_off(b, s, b.in_off);
-        bool ok = (len & 15u) == 0;
+        const bool whole = (len & 15u) == 0;
+        const bool shifted = !b.out_off || b.out_off[s] - out0 == io - in0;
+        bool ok = whole && shifted;
         if (s + 1 < b.count) ok = ok && seg_off(b, s + 1, b.in_off) == io + len;
-        if (b.out_off) ok = ok && b.out_off[s] - out0 == io - in0;
         n += ok ? 0u : 1u;
+        if (len) {
+            const int64_t d = (int64_t)(io - in0 - 16 * bstart[s]);
+            h += (!whole || !shifted || d < INT32_MIN || d > INT32_MAX) ? 1u : 0u;
+        }
     }
     if (n) atomicAdd(reinterpret_cast<unsigned long long *>(bad), (unsigned long long)n);
+    if (h) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 1), (unsigned long long)h);
 }
 
-__global__ __launch_bounds__(256) void k_start_mask(KBatch b, const uint64_t *bstart, uint64_t *mask) {
+// gapped form (delta != null): block g of segment s sits at in + in_off[0] + 16 g + d_s,
+// d_s = in_off[s] - in_off[0] - 16 bstart[s].  blk_delta[bstart[s]] = d_s (read by the
+// lanes at and after a segment start), chunk_delta[c] = d_s of the segment holding
+// block 64c (read by the lanes before the chunk's first start bit).
+__global__ __launch_bounds__(256) void k_start_mask(KBatch b, const uint64_t *bstart, uint64_t *mask,
+                                                    int32_t *blk_delta, int32_t *chunk_delta) {
+    const uint64_t in0 = seg_off(b, 0, b.in_off);
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
          s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t g = bstart[s];
-        if (bstart[s + 1] > g)  // non-empty
-            atomicOr(reinterpret_cast<unsigned long long *>(mask + (g >> 6)), 1ull << (g & 63));
+        const uint64_t g = bstart[s], ge = bstart[s + 1];
+        if (ge <= g) continue;  // empty
+        atomicOr(reinterpret_cast<unsigned long long *>(mask + (g >> 6)), 1ull << (g & 63));
+        if (blk_delta) {
+            const int32_t d = (int32_t)(int64_t)(seg_off(b, s, b.in_off) - in0 - 16 * g);
+            blk_delta[g] = d;
+            for (uint64_t t = (g + 63) >> 6; (t << 6) < ge; t++) chunk_delta[t] = d;
+        }
     }
 }
 
@@ -308,18 +330,21 @@ hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st) {
-    hipError_t err = hipMemsetAsync(bad, 0, sizeof(uint64_t), st);
+hipError_t launch_contig_check(const KBatch &b, const uint64_t *bstart, uint64_t *bad, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(bad, 0, 2 * sizeof(uint64_t), st);
     if (err != hipSuccess) return err;
-    if (b.count) hipLaunchKernelGGL(k_contig_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bad);
+    if (b.count)
+        hipLaunchKernelGGL(k_contig_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, bad);
     return hipGetLastError();
 }
 
-hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, uint64_t nchunks,
-                             hipStream_t st) {
+hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, int32_t *blk_delta,
+                             int32_t *chunk_delta, uint64_t nchunks, hipStream_t st) {
     hipError_t err = hipMemsetAsync(mask, 0, nchunks * sizeof(uint64_t), st);
     if (err != hipSuccess) return err;
-    if (b.count) hipLaunchKernelGGL(k_start_mask, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, mask);
+    if (b.count)
+        hipLaunchKernelGGL(k_start_mask, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, mask, blk_delta,
+                           chunk_delta);
     return hipGetLastError();
 }
 

@@ -48,6 +48,11 @@ struct KBatch {
     // K1d keyed: per-packet IV (dense stream decrypt with every position 0: the
     // snapshot of iv_state); null = the key slot's IV (package mode)
     const uint4 *seg_iv;
+    // K1d ragged, gapped form: block g of segment s sits at in + in_off[0] + 16 g + d_s;
+    // blk_delta[bstart[s]] = d_s, chunk_delta[c] = d_s of the segment holding block 64c
+    // (null: contiguous, d_s = 0)
+    const int32_t *blk_delta;
+    const int32_t *chunk_delta;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
@@ -69,6 +74,7 @@ struct Variant {
     int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
+    int dec_gapped = 1;    // decrypt, ragged whole-block segments with gaps: K1d ragged + address deltas
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
@@ -125,17 +131,21 @@ hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uin
 // ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
-// Package-mode decrypt of a general layout: counts the segments that break "contiguous
-// whole blocks" (len % 16 != 0, a gap or overlap to the next segment, out_off not a
-// shifted copy of in_off) into *bad (zeroed here).
-hipError_t launch_contig_check(const KBatch &b, uint64_t *bad, hipStream_t st);
-// start_mask[nchunks] (zeroed here): one bit per block that opens a non-empty segment.
+// Package-mode decrypt of a general layout (after the block-map scan): bad[0] = the
+// segments that break "contiguous whole blocks" (len % 16 != 0, a gap or overlap to the
+// next segment, out_off not a shifted copy of in_off); bad[1] = the non-empty ones that
+// also rule out the gapped form (partial block, unshifted out_off, delta beyond int32).
+// Both zeroed here.
+hipError_t launch_contig_check(const KBatch &b, const uint64_t *bstart, uint64_t *bad, hipStream_t st);
 // Stream decrypt of a dense whole-block batch: *bad (zeroed here) = streams whose
 // pos_snap is not 0; then, when it is 0, the new (iv, pos) state of every stream.
 hipError_t launch_pos_check(const KBatch &b, uint64_t *bad, hipStream_t st);
 hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st);
-hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, uint64_t nchunks,
-                             hipStream_t st);
+// start_mask[nchunks] (zeroed here): one bit per block that opens a non-empty segment.
+// Gapped form (blk_delta not null): d_s = in_off[s] - in_off[0] - 16 bstart[s] at
+// blk_delta[bstart[s]] (total_blocks entries) and chunk_delta[c] (nchunks entries).
+hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, int32_t *blk_delta,
+                             int32_t *chunk_delta, uint64_t nchunks, hipStream_t st);
 hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first,
                            uint64_t nchunks, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,

@@ -326,6 +326,48 @@ def test_contiguous_ragged_decrypt(engine, oracle, layout):
     assert np.array_equal(to_host(dst), exp)
 
 
+@pytest.mark.parametrize("gaps", ["wire4", "random", "reversed", "shifted_out", "odd_len"])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_gapped_ragged_decrypt(engine, oracle, gaps, inplace):
+    """Ragged whole-block package segments with gaps between them (the receive path:
+    bodies behind 4-byte length prefixes), empty segments interleaved: K1d ragged with
+    per-segment address deltas ('reversed': segments in descending memory order, so the
+    deltas are negative).  'odd_len' has one partial block and must fall back to K1."""
+    if inplace and gaps == "shifted_out":
+        pytest.skip("shifted output is out of place")
+    rng = np.random.default_rng(["wire4", "random", "reversed", "shifted_out", "odd_len"].index(gaps) + 31 * inplace)
+    n = 2500
+    lens = (rng.integers(0, 200, n) * 16).astype(np.int64)
+    lens[rng.random(n) < 0.05] = 0
+    lens[:3] = (64, 1024, 0)
+    if gaps == "odd_len":
+        lens[1200] += 3
+    gap = np.full(n, 4, np.int64) if gaps == "wire4" else rng.integers(0, 100, n).astype(np.int64)
+    gap[rng.random(n) < 0.1] = 0  # some runs are contiguous
+    offs = 20 + np.concatenate([[0], np.cumsum(lens[:-1] + gap[:-1])]).astype(np.int64)
+    total = int(offs[-1] + lens[-1] + 64)
+    if gaps == "reversed":  # segment 0 last in memory, segment n-1 first
+        offs = total - 64 - offs - lens + 20
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    key, iv = rng.bytes(32), rng.bytes(16)
+    import fpnn_amd
+    ks = fpnn_amd.KeySet(engine, key, 32, iv)
+    kb, ib = np.frombuffer(key, np.uint8).copy(), np.frombuffer(iv, np.uint8).copy()
+    shift = 80 if gaps == "shifted_out" else 0
+    out_offs = offs + shift
+    exp = np.zeros(total + shift, dtype=np.uint8) if shift else inp.copy()
+    oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=out_offs.astype(np.uint64),
+                         lens=lens.astype(np.uint32), keys=kb, keylen=32, ivs=ib, threads=8)
+    src = to_dev(inp)
+    dst = src if inplace else (dev_u8(total + shift) if shift else to_dev(inp))
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+    if shift:
+        kw["out_off"] = to_dev(out_offs)
+    engine.package_decrypt(src, dst, n, ks, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(dst), exp)
+
+
 @pytest.mark.parametrize("length", [32, 48, 1040, 1472, 1024, 2048, 3072, 4096])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_dense_keyed_layout(engine, oracle, length, inplace):
