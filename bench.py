@@ -36,6 +36,10 @@ import torch  # noqa: E402
 import workloads as W  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+METRIC = "AES-256 GiB/s on device-resident packet batch; 1/2/4/8-GPU scaling"  # BASELINE.json "metric"
+# newest committed PMC summary of the bench command (tools/pmc_summary.py output), per workload
+PMC_SUMMARIES = {"C2": "profiles/r02/c2/pmc_summary.json", "C4": "profiles/r02/c4/pmc_summary.json",
+                 "C5": "profiles/r02/c5/pmc_summary.json"}
 
 
 def parse():
@@ -55,13 +59,66 @@ def parse():
                     help="C2 = the bench line (default); C4 / C5 = the BASELINE.json sharded configs")
     ap.add_argument("--only", choices=["encrypt", "decrypt"], default=None,
                     help="profiling aid: run one direction only (not a bench line)")
+    ap.add_argument("--plumbing-only", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch/reduction/verify contract (no GPU work)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n: int, port: int, base=None):
+    """Environment of each of the n rank processes of a one-node job (what torchrun
+    would set): RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n, rendezvous on
+    127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(argv, n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: start the N rank processes here
+    (children of this process, before anything touches the GPU) and return the job's
+    exit code -- the first non-zero rank code, or 0.  Rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    envs = rank_envs(n, _free_port())
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # one rank failed: the others would wait forever in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
     dev = local % max(1, torch.cuda.device_count())  # == local on a node with one GPU per rank
     torch.cuda.set_device(dev)
     if world > 1:
@@ -88,55 +145,109 @@ def barrier(world):
         dist.barrier()
 
 
-def load_traffic(kernel: str):
-    """HBM bytes per launch from the committed PMC summary (profiles/pmc_*.json), if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def load_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this
+    workload's bench command, and which file that was (None, None if there is none)."""
+    rel = PMC_SUMMARIES.get(workload)
+    for path in ([rel] if rel else []) + (["profiles/r01/r01h/pmc_summary.json"] if workload == "C2" else []):
+        try:
+            with open(os.path.join(ROOT, path)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        v = d.get(kernel, {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            return v, path
+    return None, None
+
+
+def host_cpus():
+    """(threads this process may run on, cgroup CPU quota or None, physical cores or None)."""
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
     except (OSError, ValueError):
-        return None
+        pass
+    cores = None
+    try:
+        seen = set()
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                    seen.add((phys, core))
+        cores = len(seen) or None
+    except OSError:
+        pass
+    return aff, quota, cores
+
+
+def _timed_legs(run, n0: int, P: int, thread_counts, target_s: float):
+    """run(n, threads) -> seconds for n packets.  Per thread count: calibrate on n0
+    packets, then time a sample sized to ~target_s of wall time (bounded by P)."""
+    legs = {}
+    for th in thread_counts:
+        n = min(P, n0 * max(1, th))
+        t = run(n, th)
+        n = int(min(P, max(n, n * target_s / max(t, 1e-6))))
+        t = run(n, th)
+        legs[th] = (n, t)
+    return legs
 
 
 def cpu_baseline(plain_host: np.ndarray, P: int, L: int, key: bytes, iv: bytes, target_s: float, gpu_cipher):
+    """The reference's own PackageEncryptor (oracle/_ref, or the restatement where it was
+    not built) on 1 core, 16 threads and every CPU this process may use; value = all CPUs."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import Oracle, ref_available
     kind = "reference" if ref_available() else "port"
     o = Oracle(kind)
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate on a small sample, then size the sample (packets x repetitions) to
-    # ~target_s of wall time on `threads` threads (target_s * threads s of CPU work)
-    n = min(P, 8192)
-    tmp = np.empty(n * L, np.uint8)
-    out = np.empty(n * L, np.uint8)
-    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, 1)
-    want = n * target_s / max(t, 1e-6)
-    n = int(min(P, max(n, want)))
-    reps = max(1, int(round(want / n)))
-    tmp = np.empty(n * L, np.uint8)
-    out = np.empty(n * L, np.uint8)
-    t = o.time_package_roundtrip(plain_host[:n * L], tmp, out, n, L, key, iv, threads, reps)
-    ok = bool(np.array_equal(tmp, gpu_cipher[:n * L])) and bool(np.array_equal(out, plain_host[:n * L]))
-    gib = 2.0 * n * L * reps / t / 2**30
-    # one core, as SURVEY.md 8(d) asks for both: ~1 s on a prefix of the same batch
-    n1 = min(n, 16384)
-    t1 = o.time_package_roundtrip(plain_host[:n1 * L], tmp[:n1 * L], out[:n1 * L], n1, L, key, iv, 1, 1)
-    n1 = int(min(n, max(n1, n1 * 1.0 / max(t1, 1e-6))))
-    t1 = o.time_package_roundtrip(plain_host[:n1 * L], tmp[:n1 * L], out[:n1 * L], n1, L, key, iv, 1, 1)
+    aff, quota, phys = host_cpus()
+    counts = sorted({1, min(16, aff), aff})
+    tmp = np.empty(P * L, np.uint8)
+    out = np.empty(P * L, np.uint8)
+
+    def run(n, th):
+        return o.time_package_roundtrip(plain_host[:n * L], tmp[:n * L], out[:n * L], n, L, key, iv, th, 1)
+
+    legs = _timed_legs(run, 512, P, counts, target_s)
+    gib = {th: 2.0 * n * L / t / 2**30 for th, (n, t) in legs.items()}
+    best = max(counts, key=lambda th: gib[th])  # a cgroup CPU quota can make "every CPU" the slower leg
+    n_b, t_b = legs[best]
+    ok = bool(np.array_equal(tmp[:n_b * L], gpu_cipher[:n_b * L])) and \
+        bool(np.array_equal(out[:n_b * L], plain_host[:n_b * L]))
     src = "oracle/_ref: reference base/rijndael.c + core/Encryptor.cpp (-O2)" if kind == "reference" \
         else "oracle/aes_oracle.c restatement (-O2)"
-    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} x {L} B packets (first {n} of the C2 batch) x {reps} passes, "
-                      f"PackageEncryptor::encrypt then ::decrypt per packet, {threads} threads; {src}; "
-                      f"{t:.2f} s wall = {t * threads:.1f} s of CPU work; matches GPU output: {ok}",
-            "single_core": {"value": round(2.0 * n1 * L / t1 / 2**30, 4), "cores": 1,
-                            "sample": f"first {n1} packets, {t1:.2f} s"},
-            "openssl_aesni": openssl_baseline(plain_host, P, L, key, iv, threads, gpu_cipher),
-            "cpu_model": _cpu_model()}
+    quota_note = (f"; this process may use {quota:g} CPUs (cgroup cpu.max) of the host's {aff} hardware threads, "
+                  f"so legs above {int(quota)} threads are throttled") if quota else ""
+    res = {"value": round(gib[best], 4), "unit": "GiB/s", "cores": best, "kind": kind,
+           "sample": f"{n_b} x {L} B packets (first {n_b} of the C2 batch), PackageEncryptor::encrypt then "
+                     f"::decrypt per packet, {best} threads (the fastest of the 1 / 16 / all-CPU legs){quota_note}; "
+                     f"{src}; {t_b:.2f} s wall; matches GPU output: {ok}",
+           "legs": {str(th): {"value": round(gib[th], 4), "threads": th, "packets": legs[th][0],
+                              "seconds": round(legs[th][1], 3)} for th in counts},
+           "host": {"affinity_cpus": aff, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
+                    "physical_cores": phys, "cpu_model": _cpu_model()},
+           "openssl_aesni": openssl_baseline(plain_host, P, L, key, iv, counts, gpu_cipher, target_s)}
+    if phys:
+        res["whole_host_projection"] = {
+            "value": round(gib[1] * phys, 2), "unit": "GiB/s", "cores": phys,
+            "note": "NOT measured: the 1-core rate x the host's physical cores (linear scaling assumed), for "
+                    "comparison with a host that gives the reference every core"}
+    return res
 
 
-def openssl_baseline(plain_host, P, L, key, iv, threads, gpu_cipher, target_s=1.0):
+def openssl_baseline(plain_host, P, L, key, iv, counts, gpu_cipher, target_s=1.0):
     """The stronger CPU comparator SURVEY.md 8(d) names: the same package-mode work
     through the host's OpenSSL EVP cfb128 (AES-NI) -- oracle/libossl_cfb.so, built by
     `make -C oracle ossl`.  None when it was not built."""
@@ -150,29 +261,23 @@ def openssl_baseline(plain_host, P, L, key, iv, threads, gpu_cipher, target_s=1.
     f.argtypes = [u8, u8, u8, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t, C.c_char_p, C.c_int, C.c_int]
     f.restype = C.c_double
     ptr = lambda a: a.ctypes.data_as(u8)  # noqa: E731
-    n = min(P, 65536)
-    tmp, out = np.empty(n * L, np.uint8), np.empty(n * L, np.uint8)
-    t = f(ptr(plain_host), ptr(tmp), ptr(out), n, L, key, len(key), iv, threads, 1)
-    if t <= 0:
+    tmp, out = np.empty(P * L, np.uint8), np.empty(P * L, np.uint8)
+
+    def run(n, th):
+        return f(ptr(plain_host), ptr(tmp), ptr(out), n, L, key, len(key), iv, th, 1)
+
+    if run(min(P, 1024), 1) <= 0:
         return None
-    n = int(min(P, max(n, n * target_s / t)))
-    tmp, out = np.empty(n * L, np.uint8), np.empty(n * L, np.uint8)
-    t = f(ptr(plain_host), ptr(tmp), ptr(out), n, L, key, len(key), iv, threads, 1)
-    ok = bool(np.array_equal(tmp, gpu_cipher[:n * L])) and bool(np.array_equal(out, plain_host[:n * L]))
-    return {"value": round(2.0 * n * L / t / 2**30, 3), "unit": "GiB/s", "cores": threads,
+    legs = _timed_legs(run, 1024, P, counts, target_s)
+    gib = {th: 2.0 * legs[th][0] * L / legs[th][1] / 2**30 for th in counts}
+    top = max(counts, key=lambda th: gib[th])
+    n, t = legs[top]
+    ok = bool(np.array_equal(tmp[:n * L], gpu_cipher[:n * L])) and bool(np.array_equal(out[:n * L], plain_host[:n * L]))
+    return {"value": round(gib[top], 3), "unit": "GiB/s", "cores": top,
             "sample": f"{n} x {L} B packets, EVP_aes_256_cfb128 encrypt then decrypt per packet (IV reset per "
-                      f"packet), {threads} threads, {t:.2f} s; matches GPU output: {ok}"}
-
-
-def _cpu_model():
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
+                      f"packet), {top} threads (fastest leg), {t:.2f} s; matches GPU output: {ok}",
+            "legs": {str(th): {"value": round(gib[th], 3), "threads": th, "packets": legs[th][0],
+                               "seconds": round(legs[th][1], 3)} for th in counts}}
 
 
 def pcie_rate(eng, ks, P, L, steps=3):
@@ -218,8 +323,7 @@ def setup_c2(args, eng, world, rank):
     desc = {"workload": "C2: 1M x 1 KiB AES-256 package-mode CFB encrypt+decrypt per GPU",
             "packets_per_gpu": P, "payload_bytes": L, "key_bits": 256, "mode": "package",
             "global_packets": P * world, "parallelism": f"packet-shard x{world}"}
-    digest = "C2" if (world == 1 and P == cfg["packets"] and L == cfg["length"]) else None
-    return dict(plain=plain, ks=ks, kw=kw, P=P, nkeys=1, scaling="weak", config=desc, digest=digest,
+    return dict(plain=plain, ks=ks, kw=kw, P=P, nkeys=1, scaling="weak", config=desc,
                 data="synthetic (counter splitmix64 payload, seed 2; key/IV from seed 1002)",
                 key=key, iv=iv, L=L, uniform=True)
 
@@ -245,7 +349,7 @@ def setup_c4(args, eng, world, rank):
             "packets_this_rank": last - first, "global_packets": len(sizes), "global_bytes": int(sizes.sum()),
             "key_bits": 256, "mode": "package", "parallelism": f"byte-balanced packet-shard x{world}"}
     return dict(plain=plain[:nbytes], ks=ks, kw=kw, P=last - first, nkeys=1, scaling="strong", config=desc,
-                digest=None, data="synthetic (splitmix64 payload seed 4, Zipf sizes seed 4004, key/IV seed 1004)",
+                data="synthetic (splitmix64 payload seed 4, Zipf sizes seed 4004, key/IV seed 1004)",
                 key=key, iv=iv, L=None, uniform=False)
 
 
@@ -267,14 +371,87 @@ def setup_c5(args, eng, world, rank):
     desc = {"workload": "C5: 65536 keys x 4 KiB AES-256 package-mode encrypt+decrypt, per-key IV",
             "packets_this_rank": P, "global_packets": Pg, "payload_bytes": L, "key_bits": 256, "mode": "package",
             "parallelism": f"packet-shard x{world} (key table replicated)"}
-    digest = "C5" if world == 1 else None
-    return dict(plain=plain[:P * L], ks=ks, kw=kw, P=P, nkeys=Pg, scaling="strong", config=desc, digest=digest,
+    return dict(plain=plain[:P * L], ks=ks, kw=kw, P=P, nkeys=Pg, scaling="strong", config=desc,
                 data="synthetic (splitmix64 payload seed 5; keys/IVs seed 1005)", key=None, iv=None, L=L,
                 uniform=False)
 
 
+def shard_key(workload: str, world: int, rank: int, P: int, L) -> str:
+    """Key of this rank's reference digest in tests/golden/digests.json "shards"
+    (oracle/gen_golden.py shard_digests)."""
+    if workload == "C2":
+        return f"C2/r{rank}" if (P, L) == (W.C2["packets"], W.C2["length"]) else ""
+    return f"{workload}/w{world}/r{rank}"
+
+
+def verify_rank(args, job, cipher, back, plain, world, rank) -> dict:
+    v = {"rank": rank}
+    if args.only is None:
+        v["roundtrip_ok"] = bool(torch.equal(back, plain))
+    key = shard_key(args.workload, world, rank, job["P"], job["L"])
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+            gold = json.load(f).get("shards", {}).get(key)
+    except (OSError, ValueError):
+        gold = None
+    if gold:
+        v["shard"] = key
+        v["cipher_sha256_matches_reference"] = hashlib.sha256(cipher.cpu().numpy()).hexdigest() == gold
+    return v
+
+
+def gather_objects(obj, world):
+    if world <= 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def alg_bytes_per_launch(nbytes: int, P: int, kw: dict, nkeys: int) -> int:
+    """Algorithmic HBM bytes of one encrypt or decrypt launch (counting only
+    what the call reads): payload in + out, the descriptor arrays actually passed
+    (in_off/out_off u64, len/key_slot u32 per packet) and the key records (272 B each:
+    round keys + IV)."""
+    per_packet = sum(sz for name, sz in (("in_off", 8), ("out_off", 8), ("lens", 4), ("key_slot", 4))
+                     if kw.get(name) is not None)
+    return int(2 * nbytes + per_packet * P + 272 * nkeys)
+
+
+def plumbing_only(args, world, rank):
+    """CPU rehearsal of the multi-rank contract (tests/test_bench_launcher.py): the
+    launcher's world/rank environment, the barrier, max-over-ranks time and the
+    per-rank verify gather, with no GPU work."""
+    from fpnn_amd.sharding import max_over_ranks, shard_range
+    barrier(world)
+    t0 = time.perf_counter()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0 + 0.001 * rank, world)
+    first, last = shard_range(W.C2["packets"] * world, world, rank)
+    ranks = gather_objects({"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                            "packets": [first, last], "shard": shard_key("C2", world, rank, W.C2["packets"],
+                                                                          W.C2["length"])}, world)
+    if rank == 0:
+        print(json.dumps({"plumbing_only": True, "n_gpus": world, "elapsed_max": elapsed, "ranks": ranks}),
+              flush=True)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if args.plumbing_only:
+        world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+        if world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        plumbing_only(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     world, rank, local = dist_setup(args)
     import fpnn_amd
     from fpnn_amd.sharding import max_over_ranks
@@ -309,30 +486,28 @@ def main():
     barrier(world)
     elapsed = time.perf_counter() - t0
     eng.set_timing(False)
-    elapsed = max_over_ranks(elapsed, world, "cuda" if args.dist_backend == "nccl" else None)
+    dev = "cuda" if args.dist_backend == "nccl" else None
+    elapsed = max_over_ranks(elapsed, world, dev)
     n_enc, ms_enc = eng.kernel_stats(fpnn_amd.K_ENCRYPT)
     n_dec, ms_dec = eng.kernel_stats(fpnn_amd.K_DECRYPT)
-    total_bytes = sum_over_ranks(nbytes, world, "cuda" if args.dist_backend == "nccl" else None)
+    names = (eng.last_kernel(fpnn_amd.K_ENCRYPT), eng.last_kernel(fpnn_amd.K_DECRYPT))
+    total_bytes = sum_over_ranks(nbytes, world, dev)
 
-    verify = {}
+    verify = None
     if not args.no_verify:
-        if args.only is None:
-            verify["roundtrip_ok"] = bool(torch.equal(back, plain))
-        if rank == 0 and job["digest"]:
-            with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
-                gold = json.load(f)[job["digest"]]
-            verify["cipher_sha256_matches_reference"] = \
-                hashlib.sha256(cipher.cpu().numpy()).hexdigest() == gold["cipher_sha256"]
+        ranks = gather_objects(verify_rank(args, job, cipher, back, plain, world, rank), world)
+        verify = {"all_ok": all(all(v for k, v in r.items() if k.endswith("_ok") or k.startswith("cipher_"))
+                                for r in ranks),
+                  "every_rank_checked_against_reference": all("cipher_sha256_matches_reference" in r for r in ranks),
+                  "ranks": ranks}
 
     directions = 2 if args.only is None else 1
     payload = float(directions) * total_bytes * args.steps
     value = payload / elapsed / 2**30
 
     # roofline for the dominant kernel: algorithmic bytes per launch
-    alg_bytes = 2.0 * nbytes + 28.0 * P + 244.0 * job["nkeys"]
+    alg_bytes = alg_bytes_per_launch(nbytes, P, kw, job["nkeys"])
     kernels = {}
-    names = {"C2": ("cfb_encrypt_chains", "cfb_decrypt_dense"), "C4": ("cfb_encrypt_queue", "cfb_decrypt_blocks"),
-             "C5": ("cfb_encrypt_coop", "cfb_decrypt_dense")}[args.workload]
     for name, n, ms in ((names[0], n_enc, ms_enc), (names[1], n_dec, ms_dec)):
         if n:
             avg_s = ms / n / 1e3
@@ -341,10 +516,11 @@ def main():
                              "payload_GiBs": round(nbytes / avg_s / 2**30, 2)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     ach = kernels[dom]["achieved_GBs"]
-    traffic = load_traffic(dom) if args.workload == "C2" else None  # the committed PMC summary is of C2
+    traffic, traffic_src = load_traffic(dom, args.workload)
     roofline = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                "alg_bytes_per_launch": int(alg_bytes), "kernels": kernels}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": dom, "alg_bytes_per_launch": alg_bytes,
+                "alg_bytes_formula": "2*payload + descriptor arrays passed per packet + 272*keys", "kernels": kernels}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and job["uniform"]:
@@ -357,7 +533,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "AES-256 GiB/s on device-resident packet batch",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,

@@ -107,6 +107,7 @@ SIGNATURES = {
     "fpnn_aes_engine_set_timing": (C.c_int, [_vp, C.c_int]),
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "fpnn_aes_engine_reset_stats": (C.c_int, [_vp]),
+    "fpnn_aes_engine_last_kernel": (C.c_char_p, [_vp, C.c_int]),
     # rijndael.h subset (include/rijndael.h)
     "rijndael_setup_encrypt": (C.c_bool, [C.POINTER(Schedule), _u8p, C.c_size_t]),
     "rijndael_cfb_encrypt": (None, [C.POINTER(Schedule), C.c_bool, _vp, _vp, C.c_size_t, _u8p,

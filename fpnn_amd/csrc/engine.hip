@@ -202,11 +202,9 @@ struct fpnn_aes_engine {
     // host-frame pipeline
     HostSlot hs[2];
     std::unique_ptr<HostPool> pool;  // created on first use
-    // side stream for the bitsliced co-kernel
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // instrumentation
     bool timing = false;
+    const char *last_kernel[2] = {"", ""};  // base name of the last main kernel per direction
     std::vector<EventPair> ev[2];
     size_t ev_used[2] = {0, 0};
 };
@@ -265,7 +263,9 @@ int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
     return FPNN_AES_OK;
 }
 
-int timing_end(fpnn_aes_engine *e, EventPair *pair) {
+// after the main kernel of a call: close its timing pair, remember what was launched
+int timing_end(fpnn_aes_engine *e, EventPair *pair, int which) {
+    e->last_kernel[which] = last_launched();
     if (pair) HIP_TRY(hipEventRecord(pair->end, e->stream));
     return FPNN_AES_OK;
 }
@@ -349,7 +349,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));
         else
             HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
-        return timing_end(e, ev);
+        return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
     }
     // One lane per chain.  Workgroup size: the smallest power of two (>= one wave) that
     // still spreads the chains over every CU -- with few chains (C3: 4096 streams) a
@@ -363,7 +363,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
     HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, threads, e->stream));
-    return timing_end(e, ev);
+    return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
 }
 
 // total_hint: the batch's total 16-byte block count when the caller knows it on the host
@@ -387,7 +387,11 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.iv_snap = e->d_snap_iv;
         k.pos_snap = e->d_snap_pos;
     }
-    bool inplace = b->in == b->out && b->out_off == nullptr;
+    // In place whenever the buffers coincide: with out_off == in_off (same array or same
+    // values) a wave may overwrite the ciphertext block another wave's lane 0 still
+    // needs, so the chunk boundaries are saved first.  (Segments moved to disjoint
+    // offsets of the same buffer are also served correctly by this path.)
+    bool inplace = b->in == b->out;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     // Uniform layout: every segment has the same block count, known on the host.
     // (Stream mode only when there is a single segment, whose position the caller
@@ -480,35 +484,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.bstart = e->d_bstart;
         k.tile_first = e->d_tile;
     }
-    // Bitsliced co-kernel: the last share of a uniform, out-of-place, one-key package
-    // batch whose packets are whole 32-block groups goes to K1b on the side stream,
-    // concurrently with K1 on the main stream.
-    uint64_t bs_pkts = 0;
-    const uint64_t nb_all = ((uint64_t)b->uniform_len + 15) >> 4;
-    if (layout != LAYOUT_GENERAL && !inplace && km == KEY_UNIFORM && e->variant.bs_frac > 0.f &&
-        (b->uniform_len & 511) == 0 && (b->stride & 15) == 0)
-        bs_pkts = (uint64_t)((double)e->variant.bs_frac * (double)b->count + 0.5);
-    if (bs_pkts > b->count) bs_pkts = b->count;
     EventPair *ev = nullptr;
-    if (bs_pkts) {
-        if (!e->side) {
-            HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-        }
-        if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-        HIP_TRY(hipEventRecord(e->ev_fork, e->stream));
-        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-        const uint64_t first = b->count - bs_pkts;
-        HIP_TRY(launch_bs_decrypt(k, b->keys->nrounds, first, bs_pkts, (uint32_t)(nb_all / 32), e->num_cus,
-                                  e->side));
-        HIP_TRY(hipEventRecord(e->ev_join, e->side));
-        k.total_blocks = first * nb_all;  // K1 takes the leading packets
-        if (!k.total_blocks) {
-            HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
-            return timing_end(e, ev);
-        }
-    }
     const uint64_t nchunks = (k.total_blocks + 63) >> 6;
     if (inplace) {
         if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks))) return rc;
@@ -518,10 +494,9 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     const uint64_t want = (nchunks + 63) / 64;  // 16 waves per workgroup x up to 4 chunks per wave step
     const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
     const int grid = (int)(want < cap ? (want ? want : 1) : cap);
-    if (!bs_pkts && (rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+    if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
     HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, stream, inplace, grid, e->stream));
-    if (bs_pkts) HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_join, 0));
-    return timing_end(e, ev);
+    return timing_end(e, ev, FPNN_AES_K_DECRYPT);
 }
 
 }  // namespace
@@ -592,10 +567,6 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
     if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
-    if (const char *v = getenv("FPNN_AES_BITSLICE_FRAC")) {
-        const float f = (float)atof(v);
-        e->variant.bs_frac = f < 0.f ? 0.f : f > 1.f ? 1.f : f;
-    }
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_GAPPED")) e->variant.dec_gapped = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
@@ -664,9 +635,6 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         if (h.kdone) (void)hipEventDestroy(h.kdone);
         if (h.st) (void)hipStreamDestroy(h.st);
     }
-    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return FPNN_AES_OK;
@@ -1395,6 +1363,11 @@ int fpnn_aes_engine_kernel_stats(fpnn_aes_engine *e, int which, uint64_t *launch
     *launches = e->ev_used[which];
     *total_ms = sum;
     return FPNN_AES_OK;
+}
+
+const char *fpnn_aes_engine_last_kernel(fpnn_aes_engine *e, int which) {
+    if (!e || which < 0 || which > 1) return "";
+    return e->last_kernel[which];
 }
 
 int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e) {

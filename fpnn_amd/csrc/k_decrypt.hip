@@ -413,6 +413,10 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
 #define FPNN_DENSE(AL, U, PF, KEYED) \
     hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
+    set_launched(layout == LAYOUT_GENERAL && b.start_mask ? "cfb_decrypt_dense"
+                 : layout == LAYOUT_FULL && km == KEY_LANE && !aligned ? "cfb_decrypt_lanekey"
+                 : layout == LAYOUT_FULL && (km == KEY_LANE || dense) ? "cfb_decrypt_dense"
+                                                                       : "cfb_decrypt_blocks");
     if (layout == LAYOUT_GENERAL && b.start_mask) {  // contiguous (or gapped) whole-block segments, one key
         if (b.blk_delta) FPNN_DENSE_R(true); else FPNN_DENSE_R(false);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks

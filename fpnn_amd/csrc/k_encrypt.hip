@@ -557,6 +557,7 @@ hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool s
                                 uint32_t *next, hipStream_t st) {
     hipError_t err = hipMemsetAsync(next, 0, sizeof(uint32_t), st);
     if (err != hipSuccess) return err;
+    set_launched("cfb_encrypt_queue");
     switch (nrounds) {
         case 10: queue_nr<10>(b, km, stream, grid, threads, next, st); break;
         case 12: queue_nr<12>(b, km, stream, grid, threads, next, st); break;
@@ -568,6 +569,7 @@ hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool s
 
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st) {
+    set_launched("cfb_encrypt_coop");
     switch (nrounds) {
         case 10: coop_nr<10>(b, layout, km, stream, grid, threads, st); break;
         case 12: coop_nr<12>(b, layout, km, stream, grid, threads, st); break;
@@ -579,8 +581,15 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
 
 int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }
 
+namespace {
+thread_local const char *g_launched = "";
+}
+const char *last_launched() { return g_launched; }
+void set_launched(const char *name) { g_launched = name; }
+
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
                                  bool stream, int grid, int threads, hipStream_t st) {
+    set_launched("cfb_encrypt_chains");
     switch (nrounds) {
         case 10: enc_nr<10>(b, v, layout, km, stream, grid, threads, st); break;
         case 12: enc_nr<12>(b, v, layout, km, stream, grid, threads, st); break;

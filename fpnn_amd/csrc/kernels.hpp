@@ -67,7 +67,6 @@ enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 // Kernel build variant chosen per engine (defaults tuned on MI355X; overridable with
 // FPNN_AES_TABLES / FPNN_AES_ENC_CHUNK for A/B measurements).
 struct Variant {
-    float bs_frac = 0.0f;  // share of uniform package-decrypt packets given to the bitsliced K1b
     int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
     int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
@@ -78,6 +77,10 @@ struct Variant {
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
+// Base name ("cfb_decrypt_dense", ...) of the main kernel the last launch_* call on this
+// thread queued (the variant the dispatch actually chose; instrumentation and bench labels).
+const char *last_launched();
+void set_launched(const char *name);
 // threads = workgroup size (64..1024, multiple of 64): few chains are spread over all
 // CUs with small workgroups instead of packed into a few full ones.
 // Frame scan of received segments (framing.hip).
@@ -121,10 +124,6 @@ hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool s
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
                                  bool stream, bool inplace, int grid, hipStream_t st);
-// Bitsliced K1b over packets [first_pkt, first_pkt + npkt) of a uniform package batch
-// (uniform key; groups_per_pkt = blocks per packet / 32).
-hipError_t launch_bs_decrypt(const KBatch &b, int nrounds, uint64_t first_pkt, uint64_t npkt,
-                             uint32_t groups_per_pkt, int grid, hipStream_t st);
 hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
                                 hipStream_t st);
 // General-layout block map: bstart[] and *total (device); wg_sums scratch of

@@ -124,6 +124,10 @@ class Engine:
     def reset_stats(self):
         check(lib.fpnn_aes_engine_reset_stats(self._h), "reset_stats")
 
+    def last_kernel(self, which: int) -> str:
+        """Base name of the kernel variant the last call queued for that direction."""
+        return lib.fpnn_aes_engine_last_kernel(self._h, which).decode()
+
     # -- synthetic data ------------------------------------------------------------------
     def fill_synthetic(self, dst: torch.Tensor, seed: int, byte_offset: int = 0, nbytes: Optional[int] = None):
         n = dst.numel() * dst.element_size() if nbytes is None else nbytes

@@ -218,6 +218,9 @@ int fpnn_aes_engine_set_timing(fpnn_aes_engine *e, int enable);
 int fpnn_aes_engine_kernel_stats(fpnn_aes_engine *e, int which /* FPNN_AES_K_* */, uint64_t *launches,
                                  double *total_ms);
 int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e);
+/* Name of the kernel variant the last call queued as its main kernel for that direction
+ * ("cfb_decrypt_dense", "cfb_encrypt_queue", ...; "" before any call).  Static storage. */
+const char *fpnn_aes_engine_last_kernel(fpnn_aes_engine *e, int which);
 #define FPNN_AES_K_DECRYPT 0
 #define FPNN_AES_K_ENCRYPT 1
 

@@ -9,7 +9,8 @@ container only).  Writes data only -- inputs and the reference's outputs:
   cfb_cases.json    random rijndael_cfb_encrypt calls (16/24/32-byte keys, pos carry)
   package_cases.json PackageEncryptor encrypt / decrypt / encrypt(std::string*) frames
   stream_cases.json StreamEncryptor call sequences (state carried across frames)
-  digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5)
+  digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5) and
+                    per-rank shard digests of the bench workloads (C2 r0-7, C4/C5 at world 1/2/4/8)
 
 Usage: python oracle/gen_golden.py [--skip-large]
 """
@@ -179,9 +180,65 @@ def digest_c3(ref: Oracle, threads: int):
             "first_stream_sha256": per[0].hex()}
 
 
+def shard_digests(ref: Oracle, threads: int):
+    """Per-rank reference digests of the bench's sharded workloads (bench.py setup_*):
+    C2 weak scaling -- rank r owns packets [r*P, (r+1)*P) of one global batch, for any
+    world size, so one digest per rank index r = 0..7; C4 (Zipf, byte-balanced contiguous
+    ranges) and C5 (even packet split) strong scaling -- one digest per (world, rank) for
+    world 1, 2, 4, 8.  The shard split is fpnn_amd/sharding.py's shard_range."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from fpnn_amd.sharding import shard_range
+    out = {}
+    c = configs.C2
+    key, iv = configs.single_key(c)
+    P, L = c["packets"], c["length"]
+    kb, ib = np.frombuffer(key, np.uint8).copy(), np.frombuffer(iv, np.uint8).copy()
+    for r in range(8):
+        inp = synth_bytes(P * L, c["payload_seed"], offset=r * P * L, threads=threads)
+        enc = np.empty_like(inp)
+        ref.package_batch(True, inp, enc, P, stride=L, uniform_len=L, keys=kb, keylen=len(key), ivs=ib,
+                          threads=threads)
+        out[f"C2/r{r}"] = hashlib.sha256(enc).hexdigest()
+        print("C2 shard", r, out[f"C2/r{r}"], flush=True)
+    # C4: the whole 4 GiB batch once, then each shard's byte range
+    c = configs.C4
+    sizes = configs.zipf_sizes(c).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1])]).astype(np.uint64)
+    total = int(sizes.sum())
+    key, iv = configs.single_key(c)
+    inp = synth_bytes(total, c["payload_seed"], threads=threads)
+    enc = np.empty_like(inp)
+    ref.package_batch(True, inp, enc, len(sizes), in_off=offs, lens=sizes.astype(np.uint32),
+                      keys=np.frombuffer(key, np.uint8).copy(), keylen=len(key),
+                      ivs=np.frombuffer(iv, np.uint8).copy(), threads=threads)
+    del inp
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            a, b = shard_range(len(sizes), world, r, sizes)
+            lo = int(offs[a]) if b > a else 0
+            hi = int(offs[b - 1] + sizes[b - 1]) if b > a else 0
+            out[f"C4/w{world}/r{r}"] = hashlib.sha256(enc[lo:hi]).hexdigest()
+    del enc
+    # C5: 65 536 keyed packets, split evenly
+    c = configs.C5
+    keys, ivs = configs.many_keys(c)
+    P, L = c["packets"], c["length"]
+    inp = synth_bytes(P * L, c["payload_seed"], threads=threads)
+    enc = np.empty_like(inp)
+    ref.package_batch(True, inp, enc, P, stride=L, uniform_len=L, key_slot=np.arange(P, dtype=np.uint32), keys=keys,
+                      keylen=c["keylen"], ivs=ivs, threads=threads)
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            a, b = shard_range(P, world, r)
+            out[f"C5/w{world}/r{r}"] = hashlib.sha256(enc[a * L:b * L]).hexdigest()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
+    ap.add_argument("--shards-only", action="store_true",
+                    help="only (re)compute the per-rank shard digests into digests.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -192,6 +249,12 @@ def main():
             json.dump(obj, f, indent=1)
         print("wrote", name)
 
+    if args.shards_only:
+        with open(os.path.join(GOLDEN, "digests.json")) as f:
+            d = json.load(f)
+        d["shards"] = shard_digests(ref, args.threads)
+        dump("digests.json", d)
+        return
     dump("kat.json", gen_kat(ref))
     dump("cfb_cases.json", gen_cfb_cases(ref))
     dump("package_cases.json", gen_package_cases(ref))
@@ -205,6 +268,7 @@ def main():
         print("C5", d["C5"])
         d["C3"] = digest_c3(ref, args.threads)
         print("C3", d["C3"])
+        d["shards"] = shard_digests(ref, args.threads)
         dump("digests.json", d)
 
 
