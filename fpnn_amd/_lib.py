@@ -81,6 +81,10 @@ SIGNATURES = {
     "fpnn_aes_last_error": (C.c_char_p, []),
     "fpnn_aes_version": (C.c_char_p, []),
     "fpnn_aes_setup_encrypt": (C.c_int, [C.POINTER(Schedule), _u8p, C.c_size_t]),
+    "fpnn_aes_setup_decrypt": (C.c_int, [C.POINTER(Schedule), _u8p, C.c_size_t]),
+    "fpnn_aes_ecb_host": (C.c_int, [_vp, C.POINTER(Schedule), C.c_int, _vp, _vp, C.c_size_t]),
+    "fpnn_aes_cbc_host": (C.c_int, [_vp, C.POINTER(Schedule), C.c_int, _vp, _vp, C.c_size_t, _u8p]),
+    "fpnn_aes_ofb_host": (C.c_int, [_vp, C.POINTER(Schedule), _vp, _vp, C.c_size_t, _u8p, C.POINTER(C.c_size_t)]),
     "fpnn_aes_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "fpnn_aes_engine_create": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
     "fpnn_aes_engine_destroy": (C.c_int, [_vp]),
@@ -108,8 +112,14 @@ SIGNATURES = {
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "fpnn_aes_engine_reset_stats": (C.c_int, [_vp]),
     "fpnn_aes_engine_last_kernel": (C.c_char_p, [_vp, C.c_int]),
-    # rijndael.h subset (include/rijndael.h)
+    # rijndael.h (include/rijndael.h)
     "rijndael_setup_encrypt": (C.c_bool, [C.POINTER(Schedule), _u8p, C.c_size_t]),
+    "rijndael_setup_decrypt": (C.c_bool, [C.POINTER(Schedule), _u8p, C.c_size_t]),
+    "rijndael_encrypt": (None, [C.POINTER(Schedule), _vp, _vp]),
+    "rijndael_decrypt": (None, [C.POINTER(Schedule), _vp, _vp]),
+    "rijndael_cbc_encrypt": (None, [C.POINTER(Schedule), _vp, _vp, C.c_size_t, _u8p]),
+    "rijndael_cbc_decrypt": (None, [C.POINTER(Schedule), _vp, _vp, C.c_size_t, _u8p]),
+    "rijndael_ofb_encrypt": (None, [C.POINTER(Schedule), _vp, _vp, C.c_size_t, _u8p, C.POINTER(C.c_size_t)]),
     "rijndael_cfb_encrypt": (None, [C.POINTER(Schedule), C.c_bool, _vp, _vp, C.c_size_t, _u8p,
                                     C.POINTER(C.c_size_t)]),
 }

@@ -194,6 +194,60 @@ __device__ __forceinline__ void aes_encrypt_blocks(uint4 (&st)[M], const RoundKe
 }
 
 // ---------------------------------------------------------------------------
+// Inverse cipher (base/rijndael.c:961-1068, rijndael_decrypt) for the rest of the
+// rijndael.h surface (ECB / CBC decrypt).  The LDS image is the same layout filled from
+// Td0 (td0le) instead of Te0, followed by the inverse S-box packed four entries per word
+// and replicated 32x: entry x of copy c at byte kIsboxBase + (x & ~3) * 32 + c * 4 + (x & 3),
+// so lane l reads bank l & 31 -- conflict-free -- for 8 KiB instead of 32.
+constexpr uint32_t kIsboxBase = 131072u;
+constexpr uint32_t kIsboxBytes = 8192u;
+
+__device__ __forceinline__ void lds_fill_isbox(uint32_t *lds_words, const uint8_t *__restrict__ isbox) {
+    for (uint32_t i = threadIdx.x; i < kIsboxBytes / 4; i += blockDim.x) {
+        const uint32_t q = i >> 5;  // group of four entries; copy = i & 31
+        lds_words[(kIsboxBase >> 2) + i] = (uint32_t)isbox[4 * q] | ((uint32_t)isbox[4 * q + 1] << 8) |
+                                           ((uint32_t)isbox[4 * q + 2] << 16) | ((uint32_t)isbox[4 * q + 3] << 24);
+    }
+}
+
+// inverse S-box of byte j of w, placed at byte k of the result
+template <int J, int K>
+__device__ __forceinline__ uint32_t isb(const char *lds, uint32_t lb0, uint32_t w) {
+    const uint32_t x = (w >> (8 * J)) & 0xffu;
+    const uint32_t v = *reinterpret_cast<const uint8_t *>(lds + kIsboxBase + ((x & ~3u) << 5) + (x & 3u) + lb0);
+    return v << (8 * K);
+}
+
+// One block through the inverse cipher with the decryption schedule rk (block byte
+// order, the reference's setup_decrypt rk[] byte-swapped).  T holds Td0..Td3.
+template <int NR, int NT>
+__device__ __forceinline__ uint4 aes_decrypt_block(uint4 in, const RoundKeys<NR> &rk, const Tables4<NT> &T) {
+    uint32_t s0 = in.x ^ rk.k[0], s1 = in.y ^ rk.k[1], s2 = in.z ^ rk.k[2], s3 = in.w ^ rk.k[3];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {  // column c takes rows 0..3 from columns c, c-1, c-2, c-3
+        const uint32_t t0 = xor3(xor3(T.template t<0>(s0), T.template t<1>(s3), T.template t<2>(s2)),
+                                 T.template t<3>(s1), rk.k[4 * r + 0]);
+        const uint32_t t1 = xor3(xor3(T.template t<0>(s1), T.template t<1>(s0), T.template t<2>(s3)),
+                                 T.template t<3>(s2), rk.k[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(T.template t<0>(s2), T.template t<1>(s1), T.template t<2>(s0)),
+                                 T.template t<3>(s3), rk.k[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(T.template t<0>(s3), T.template t<1>(s2), T.template t<2>(s1)),
+                                 T.template t<3>(s0), rk.k[4 * r + 3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint32_t lb = T.lb.lb0;
+    auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+        return (isb<0, 0>(T.lds, lb, a) | isb<1, 1>(T.lds, lb, b) | isb<2, 2>(T.lds, lb, c) | isb<3, 3>(T.lds, lb, d)) ^ k;
+    };
+    uint4 o;
+    o.x = last(s0, s3, s2, s1, rk.k[4 * NR + 0]);
+    o.y = last(s1, s0, s3, s2, rk.k[4 * NR + 1]);
+    o.z = last(s2, s1, s0, s3, rk.k[4 * NR + 2]);
+    o.w = last(s3, s2, s1, s0, rk.k[4 * NR + 3]);
+    return o;
+}
+
+// ---------------------------------------------------------------------------
 // 16-byte block helpers.  Interior blocks use (possibly unaligned) dwordx4 accesses;
 // edge blocks of a segment use byte accesses restricted to the segment so that no
 // byte outside [in, in+len) is read and none outside [out, out+len) is written.

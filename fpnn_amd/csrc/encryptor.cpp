@@ -52,6 +52,24 @@ int cfb(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *o
                              p_num);
 }
 
+// rijndael.h has no error path: report and abort (never a CPU fallback)
+void or_abort(int rc, const char *fn) {
+    if (rc == FPNN_AES_OK) return;
+    fprintf(stderr, "%s (fpnn_aes, MI355X): %s\n", fn, describe(rc).c_str());
+    abort();
+}
+
+fpnn_aes_engine *engine_or_abort(const char *fn) {
+    int rc;
+    fpnn_aes_engine *e = thread_engine(&rc);
+    if (!e) or_abort(rc ? rc : FPNN_AES_ERR_NODEV, fn);
+    return e;
+}
+
+const fpnn_aes_schedule *sched(const rijndael_context *ctx) {
+    return reinterpret_cast<const fpnn_aes_schedule *>(ctx);
+}
+
 void cfb_or_throw(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *out, size_t len,
                   uint8_t ivec[16], size_t *p_num) {
     const int rc = cfb(ctx, encrypt, in, out, len, ivec, p_num);
@@ -66,13 +84,41 @@ bool rijndael_setup_encrypt(rijndael_context *ctx, const uint8_t *key, size_t ke
     return fpnn_aes_setup_encrypt(reinterpret_cast<fpnn_aes_schedule *>(ctx), key, keylen) == FPNN_AES_OK;
 }
 
+bool rijndael_setup_decrypt(rijndael_context *ctx, const uint8_t *key, size_t keylen) {
+    return fpnn_aes_setup_decrypt(reinterpret_cast<fpnn_aes_schedule *>(ctx), key, keylen) == FPNN_AES_OK;
+}
+
+void rijndael_encrypt(const rijndael_context *ctx, const uint8_t plain[16], uint8_t cipher[16]) {
+    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_encrypt"), sched(ctx), 1, plain, cipher, 1),
+             "rijndael_encrypt");
+}
+
+void rijndael_decrypt(const rijndael_context *ctx, const uint8_t cipher[16], uint8_t plain[16]) {
+    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_decrypt"), sched(ctx), 0, cipher, plain, 1),
+             "rijndael_decrypt");
+}
+
+void rijndael_cbc_encrypt(const rijndael_context *ctx, const uint8_t *plain, uint8_t *cipher, size_t len,
+                          uint8_t ivec[16]) {
+    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_encrypt"), sched(ctx), 1, plain, cipher, len, ivec),
+             "rijndael_cbc_encrypt");
+}
+
+void rijndael_cbc_decrypt(const rijndael_context *ctx, const uint8_t *cipher, uint8_t *plain, size_t len,
+                          uint8_t ivec[16]) {
+    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_decrypt"), sched(ctx), 0, cipher, plain, len, ivec),
+             "rijndael_cbc_decrypt");
+}
+
 void rijndael_cfb_encrypt(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *out, size_t len,
                           uint8_t ivec[16], size_t *p_num) {
-    const int rc = cfb(ctx, encrypt, in, out, len, ivec, p_num);
-    if (rc != FPNN_AES_OK) {
-        fprintf(stderr, "rijndael_cfb_encrypt (fpnn_aes, MI355X): %s\n", describe(rc).c_str());
-        abort();  // the reference has no error path; never fall back to a CPU cipher
-    }
+    or_abort(cfb(ctx, encrypt, in, out, len, ivec, p_num), "rijndael_cfb_encrypt");
+}
+
+void rijndael_ofb_encrypt(const rijndael_context *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16],
+                          size_t *p_num) {
+    or_abort(fpnn_aes_ofb_host(engine_or_abort("rijndael_ofb_encrypt"), sched(ctx), in, out, len, ivec, p_num),
+             "rijndael_ofb_encrypt");
 }
 
 }  // extern "C"

@@ -165,18 +165,12 @@ struct fpnn_aes_engine {
     bool own_stream = false;
     int num_cus = 256;
     Variant variant;
-    uint8_t *d_tables = nullptr;  // t0le[256] (1 KiB) then sbox[256]
+    uint8_t *d_tables = nullptr;  // t0le[256] (1 KiB), sbox[256], td0le[256] (1 KiB), isbox[256]
     // general-layout scratch
     uint64_t *d_bstart = nullptr;
     uint64_t cap_bstart = 0;
     uint64_t *d_wgsums = nullptr;
     uint64_t cap_wgsums = 0;
-    uint64_t *d_tile = nullptr;
-    uint64_t cap_tile = 0;
-    uint64_t *d_mask = nullptr;  // contiguous ragged decrypt: segment-start bits per chunk
-    uint64_t cap_mask = 0;
-    int32_t *d_blk_delta = nullptr, *d_chunk_delta = nullptr;  // gapped ragged decrypt
-    uint64_t cap_blk_delta = 0, cap_chunk_delta = 0;
     uint4 *d_boundary = nullptr;
     uint64_t cap_boundary = 0;
     uint4 *d_snap_iv = nullptr;  // stream-decrypt state snapshot
@@ -193,6 +187,8 @@ struct fpnn_aes_engine {
     uint64_t cap_fr_off = 0;
     uint32_t *d_fr_slot = nullptr;  // package receive: key slot per frame slot
     uint64_t cap_fr_slot = 0;
+    RaggedPlan *d_plan = nullptr;  // K1r: one entry per wave of the decrypt grid
+    uint64_t cap_plan = 0;
     uint64_t *d_total = nullptr;  // [0] ragged block total, [1] non-contiguous segments
     uint64_t *h_total = nullptr;  // pinned
     // host staging for fpnn_aes_cfb_host
@@ -220,8 +216,11 @@ struct fpnn_aes_keyset {
 
 namespace {
 
+// device table block: t0le (1 KiB) | sbox (256) | td0le (1 KiB) | isbox (256)
 const uint32_t *t0le_of(const fpnn_aes_engine *e) { return reinterpret_cast<const uint32_t *>(e->d_tables); }
 const uint8_t *sbox_of(const fpnn_aes_engine *e) { return e->d_tables + 1024; }
+const uint32_t *td0le_of(const fpnn_aes_engine *e) { return reinterpret_cast<const uint32_t *>(e->d_tables + 1280); }
+const uint8_t *isbox_of(const fpnn_aes_engine *e) { return e->d_tables + 2304; }
 
 struct DeviceGuard {
     int prev = -1;
@@ -366,12 +365,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
 }
 
-// total_hint: the batch's total 16-byte block count when the caller knows it on the host
-// (the host-frame paths), which saves the general layout's device->host round trip.
-constexpr uint64_t kNoHint = ~0ull;
-
-int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream,
-                uint64_t total_hint = kNoHint) {
+int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
     int rc = check_batch(e, b);
     if (rc) return rc;
     if (stream && b->count && (!iv_state || !pos_state || ((uintptr_t)iv_state & 15))) return FPNN_AES_ERR_ARG;
@@ -387,11 +381,10 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.iv_snap = e->d_snap_iv;
         k.pos_snap = e->d_snap_pos;
     }
-    // In place whenever the buffers coincide: with out_off == in_off (same array or same
-    // values) a wave may overwrite the ciphertext block another wave's lane 0 still
-    // needs, so the chunk boundaries are saved first.  (Segments moved to disjoint
-    // offsets of the same buffer are also served correctly by this path.)
-    bool inplace = b->in == b->out;
+    // In place whenever the buffers coincide (K1 / K1d: a wave may overwrite the
+    // ciphertext block another wave's lane 0 still needs, so chunk boundaries are saved
+    // first; K1r saves its waves' boundaries in its plan in any case).
+    const bool inplace = b->in == b->out;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     // Uniform layout: every segment has the same block count, known on the host.
     // (Stream mode only when there is a single segment, whose position the caller
@@ -419,83 +412,34 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.nb_uniform = (uint32_t)nb;
             k.magic = magic_for((uint32_t)nb);
         }
-    } else if (stream && km == KEY_LANE && !b->len && e->variant.dec_dense && b->uniform_len >= 1024 &&
-               b->uniform_len % 1024 == 0 && (b->in_off || (!b->out_off && b->stride == b->uniform_len)) &&
-               ((uint64_t)b->uniform_len >> 4) * b->count < (1ull << 32)) {
-        // dense stream decrypt, one key slot per stream, whole 64-block chunks (C3): when
-        // every stream is at CFB position 0 and (offset arrays) stream s sits at s * L
-        // (checked on the device; one host sync), it is K1d keyed with the streams'
-        // carried IVs, and the new state is each stream's last ciphertext block (written
-        // first: the decrypt may run in place)
-        HIP_TRY(launch_pos_check(k, e->d_total + 1, e->stream));
-        HIP_TRY(hipMemcpyAsync(e->h_total + 1, e->d_total + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-        HIP_TRY(hipStreamSynchronize(e->stream));
-        if (e->h_total[1] == 0) {
-            const uint64_t nb = b->uniform_len >> 4;
-            k.in_off = k.out_off = nullptr;
-            k.stride = b->uniform_len;
-            inplace = b->in == b->out;  // out_off may repeat in_off
-            HIP_TRY(launch_stream_dense_state(k, e->stream));
-            layout = LAYOUT_FULL;
-            k.total_blocks = nb * b->count;
-            k.nb_uniform = (uint32_t)nb;
-            k.magic = magic_for((uint32_t)nb);
-            k.seg_iv = e->d_snap_iv;
-        }
     }
     if (layout == LAYOUT_GENERAL) {
+        // K1r: block-map scan, per-wave plan and decrypt all on the device; the host
+        // never learns the block total, so nothing here waits for the GPU
         const uint64_t nwg = (b->count + 1023) / 1024;
         if ((rc = grow(e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
         if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
+        const int grid = e->num_cus;
+        if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
         HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
-        uint64_t total = total_hint;
-        // Package mode, one key, and the host has to wait for the total anyway: also ask
-        // whether the segments are contiguous whole blocks, which K1d decrypts with
-        // dense addressing and a start-bit mask instead of a per-lane segment search.
-        const bool try_dense = !stream && km == KEY_UNIFORM && total == kNoHint && e->variant.dec_dense;
-        if (try_dense) HIP_TRY(launch_contig_check(k, e->d_bstart, e->d_total + 1, e->stream));
-        bool contiguous = false, gapped = false;
-        if (total == kNoHint) {
-            HIP_TRY(hipMemcpyAsync(e->h_total, e->d_total, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-            HIP_TRY(hipStreamSynchronize(e->stream));
-            total = e->h_total[0];
-            contiguous = try_dense && e->h_total[1] == 0;
-            // whole-block segments with gaps between them (wire frames: 4-byte length
-            // prefixes): K1d ragged with a per-segment address delta
-            gapped = try_dense && !contiguous && e->h_total[2] == 0 && e->variant.dec_gapped && total < (1ull << 32);
-        }
-        if (!total) return FPNN_AES_OK;
-        const uint64_t nchunks = (total + 63) >> 6;
-        if (contiguous || gapped) {
-            if ((rc = grow(e->d_mask, e->cap_mask, nchunks))) return rc;
-            if (gapped) {
-                if ((rc = grow(e->d_blk_delta, e->cap_blk_delta, total))) return rc;
-                if ((rc = grow(e->d_chunk_delta, e->cap_chunk_delta, nchunks))) return rc;
-                k.blk_delta = e->d_blk_delta;
-                k.chunk_delta = e->d_chunk_delta;
-            }
-            HIP_TRY(launch_start_mask(k, e->d_bstart, e->d_mask, k.blk_delta ? e->d_blk_delta : nullptr,
-                                      e->d_chunk_delta, nchunks, e->stream));
-            k.start_mask = e->d_mask;
-        }
-        if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
-        HIP_TRY(launch_tile_map(k, stream, e->d_bstart, e->d_tile, nchunks, e->stream));
-        k.total_blocks = total;
         k.bstart = e->d_bstart;
-        k.tile_first = e->d_tile;
+        EventPair *ev = nullptr;
+        if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, grid, e->stream));
+        return timing_end(e, ev, FPNN_AES_K_DECRYPT);
     }
     EventPair *ev = nullptr;
     const uint64_t nchunks = (k.total_blocks + 63) >> 6;
     if (inplace) {
         if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks))) return rc;
-        HIP_TRY(launch_boundary_save(k, layout, stream, e->d_boundary, nchunks, e->stream));
+        HIP_TRY(launch_boundary_save(k, e->d_boundary, nchunks, e->stream));
         k.boundary = e->d_boundary;
     }
     const uint64_t want = (nchunks + 63) / 64;  // 16 waves per workgroup x up to 4 chunks per wave step
     const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
     const int grid = (int)(want < cap ? (want ? want : 1) : cap);
     if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, stream, inplace, grid, e->stream));
+    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, inplace, grid, e->stream));
     return timing_end(e, ev, FPNN_AES_K_DECRYPT);
 }
 
@@ -522,13 +466,20 @@ const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
 
 const char *fpnn_aes_version(void) {
     return "fpnn_aes 0.1 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
-           "decrypt: K1d dense/keyed/ragged, K1k lane keys, K1 general, one lane per block; "
+           "decrypt: K1d dense/keyed, K1k lane keys, K1r ragged (no host sync), K1 uniform, one lane per block; "
            "encrypt: K2 lane per chain, K2c/K2q quad per chain)";
 }
 
 int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen) {
     if (!ctx || !key) return FPNN_AES_ERR_ARG;
     const int nr = expand_key_be(ctx->rk, key, keylen);
+    ctx->nrounds = nr;
+    return nr ? FPNN_AES_OK : FPNN_AES_ERR_KEYLEN;
+}
+
+int fpnn_aes_setup_decrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen) {
+    if (!ctx || !key) return FPNN_AES_ERR_ARG;
+    const int nr = expand_key_dec_be(ctx->rk, key, keylen);
     ctx->nrounds = nr;
     return nr ? FPNN_AES_OK : FPNN_AES_ERR_KEYLEN;
 }
@@ -583,10 +534,12 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
             if (err != hipSuccess) { rc = hip_fail(err, "hipStreamCreate"); break; }
             e->own_stream = true;
         }
-        hipError_t err = hipMalloc(reinterpret_cast<void **>(&e->d_tables), 1024 + 256);
+        hipError_t err = hipMalloc(reinterpret_cast<void **>(&e->d_tables), 2 * (1024 + 256));
         if (err != hipSuccess) { rc = hip_fail(err, "hipMalloc(tables)"); break; }
         err = hipMemcpy(e->d_tables, kTables.t0le, 1024, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1024, kTables.sbox, 256, hipMemcpyHostToDevice);
+        if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1280, kTables.td0le, 1024, hipMemcpyHostToDevice);
+        if (err == hipSuccess) err = hipMemcpy(e->d_tables + 2304, kTables.isbox, 256, hipMemcpyHostToDevice);
         if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
         err = hipMalloc(reinterpret_cast<void **>(&e->d_total), 4 * sizeof(uint64_t));  // total, contiguity, gapped
         if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), 4 * sizeof(uint64_t), 0);
@@ -607,10 +560,6 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_tables);
     (void)hipFree(e->d_bstart);
     (void)hipFree(e->d_wgsums);
-    (void)hipFree(e->d_tile);
-    (void)hipFree(e->d_mask);
-    (void)hipFree(e->d_blk_delta);
-    (void)hipFree(e->d_chunk_delta);
     (void)hipFree(e->d_boundary);
     (void)hipFree(e->d_snap_iv);
     (void)hipFree(e->d_snap_pos);
@@ -619,6 +568,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_buckets);
     (void)hipFree(e->d_fr_off);
     (void)hipFree(e->d_fr_slot);
+    (void)hipFree(e->d_plan);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_total) (void)hipHostFree(e->h_total);
@@ -656,8 +606,8 @@ int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t 
     if ((rc = grow(e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
     if ((rc = grow(e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
     const uint64_t nchunks = (max_blocks + 63) / 64;
-    if ((rc = grow(e->d_tile, e->cap_tile, nchunks + 1))) return rc;
     if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
+    if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)e->num_cus * (kThreads / 64)))) return rc;
     return FPNN_AES_OK;
 }
 
@@ -855,6 +805,112 @@ int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
 
 // ---- single call from host memory ------------------------------------------------
 
+}  // extern "C"
+
+namespace {
+
+// pinned + device staging of the synchronous single-call paths, grown on demand
+int stage_reserve(fpnn_aes_engine *e, uint64_t need) {
+    if (need <= e->cap_stage) return FPNN_AES_OK;
+    uint64_t n = e->cap_stage ? e->cap_stage : 65536;
+    while (n < need) n *= 2;
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->d_stage) (void)hipFree(e->d_stage);
+    e->h_stage = nullptr;
+    e->d_stage = nullptr;
+    e->cap_stage = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_stage), n, 0));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stage), n));
+    e->cap_stage = n;
+    return FPNN_AES_OK;
+}
+
+// DevKey of a host schedule (rijndael_context layout, big-endian rk words)
+void devkey_from_schedule(DevKey *hk, const fpnn_aes_schedule *ctx) {
+    memset(hk, 0, sizeof *hk);
+    for (int k = 0; k < 4 * (ctx->nrounds + 1); k++) hk->rk[k] = bswap32(ctx->rk[k]);
+    hk->nrounds = (uint32_t)ctx->nrounds;
+}
+
+bool valid_rounds(int nr) { return nr == 10 || nr == 12 || nr == 14; }
+
+// One synchronous rijndael.h call in the non-CFB modes (k_modes.hip).  Staging:
+// [DevKey 272][iv 16][pos 4 | pad 12][in: in_bytes, 16-padded][out: out_bytes]
+int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const uint8_t *in, uint64_t in_copy,
+               uint64_t in_bytes, uint8_t *out, uint64_t out_copy, uint64_t nblocks, uint64_t len, uint8_t *ivec,
+               size_t *p_num) {
+    const uint64_t hdr = sizeof(DevKey) + 32;
+    const uint64_t ipad = (in_bytes + 15) & ~15ull, opad = (std::max(out_copy, nblocks * 16) + 15) & ~15ull;
+    DeviceGuard g(e->device);
+    if (int rc = stage_reserve(e, hdr + ipad + opad)) return rc;
+    devkey_from_schedule(reinterpret_cast<DevKey *>(e->h_stage), ctx);
+    uint8_t *h_iv = e->h_stage + sizeof(DevKey);
+    uint32_t *h_pos = reinterpret_cast<uint32_t *>(h_iv + 16);
+    if (ivec) memcpy(h_iv, ivec, 16); else memset(h_iv, 0, 16);
+    *h_pos = p_num ? (uint32_t)*p_num : 0u;
+    if (in_copy) memcpy(e->h_stage + hdr, in, in_copy);
+    if (ipad > in_copy) memset(e->h_stage + hdr + in_copy, 0, ipad - in_copy);  // CBC: zero padding
+    HIP_TRY(hipMemcpyAsync(e->d_stage, e->h_stage, hdr + ipad, hipMemcpyHostToDevice, e->stream));
+    ModeArgs a;
+    a.in = e->d_stage + hdr;
+    a.out = e->d_stage + hdr + ipad;
+    a.nblocks = nblocks;
+    a.len = len;
+    a.key = reinterpret_cast<const DevKey *>(e->d_stage);
+    a.iv = e->d_stage + sizeof(DevKey);
+    a.pos = reinterpret_cast<uint32_t *>(a.iv + 16);
+    a.t0le = t0le_of(e);
+    a.td0le = td0le_of(e);
+    a.isbox = isbox_of(e);
+    HIP_TRY(launch_block_modes(a, ctx->nrounds, mode, e->num_cus, e->stream));
+    e->last_kernel[FPNN_AES_K_ENCRYPT] = last_launched();
+    HIP_TRY(hipMemcpyAsync(h_iv, a.iv, 32, hipMemcpyDeviceToHost, e->stream));
+    if (out_copy) HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + ipad, a.out, out_copy, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (out_copy) memcpy(out, e->h_stage + hdr + ipad, out_copy);
+    if (ivec && mode != MODE_CBC_DEC) memcpy(ivec, h_iv, 16);
+    if (p_num) *p_num = *h_pos;
+    return FPNN_AES_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fpnn_aes_ecb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in, uint8_t *out,
+                      size_t nblocks) {
+    if (!e || !ctx || (nblocks && (!in || !out))) return FPNN_AES_ERR_ARG;
+    if (!valid_rounds(ctx->nrounds)) return FPNN_AES_ERR_KEYLEN;
+    if (!nblocks) return FPNN_AES_OK;
+    return modes_call(e, ctx, encrypt ? MODE_ECB_ENC : MODE_ECB_DEC, in, 16ull * nblocks, 16ull * nblocks, out,
+                      16ull * nblocks, nblocks, 0, nullptr, nullptr);
+}
+
+int fpnn_aes_cbc_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in, uint8_t *out,
+                      size_t len, uint8_t ivec[16]) {
+    if (!e || !ctx || !ivec || (len && (!in || !out))) return FPNN_AES_ERR_ARG;
+    if (!valid_rounds(ctx->nrounds)) return FPNN_AES_ERR_KEYLEN;
+    if (!len) return FPNN_AES_OK;
+    const uint64_t nb = (len + 15) / 16, whole = 16 * nb;
+    if (encrypt)  // reads len bytes (the last block zero-padded), writes whole blocks
+        return modes_call(e, ctx, MODE_CBC_ENC, in, len, whole, out, whole, nb, len, ivec, nullptr);
+    // decrypt reads whole blocks, writes len bytes; ivec := the last ciphertext block
+    uint8_t last[16];
+    memcpy(last, in + whole - 16, 16);  // before an in-place call overwrites it
+    const int rc = modes_call(e, ctx, MODE_CBC_DEC, in, whole, whole, out, len, nb, len, ivec, nullptr);
+    if (rc == FPNN_AES_OK) memcpy(ivec, last, 16);
+    return rc;
+}
+
+int fpnn_aes_ofb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, const uint8_t *in, uint8_t *out, size_t len,
+                      uint8_t ivec[16], size_t *p_num) {
+    if (!e || !ctx || !ivec || !p_num || (len && (!in || !out))) return FPNN_AES_ERR_ARG;
+    if (!valid_rounds(ctx->nrounds)) return FPNN_AES_ERR_KEYLEN;
+    if (*p_num > 15) return FPNN_AES_ERR_ARG;
+    if (!len) return FPNN_AES_OK;
+    return modes_call(e, ctx, MODE_OFB, in, len, len, out, len, 0, len, ivec, p_num);
+}
+
 int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in,
                       uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num) {
     if (!e || !ctx || !ivec || !p_num || (len && (!in || !out))) return FPNN_AES_ERR_ARG;
@@ -867,23 +923,8 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     // staging layout: [DevKey 272][iv 16][pos 4 | pad 12][payload len] ... [out len]
     const uint64_t hdr = sizeof(DevKey) + 32;
     const uint64_t pay = (len + 15) & ~15ull;
-    const uint64_t need = hdr + 2 * pay;
-    if (need > e->cap_stage) {
-        uint64_t n = e->cap_stage ? e->cap_stage : 65536;
-        while (n < need) n *= 2;
-        if (e->h_stage) (void)hipHostFree(e->h_stage);
-        if (e->d_stage) (void)hipFree(e->d_stage);
-        e->h_stage = nullptr;
-        e->d_stage = nullptr;
-        e->cap_stage = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_stage), n, 0));
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stage), n));
-        e->cap_stage = n;
-    }
-    DevKey *hk = reinterpret_cast<DevKey *>(e->h_stage);
-    memset(hk, 0, sizeof *hk);
-    for (int k = 0; k < 4 * (nr + 1); k++) hk->rk[k] = bswap32(ctx->rk[k]);
-    hk->nrounds = (uint32_t)nr;
+    if (int rc = stage_reserve(e, hdr + 2 * pay)) return rc;
+    devkey_from_schedule(reinterpret_cast<DevKey *>(e->h_stage), ctx);
     uint8_t *h_iv = e->h_stage + sizeof(DevKey);
     uint32_t *h_pos = reinterpret_cast<uint32_t *>(h_iv + 16);
     memcpy(h_iv, ivec, 16);
@@ -1268,7 +1309,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         uint8_t *ivp = stream ? d_state + 16 * state0 : nullptr;
         uint32_t *posp = stream ? reinterpret_cast<uint32_t *>(d_state + 16 * nseg) + state0 : nullptr;
         e->stream = s.st;  // queue this chunk's kernels on the slot stream
-        rc = encrypt ? run_encrypt(e, &b, ivp, posp, stream) : run_decrypt(e, &b, ivp, posp, stream, total_blocks);
+        rc = encrypt ? run_encrypt(e, &b, ivp, posp, stream) : run_decrypt(e, &b, ivp, posp, stream);
         e->stream = main_stream;
         if (rc) break;
         HIP_TRY(hipEventRecord(s.kdone, s.st));

@@ -157,17 +157,10 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 //   KEYED: one key per packet (key_slot[] with the dense layout, chunk-aligned packets:
 //   the C5 shape).  A step's U chunks never straddle two packets (U divides nb/64), so
 //   the step's key is wave-uniform: slot and round keys are scalar loads per step.
-//   GAPPED (with RAGGED): whole-block segments with gaps between them (wire frames behind
-//   4-byte length prefixes).  Block g of segment s sits at in + in_off[0] + 16 g + d_s:
-//   a lane takes d_s from blk_delta at its segment's start bit in the chunk, or, before
-//   the chunk's first start bit, from chunk_delta[c] (wave-uniform).
-template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED, bool RAGGED = false,
-          bool GAPPED = false>
+template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_dense(KBatch b) {
     static_assert(U % IL == 0, "IL-way interleave of U chunks");
     static_assert(!KEYED || ALIGNED, "per-packet keys need chunk-aligned packets");
-    static_assert(!RAGGED || (!ALIGNED && !KEYED), "ragged batches use the start mask");
-    static_assert(!GAPPED || RAGGED, "the gapped form is a ragged batch");
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -190,15 +183,10 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t lane16 = lane * 16u;
-    // RAGGED: contiguous segments from in_off[0] (out_off[0]); packet starts come from
-    // the per-chunk bit mask built by the scan (bit l of start_mask[c]: block 64c + l
-    // opens a segment)
-    const uint64_t off0 = RAGGED && b.in_off ? b.in_off[0] : 0;
-    const uint8_t *inb = b.in + off0;
-    uint8_t *outb = b.out + (RAGGED && b.out_off ? b.out_off[0] : off0);
-    auto starts = [&](uint64_t c) -> uint64_t { return ((__attribute__((address_space(4))) const uint64_t *)b.start_mask)[c]; };
+    const uint8_t *inb = b.in;
+    uint8_t *outb = b.out;
     // wave-uniform: does the chunk's first block open a packet?
-    auto opens = [&](uint64_t c) -> bool { return RAGGED ? (starts(c) & 1ull) != 0 : chunk_bi0<ALIGNED>(c, nb, b.magic) == 0; };
+    auto opens = [&](uint64_t c) -> bool { return chunk_bi0<ALIGNED>(c, nb, b.magic) == 0; };
 
     // One step = U consecutive chunks.  FULL: all U chunks hold 64 valid blocks (no
     // clamping, unconditional stores).  A StepBuf holds the step's ciphertext and lane
@@ -208,10 +196,6 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
     struct StepBuf {
         uint4 x[U];
         uint4 f;
-        int32_t d[U];  // GAPPED: the lane's segment address delta per chunk
-    };
-    auto cdelta = [&](uint64_t c) -> int64_t {
-        return GAPPED ? (int64_t)((__attribute__((address_space(4))) const int32_t *)b.chunk_delta)[c] : 0;
     };
     auto load = [&](uint64_t st, StepBuf &D, auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
@@ -219,7 +203,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         // more stores than necessary
         const uint64_t c0 = FULL || st * U < nchunks ? st * U : nchunks - 1;
         if (!opens(c0))  // wave-uniform; at a packet start the IV is used
-            D.f = INPLACE ? b.boundary[c0] : load16(inb + (c0 << 10) - 16 + cdelta(c0));  // any byte alignment
+            D.f = INPLACE ? b.boundary[c0] : load16(inb + (c0 << 10) - 16);  // any byte alignment
 #pragma unroll
         for (int j = 0; j < U; j++) {
             const uint64_t c = st * U + j;
@@ -229,16 +213,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 const uint64_t left = total - (cl << 6);
                 if (left < 64) lo = min(lane, (uint32_t)left - 1u) * 16u;
             }
-            int64_t dl = 0;
-            if (GAPPED) {  // the delta of the segment holding the lane's (clamped) block
-                const uint32_t lc = lo >> 4;
-                const uint64_t below = starts(cl) & (lc == 63 ? ~0ull : (2ull << lc) - 1ull);
-                const uint32_t p = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
-                const int32_t bd = b.blk_delta[(cl << 6) + p];
-                D.d[j] = below ? bd : (int32_t)cdelta(cl);
-                dl = D.d[j];
-            }
-            D.x[j] = load16(inb + (cl << 10) + lo + dl);
+            D.x[j] = load16(inb + (cl << 10) + lo);
         }
     };
     auto step = [&](uint64_t st, StepBuf &X, StepBuf &NX, bool pref, auto full_tag) {
@@ -246,10 +221,6 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         if (KEYED) {
             const uint32_t pkt = fast_div((uint32_t)((st * U) << 6), b.magic);
             set_key(((ConstU32 *)b.key_slot)[pkt]);
-            if (b.seg_iv) {  // dense stream decrypt: the stream's carried IV (wave-uniform)
-                ConstU32 *ivp = (ConstU32 *)(b.seg_iv + pkt);
-                iv = make_uint4(ivp[0], ivp[1], ivp[2], ivp[3]);
-            }
         }
         if (!PF || !FULL) load(st, X, full_tag);
         uint4 ks[U];
@@ -257,16 +228,13 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
         for (int j = 0; j < U; j++) {
             const uint64_t c = st * U + j;
             const uint64_t cl = FULL || c < nchunks ? c : nchunks - 1;
-            const uint64_t m = RAGGED ? starts(cl) : 0;
-            const uint32_t bi0 = RAGGED ? (uint32_t)(~m & 1ull) : chunk_bi0<ALIGNED>(cl, nb, b.magic);
+            const uint32_t bi0 = chunk_bi0<ALIGNED>(cl, nb, b.magic);
             // C_{i-1} of lane 0 (wave-uniform): IV at a packet start, else the block
             // before the chunk (lane 63 of chunk j-1; for j = 0 loaded with the step)
             const uint4 fill = bi0 == 0 ? iv : j == 0 ? X.f : readlane63(X.x[j - 1]);
             uint4 kin = make_uint4(wave_shr1(X.x[j].x, fill.x), wave_shr1(X.x[j].y, fill.y),
                                    wave_shr1(X.x[j].z, fill.z), wave_shr1(X.x[j].w, fill.w));
-            if (RAGGED) {  // lanes 1..63 that open a packet take the IV
-                if (lane != 0 && ((m >> lane) & 1ull)) kin = iv;
-            } else if (!ALIGNED) {
+            if (!ALIGNED) {  // lanes 1..63 that open a packet take the IV
                 const uint32_t r = bi0 + lane;
                 const uint32_t q = fast_div(r, b.magic);
                 if (lane != 0 && r == q * nb) kin = iv;
@@ -290,7 +258,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                 if (c >= nchunks) break;  // wave-uniform
                 if (!ALIGNED && (c << 6) + lane >= total) continue;
             }
-            store16(outb + (c << 10) + lane16 + (GAPPED ? (int64_t)X.d[j] : 0), X.x[j] ^ ks[j]);
+            store16(outb + (c << 10) + lane16, X.x[j] ^ ks[j]);
         }
     };
     const uint64_t nfull = (total >> 6) / U;  // steps made of U whole chunks
@@ -403,23 +371,17 @@ __global__ __launch_bounds__(256) void k_boundary_save(KBatch b, uint4 *boundary
 constexpr int dec_u(bool stream, int km) { return (!stream && km == KEY_UNIFORM) ? 4 : 1; }
 
 template <int NR, bool INPLACE, int NT>
-static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int dense, int grid, hipStream_t st) {
-#define FPNN_DEC(L, K, S, NTX) \
-    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, K, S, INPLACE, NTX, dec_u(S, K), 1>), dim3(grid), dim3(kThreads), \
-                       0, st, b)
-#define FPNN_DENSE_R(G) \
-    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, false, 4, 1, true, false, true, G>), dim3(grid), \
+static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, int grid, hipStream_t st) {
+#define FPNN_DEC(L, NTX) \
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, KEY_UNIFORM, false, INPLACE, NTX, 4, 1>), dim3(grid), \
                        dim3(kThreads), 0, st, b)
 #define FPNN_DENSE(AL, U, PF, KEYED) \
     hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
-    set_launched(layout == LAYOUT_GENERAL && b.start_mask ? "cfb_decrypt_dense"
-                 : layout == LAYOUT_FULL && km == KEY_LANE && !aligned ? "cfb_decrypt_lanekey"
+    set_launched(layout == LAYOUT_FULL && km == KEY_LANE && !aligned ? "cfb_decrypt_lanekey"
                  : layout == LAYOUT_FULL && (km == KEY_LANE || dense) ? "cfb_decrypt_dense"
                                                                        : "cfb_decrypt_blocks");
-    if (layout == LAYOUT_GENERAL && b.start_mask) {  // contiguous (or gapped) whole-block segments, one key
-        if (b.blk_delta) FPNN_DENSE_R(true); else FPNN_DENSE_R(false);
-    } else if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
+    if (layout == LAYOUT_FULL && km == KEY_LANE && !aligned) {  // dense, one key per packet, mixed chunks
         hipLaunchKernelGGL((k_cfb_decrypt_lanekey<NR, INPLACE, 4>), dim3(grid), dim3(kThreads), 0, st, b);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet
         const uint32_t nbc = b.nb_uniform / 64;
@@ -431,57 +393,41 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, 
     } else if (layout == LAYOUT_FULL && dense) {
         if (aligned) FPNN_DENSE(true, 4, false, false); else FPNN_DENSE(false, 4, false, false);
     } else if (layout == LAYOUT_FULL) {
-        FPNN_DEC(LAYOUT_FULL, KEY_UNIFORM, false, NT);
-    } else if (layout == LAYOUT_UNIFORM) {
-        if (stream) FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
-    } else if (km == KEY_UNIFORM) {
-        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_DEC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
-    } else {
-        if (stream) FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_DEC(LAYOUT_GENERAL, KEY_LANE, false, 4);
+        FPNN_DEC(LAYOUT_FULL, NT);
+    } else {  // LAYOUT_UNIFORM package batch with a partial last block per packet
+        FPNN_DEC(LAYOUT_UNIFORM, NT);
     }
-#undef FPNN_DENSE_R
 #undef FPNN_DENSE
 #undef FPNN_DEC
 }
 
 template <int NR>
-static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, bool inplace, int grid,
+static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool inplace, int grid,
                    hipStream_t st) {
     const int dense = b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0;
     if (v.tables == 2 && km == KEY_UNIFORM) {
-        if (inplace) dec_launch<NR, true, 2>(b, layout, km, stream, dense, grid, st);
-        else dec_launch<NR, false, 2>(b, layout, km, stream, dense, grid, st);
+        if (inplace) dec_launch<NR, true, 2>(b, layout, km, dense, grid, st);
+        else dec_launch<NR, false, 2>(b, layout, km, dense, grid, st);
     } else {
-        if (inplace) dec_launch<NR, true, 4>(b, layout, km, stream, dense, grid, st);
-        else dec_launch<NR, false, 4>(b, layout, km, stream, dense, grid, st);
+        if (inplace) dec_launch<NR, true, 4>(b, layout, km, dense, grid, st);
+        else dec_launch<NR, false, 4>(b, layout, km, dense, grid, st);
     }
 }
 
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool stream, bool inplace, int grid, hipStream_t st) {
+                                 bool inplace, int grid, hipStream_t st) {
     switch (nrounds) {
-        case 10: dec_nr<10>(b, v, layout, km, stream, inplace, grid, st); break;
-        case 12: dec_nr<12>(b, v, layout, km, stream, inplace, grid, st); break;
-        case 14: dec_nr<14>(b, v, layout, km, stream, inplace, grid, st); break;
+        case 10: dec_nr<10>(b, v, layout, km, inplace, grid, st); break;
+        case 12: dec_nr<12>(b, v, layout, km, inplace, grid, st); break;
+        case 14: dec_nr<14>(b, v, layout, km, inplace, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
-                                hipStream_t st) {
+hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchunks, hipStream_t st) {
     const int grid = grid_for(nchunks, 256, 4096);
-    if (layout != LAYOUT_GENERAL) {
-        if (stream)
-            hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, true>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
-        else
-            hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, false>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
-    } else {
-        if (stream)
-            hipLaunchKernelGGL((k_boundary_save<LAYOUT_GENERAL, true>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
-        else
-            hipLaunchKernelGGL((k_boundary_save<LAYOUT_GENERAL, false>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
-    }
+    hipLaunchKernelGGL((k_boundary_save<LAYOUT_UNIFORM, false>), dim3(grid), dim3(256), 0, st, b, boundary, nchunks);
     return hipGetLastError();
 }
 

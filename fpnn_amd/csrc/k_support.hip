@@ -1,6 +1,6 @@
 // k_support.hip -- small gfx950 kernels around the cipher: the ragged decrypt block
-// map (scan + tile map), the longest-first encrypt ordering, device key expansion
-// and the synthetic payload generator.
+// map (scan), the longest-first encrypt ordering, device key expansion and the
+// synthetic payload generator.
 #include "segments.hpp"
 
 namespace fpnn_aes {
@@ -76,18 +76,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_sums(uint64_t *wg_sums, u
 __global__ __launch_bounds__(kScanThreads) void k_scan_add(uint64_t *bstart, const uint64_t *wg_sums, uint64_t count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) bstart[i] += wg_sums[i / kScanTile];
-}
-
-template <bool STREAM>
-__global__ __launch_bounds__(kScanThreads) void k_tile_map(KBatch b, const uint64_t *bstart, uint64_t *tile_first,
-                                                           uint64_t nchunks) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s == 0) tile_first[nchunks] = b.count ? b.count - 1 : 0;
-    if (s >= b.count) return;
-    const uint64_t nb = nblocks_of<STREAM>(b, s);
-    if (!nb) return;
-    const uint64_t first = bstart[s], last = first + nb - 1;
-    for (uint64_t t = (first + 63) >> 6; (t << 6) <= last; t++) tile_first[t] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -238,116 +226,6 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
     }
 }
 
-__device__ __forceinline__ uint64_t seg_off(const KBatch &b, uint64_t s, const uint64_t *off) {
-    return off ? off[s] : s * b.stride;
-}
-
-// bad[0]: segments that break "contiguous whole blocks"; bad[1]: non-empty segments
-// that also rule out the gapped form (K1d ragged with a per-segment offset delta): a
-// partial last block, out_off not a shifted copy of in_off, or a delta
-// (in_off[s] - in_off[0] - 16 bstart[s]) outside int32.  Empty segments never count
-// for bad[1] (their offsets are not read).
-__global__ __launch_bounds__(256) void k_contig_check(KBatch b, const uint64_t *bstart, uint64_t *bad) {
-    uint32_t n = 0, h = 0;
-    const uint64_t in0 = seg_off(b, 0, b.in_off);
-    const uint64_t out0 = b.out_off ? b.out_off[0] : in0;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t len = b.len ? b.len[s] : b.uniform_len;
-        const uint64_t io = seg_off(b, s, b.in_off);
-        const bool whole = (len & 15u) == 0;
-        const bool shifted = !b.out_off || b.out_off[s] - out0 == io - in0;
-        bool ok = whole && shifted;
-        if (s + 1 < b.count) ok = ok && seg_off(b, s + 1, b.in_off) == io + len;
-        n += ok ? 0u : 1u;
-        if (len) {
-            const int64_t d = (int64_t)(io - in0 - 16 * bstart[s]);
-            h += (!whole || !shifted || d < INT32_MIN || d > INT32_MAX) ? 1u : 0u;
-        }
-    }
-    if (n) atomicAdd(reinterpret_cast<unsigned long long *>(bad), (unsigned long long)n);
-    if (h) atomicAdd(reinterpret_cast<unsigned long long *>(bad + 1), (unsigned long long)h);
-}
-
-// gapped form (delta != null): block g of segment s sits at in + in_off[0] + 16 g + d_s,
-// d_s = in_off[s] - in_off[0] - 16 bstart[s].  blk_delta[bstart[s]] = d_s (read by the
-// lanes at and after a segment start), chunk_delta[c] = d_s of the segment holding
-// block 64c (read by the lanes before the chunk's first start bit).
-__global__ __launch_bounds__(256) void k_start_mask(KBatch b, const uint64_t *bstart, uint64_t *mask,
-                                                    int32_t *blk_delta, int32_t *chunk_delta) {
-    const uint64_t in0 = seg_off(b, 0, b.in_off);
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t g = bstart[s], ge = bstart[s + 1];
-        if (ge <= g) continue;  // empty
-        atomicOr(reinterpret_cast<unsigned long long *>(mask + (g >> 6)), 1ull << (g & 63));
-        if (blk_delta) {
-            const int32_t d = (int32_t)(int64_t)(seg_off(b, s, b.in_off) - in0 - 16 * g);
-            blk_delta[g] = d;
-            for (uint64_t t = (g + 63) >> 6; (t << 6) < ge; t++) chunk_delta[t] = d;
-        }
-    }
-}
-
-// Dense stream decrypt: streams whose CFB position is not 0 (their first block is
-// partial, so K1d's whole-block addressing does not apply) or, with offset arrays,
-// that do not sit at s * uniform_len.
-__global__ __launch_bounds__(256) void k_pos_check(KBatch b, uint64_t *bad) {
-    uint32_t n = 0;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t o = s * b.uniform_len;
-        bool ok = b.pos_snap[s] == 0u;
-        if (b.in_off) ok = ok && b.in_off[s] == o;
-        if (b.out_off) ok = ok && b.out_off[s] == o;
-        n += ok ? 0u : 1u;
-    }
-    if (n) atomicAdd(reinterpret_cast<unsigned long long *>(bad), (unsigned long long)n);
-}
-
-// Dense stream decrypt, every position 0 and whole blocks: the state each stream leaves
-// is (its last ciphertext block, 0) -- base/rijndael.c:1171-1201 ends a whole block with
-// ivec = that block and pos = 0.  Runs before the decrypt (which may overwrite the
-// ciphertext in place); the decrypt reads the incoming IVs from the snapshot.
-__global__ __launch_bounds__(256) void k_stream_dense_state(KBatch b) {
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 last = *reinterpret_cast<const uint4 *>(b.in + s * b.stride + b.uniform_len - 16);
-        *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = last;
-        b.pos_state[s] = 0u;
-    }
-}
-
-hipError_t launch_pos_check(const KBatch &b, uint64_t *bad, hipStream_t st) {
-    hipError_t err = hipMemsetAsync(bad, 0, sizeof(uint64_t), st);
-    if (err != hipSuccess) return err;
-    if (b.count) hipLaunchKernelGGL(k_pos_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bad);
-    return hipGetLastError();
-}
-
-hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st) {
-    if (b.count) hipLaunchKernelGGL(k_stream_dense_state, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b);
-    return hipGetLastError();
-}
-
-hipError_t launch_contig_check(const KBatch &b, const uint64_t *bstart, uint64_t *bad, hipStream_t st) {
-    hipError_t err = hipMemsetAsync(bad, 0, 2 * sizeof(uint64_t), st);
-    if (err != hipSuccess) return err;
-    if (b.count)
-        hipLaunchKernelGGL(k_contig_check, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, bad);
-    return hipGetLastError();
-}
-
-hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, int32_t *blk_delta,
-                             int32_t *chunk_delta, uint64_t nchunks, hipStream_t st) {
-    hipError_t err = hipMemsetAsync(mask, 0, nchunks * sizeof(uint64_t), st);
-    if (err != hipSuccess) return err;
-    if (b.count)
-        hipLaunchKernelGGL(k_start_mask, dim3(grid_for(b.count, 256, 4096)), dim3(256), 0, st, b, bstart, mask, blk_delta,
-                           chunk_delta);
-    return hipGetLastError();
-}
-
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,
                                  hipStream_t st) {
     const uint64_t nwg = (b.count + kScanTile - 1) / kScanTile;
@@ -361,16 +239,6 @@ hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart,
     if (b.count)
         hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((b.count + kScanThreads - 1) / kScanThreads)),
                            dim3(kScanThreads), 0, st, bstart, wg_sums, b.count);
-    return hipGetLastError();
-}
-
-hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first, uint64_t nchunks,
-                           hipStream_t st) {
-    const unsigned grid = (unsigned)((b.count + kScanThreads) / kScanThreads);
-    if (stream)
-        hipLaunchKernelGGL((k_tile_map<true>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
-    else
-        hipLaunchKernelGGL((k_tile_map<false>), dim3(grid), dim3(kScanThreads), 0, st, b, bstart, tile_first, nchunks);
     return hipGetLastError();
 }
 

@@ -33,7 +33,6 @@ struct KBatch {
     uint32_t pad0;
     uint64_t magic;          // ceil(2^64 / nb_uniform)
     const uint64_t *bstart;  // general: first virtual block of each segment (count + 1)
-    const uint64_t *tile_first;  // general: segment holding block 64*c (nchunks + 1)
     const uint4 *boundary;   // in-place: Cx block preceding each 64-block chunk
     // stream decrypt: the (iv, pos) state as it was when the call was queued.  The
     // kernel writes the new state into iv_state/pos_state while other waves may still
@@ -42,17 +41,6 @@ struct KBatch {
     const uint32_t *pos_snap;
     // encrypt of ragged batches: segment visiting order (longest first), or null
     const uint32_t *perm;
-    // decrypt of contiguous ragged batches (K1d ragged): bit l of start_mask[c] set when
-    // block 64c + l opens a segment; null otherwise
-    const uint64_t *start_mask;
-    // K1d keyed: per-packet IV (dense stream decrypt with every position 0: the
-    // snapshot of iv_state); null = the key slot's IV (package mode)
-    const uint4 *seg_iv;
-    // K1d ragged, gapped form: block g of segment s sits at in + in_off[0] + 16 g + d_s;
-    // blk_delta[bstart[s]] = d_s, chunk_delta[c] = d_s of the segment holding block 64c
-    // (null: contiguous, d_s = 0)
-    const int32_t *blk_delta;
-    const int32_t *chunk_delta;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
@@ -60,7 +48,7 @@ struct KBatch {
 // byte-granular head/tail paths); with KEY_LANE, FULL also means dense (stride ==
 // uniform_len) with key_slot[] holding one slot per packet (K1d keyed when
 // uniform_len % 1024 == 0, else K1k).
-// GENERAL: offset/length/slot arrays.
+// GENERAL: offset/length/slot arrays (decrypt: K1r, k_ragged.hip).
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
@@ -122,31 +110,39 @@ hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool s
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
 // (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
+// K1 / K1d / K1k for uniform and dense layouts (every segment's block count known on the host).
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool stream, bool inplace, int grid, hipStream_t st);
-hipError_t launch_boundary_save(const KBatch &b, Layout layout, bool stream, uint4 *boundary, uint64_t nchunks,
-                                hipStream_t st);
-// General-layout block map: bstart[] and *total (device); wg_sums scratch of
-// ceil(count/1024) entries.
+                                 bool inplace, int grid, hipStream_t st);
+// K1r (k_ragged.hip): ragged decrypt with no host round trip.  b.bstart[0..count] from
+// launch_block_map_scan (bstart[count] = total blocks, device only); plan: one entry per
+// wave of the grid (grid * kThreads / 64), filled by the plan kernel queued first.
+struct RaggedPlan {
+    uint64_t s0;  // segment holding the wave's first block
+    uint64_t pad;
+    uint4 fill;   // ciphertext block before it (same segment), saved before any write
+};
+hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, int grid,
+                                 hipStream_t st);
+// In-place K1 / K1d: save the ciphertext block before every 64-block chunk.
+hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchunks, hipStream_t st);
+// General-layout block map: bstart[0..count] (bstart[count] = *total = total blocks, both
+// device); wg_sums scratch of ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
-// Package-mode decrypt of a general layout (after the block-map scan): bad[0] = the
-// segments that break "contiguous whole blocks" (len % 16 != 0, a gap or overlap to the
-// next segment, out_off not a shifted copy of in_off); bad[1] = the non-empty ones that
-// also rule out the gapped form (partial block, unshifted out_off, delta beyond int32).
-// Both zeroed here.
-hipError_t launch_contig_check(const KBatch &b, const uint64_t *bstart, uint64_t *bad, hipStream_t st);
-// Stream decrypt of a dense whole-block batch: *bad (zeroed here) = streams whose
-// pos_snap is not 0; then, when it is 0, the new (iv, pos) state of every stream.
-hipError_t launch_pos_check(const KBatch &b, uint64_t *bad, hipStream_t st);
-hipError_t launch_stream_dense_state(const KBatch &b, hipStream_t st);
-// start_mask[nchunks] (zeroed here): one bit per block that opens a non-empty segment.
-// Gapped form (blk_delta not null): d_s = in_off[s] - in_off[0] - 16 bstart[s] at
-// blk_delta[bstart[s]] (total_blocks entries) and chunk_delta[c] (nchunks entries).
-hipError_t launch_start_mask(const KBatch &b, const uint64_t *bstart, uint64_t *mask, int32_t *blk_delta,
-                             int32_t *chunk_delta, uint64_t nchunks, hipStream_t st);
-hipError_t launch_tile_map(const KBatch &b, bool stream, const uint64_t *bstart, uint64_t *tile_first,
-                           uint64_t nchunks, hipStream_t st);
+// The rest of rijndael.h (k_modes.hip): ECB / CBC / OFB over one host call's buffers.
+enum : int { MODE_ECB_ENC = 0, MODE_ECB_DEC = 1, MODE_CBC_ENC = 2, MODE_CBC_DEC = 3, MODE_OFB = 4 };
+struct ModeArgs {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t nblocks;      // whole 16-byte blocks to process (ECB, CBC)
+    uint64_t len;          // OFB: bytes
+    const DevKey *key;     // encryption schedule, or the decryption schedule (ECB/CBC decrypt)
+    uint8_t *iv;           // 16 B, in/out (CBC encrypt, OFB); CBC decrypt reads it
+    uint32_t *pos;         // OFB position, in/out
+    const uint32_t *t0le, *td0le;
+    const uint8_t *isbox;
+};
+hipError_t launch_block_modes(const ModeArgs &a, int nrounds, int mode, int num_cus, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
 hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, int grid,

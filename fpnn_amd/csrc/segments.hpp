@@ -77,27 +77,17 @@ __device__ __forceinline__ uint64_t seg_blocks(uint32_t len, uint32_t n0) {
     return len ? ((uint64_t)n0 + len + 15) >> 4 : 0;
 }
 
+// segment and block-in-segment of virtual block gblk of a uniform layout (clamped into
+// the batch for lanes past its end)
 template <int LAYOUT>
 __device__ __forceinline__ void locate_block(const KBatch &b, uint64_t c, uint64_t gblk, uint64_t total, uint64_t &s,
                                              uint32_t &bi) {
-    if (LAYOUT != LAYOUT_GENERAL) {
-        const uint32_t g32 = (uint32_t)(gblk < total ? gblk : total - 1);
-        const uint32_t q = fast_div(g32, b.magic);
-        s = q;
-        bi = g32 - q * b.nb_uniform;
-    } else {
-        const uint64_t gg = gblk < total ? gblk : total - 1;
-        uint64_t lo = b.tile_first[c], hi = b.tile_first[c + 1];
-        while (lo < hi) {  // largest s in [lo, hi] with bstart[s] <= gg
-            const uint64_t mid = (lo + hi + 1) >> 1;
-            if (b.bstart[mid] <= gg)
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-        s = lo;
-        bi = (uint32_t)(gg - b.bstart[lo]);
-    }
+    static_assert(LAYOUT != LAYOUT_GENERAL, "general layouts are located by K1r's window");
+    (void)c;
+    const uint32_t g32 = (uint32_t)(gblk < total ? gblk : total - 1);
+    const uint32_t q = fast_div(g32, b.magic);
+    s = q;
+    bi = g32 - q * b.nb_uniform;
 }
 
 __device__ __forceinline__ uint4 readlane63(const uint4 &v) {

@@ -61,6 +61,16 @@ def setup_encrypt(key: bytes) -> Schedule:
     return ctx
 
 
+def setup_decrypt(key: bytes) -> Schedule:
+    """rijndael_setup_decrypt: host decryption schedule, reference rk[] layout."""
+    ctx = Schedule()
+    rc = lib.fpnn_aes_setup_decrypt(C.byref(ctx), _buf(key), len(key))
+    if rc == ERR_KEYLEN:
+        raise FpnnAesError(rc, f"key length {len(key)} (must be 16, 24 or 32)")
+    check(rc, "setup_decrypt")
+    return ctx
+
+
 def device_count() -> int:
     n = C.c_int(0)
     rc = lib.fpnn_aes_device_count(C.byref(n))
@@ -140,6 +150,36 @@ class Engine:
         out = C.create_string_buffer(max(1, len(data)))
         check(lib.fpnn_aes_cfb_host(self._h, C.byref(ctx), int(encrypt), C.c_char_p(data), out, len(data), iv,
                                     C.byref(n)), "cfb_host")
+        return out.raw[: len(data)], bytes(iv), n.value
+
+    # -- the rest of rijndael.h (synchronous, host bytes) ----------------------------------------
+    def ecb(self, ctx: Schedule, encrypt: bool, data: bytes) -> bytes:
+        """rijndael_encrypt / rijndael_decrypt over len(data)/16 blocks."""
+        if len(data) % 16:
+            raise ValueError("ECB takes whole 16-byte blocks")
+        out = C.create_string_buffer(max(1, len(data)))
+        check(lib.fpnn_aes_ecb_host(self._h, C.byref(ctx), int(encrypt), C.c_char_p(data), out, len(data) // 16),
+              "ecb_host")
+        return out.raw[: len(data)]
+
+    def cbc(self, ctx: Schedule, encrypt: bool, data: bytes, ivec: bytes, length: Optional[int] = None):
+        """rijndael_cbc_encrypt / _decrypt; returns (out, new_ivec).  length defaults to
+        len(data); decrypt reads 16*ceil(length/16) bytes of data."""
+        n = len(data) if length is None else length
+        whole = (n + 15) // 16 * 16
+        src = bytes(data) + bytes(max(0, whole - len(data)))
+        iv = (C.c_uint8 * 16)(*ivec)
+        out = C.create_string_buffer(max(1, whole))
+        check(lib.fpnn_aes_cbc_host(self._h, C.byref(ctx), int(encrypt), C.c_char_p(src), out, n, iv), "cbc_host")
+        return out.raw[: whole if encrypt else n], bytes(iv)
+
+    def ofb(self, ctx: Schedule, data: bytes, ivec: bytes, num: int = 0):
+        """rijndael_ofb_encrypt; returns (out, new_ivec, new_num)."""
+        iv = (C.c_uint8 * 16)(*ivec)
+        n = C.c_size_t(num)
+        out = C.create_string_buffer(max(1, len(data)))
+        check(lib.fpnn_aes_ofb_host(self._h, C.byref(ctx), C.c_char_p(data), out, len(data), iv, C.byref(n)),
+              "ofb_host")
         return out.raw[: len(data)], bytes(iv), n.value
 
     # -- many frames in host memory (the cross-connection batch path) ----------------------

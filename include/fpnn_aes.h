@@ -51,6 +51,11 @@ typedef struct {
  * FPNN_AES_ERR_KEYLEN (and sets nrounds = 0, like the reference). */
 int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen);
 
+/* Decryption key schedule.  Mirrors rijndael_setup_decrypt (base/rijndael.c:805-850):
+ * the encryption schedule with the round keys reversed and InvMixColumns applied to all
+ * but the first and last -- the same rk[] words as the reference. */
+int fpnn_aes_setup_decrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen);
+
 /* ---- engine: one GPU, one HIP stream ---------------------------------------- */
 typedef struct fpnn_aes_engine fpnn_aes_engine;
 #define FPNN_AES_OWN_STREAM ((void *)(intptr_t)-1)
@@ -138,6 +143,23 @@ int fpnn_aes_stream_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t
  * runs the GPU kernels, copies back and updates ivec/p_num.  Synchronous. */
 int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt,
                       const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num);
+
+/* ---- the rest of rijndael.h, single calls from host memory (synchronous) ------------------ */
+/* ECB: nblocks independent 16-byte blocks through the forward cipher (encrypt != 0,
+ * ctx from fpnn_aes_setup_encrypt; rijndael_encrypt, base/rijndael.c:852-959) or the
+ * inverse cipher (ctx from fpnn_aes_setup_decrypt; rijndael_decrypt, :961-1068).
+ * in == out allowed. */
+int fpnn_aes_ecb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in, uint8_t *out,
+                      size_t nblocks);
+/* CBC exactly as rijndael_cbc_encrypt / _decrypt (base/rijndael.c:1070-1153): encrypt
+ * zero-pads a partial last block and writes 16*ceil(len/16) bytes; decrypt reads
+ * 16*ceil(len/16) bytes and writes len; ivec is updated to the last ciphertext block.
+ * Decrypt takes the setup_decrypt schedule.  in == out allowed. */
+int fpnn_aes_cbc_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in, uint8_t *out,
+                      size_t len, uint8_t ivec[16]);
+/* OFB exactly as rijndael_ofb_encrypt (base/rijndael.c:1155-1169), (ivec, *p_num) carried. */
+int fpnn_aes_ofb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, const uint8_t *in, uint8_t *out, size_t len,
+                      uint8_t ivec[16], size_t *p_num);
 
 /* ---- many frames from host memory (the cross-connection batch path, §8f row 1) ------- */
 /* One entry per frame.  src/dst are host pointers (dst may equal src for in-place;

@@ -12,6 +12,10 @@
  *     tables are *generated* here from GF(2^8) arithmetic, not copied.
  *   - FIPS-197 key expansion with big-endian words (base/rijndael.c:696-799).
  *   - CFB-128 byte loop with the (ivec, *p_num) carry (base/rijndael.c:1171-1201).
+ *   - The rest of the rijndael.h surface: the decryption key schedule (reversed round
+ *     keys with InvMixColumns, base/rijndael.c:805-850), the inverse cipher (Td0..Td4,
+ *     :348-686, 961-1068), CBC with its zero-padded / partial last block (:1070-1153)
+ *     and OFB with the (ivec, *p_num) carry (:1155-1169).
  *   - PackageEncryptor / StreamEncryptor call semantics (core/Encryptor.cpp:10-70).
  *
  * Parity pinned by (tests/test_oracle.py):
@@ -31,7 +35,9 @@
 /* Table generation (equivalent of the static tables at base/rijndael.c:8-346) */
 
 static uint8_t g_sbox[256];
+static uint8_t g_isbox[256];
 static uint32_t g_te[4][256];
+static uint32_t g_td[4][256];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
 static uint8_t gf_mul2(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0x00)); }
@@ -61,6 +67,16 @@ static void build_tables(void)
         uint32_t t0 = ((uint32_t)s2 << 24) | ((uint32_t)s << 16) | ((uint32_t)s << 8) | s3;
         for (int k = 0; k < 4; k++)
             g_te[k][x] = ror32(t0, 8 * k);
+        g_isbox[s] = (uint8_t)x;
+    }
+    /* inverse tables: InvSubBytes o InvMixColumns, column (14i, 9i, 13i, 11i) */
+    for (int x = 0; x < 256; x++) {
+        uint8_t i1 = g_isbox[x], i2 = gf_mul2(i1), i4 = gf_mul2(i2), i8 = gf_mul2(i4);
+        uint8_t i9 = (uint8_t)(i8 ^ i1), i11 = (uint8_t)(i8 ^ i2 ^ i1), i13 = (uint8_t)(i8 ^ i4 ^ i1),
+                i14 = (uint8_t)(i8 ^ i4 ^ i2);
+        uint32_t t0 = ((uint32_t)i14 << 24) | ((uint32_t)i9 << 16) | ((uint32_t)i13 << 8) | i11;
+        for (int k = 0; k < 4; k++)
+            g_td[k][x] = ror32(t0, 8 * k);
     }
 }
 
@@ -143,6 +159,104 @@ void ao_encrypt_block(const ao_ctx *ctx, const uint8_t in[16], uint8_t out[16])
                      (uint32_t)g_sbox[s[(i + 3) & 3] & 0xff];
         store_be32(out + 4 * i, v ^ rk[4 * nr + i]);
     }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Decryption key schedule: base/rijndael.c:805-850 -- the encryption schedule with
+   the round-key order reversed and InvMixColumns applied to every round key but the
+   first and the last (InvMixColumns(w) = Td0[S[b0]] ^ Td1[S[b1]] ^ Td2[S[b2]] ^ Td3[S[b3]]) */
+
+int ao_setup_decrypt(ao_ctx *ctx, const uint8_t *key, size_t keylen)
+{
+    if (!ao_setup_encrypt(ctx, key, keylen))
+        return 0;
+    const int nr = ctx->nrounds;
+    uint32_t *rk = ctx->rk;
+    for (int i = 0, j = 4 * nr; i < j; i += 4, j -= 4)
+        for (int k = 0; k < 4; k++) {
+            uint32_t t = rk[i + k];
+            rk[i + k] = rk[j + k];
+            rk[j + k] = t;
+        }
+    for (int r = 1; r < nr; r++)
+        for (int k = 0; k < 4; k++) {
+            uint32_t w = rk[4 * r + k];
+            rk[4 * r + k] = g_td[0][g_sbox[w >> 24]] ^ g_td[1][g_sbox[(w >> 16) & 0xff]] ^
+                            g_td[2][g_sbox[(w >> 8) & 0xff]] ^ g_td[3][g_sbox[w & 0xff]];
+        }
+    return nr;
+}
+
+/* Inverse cipher: base/rijndael.c:961-1068 (equivalent inverse cipher, FIPS-197 5.3.5):
+   column c takes rows 0..3 from state columns c, c-1, c-2, c-3. */
+void ao_decrypt_block(const ao_ctx *ctx, const uint8_t in[16], uint8_t out[16])
+{
+    const uint32_t *rk = ctx->rk;
+    const int nr = ctx->nrounds;
+    uint32_t s[4], t[4];
+    for (int i = 0; i < 4; i++)
+        s[i] = load_be32(in + 4 * i) ^ rk[i];
+    for (int r = 1; r < nr; r++) {
+        for (int i = 0; i < 4; i++)
+            t[i] = g_td[0][s[i] >> 24] ^ g_td[1][(s[(i + 3) & 3] >> 16) & 0xff] ^
+                   g_td[2][(s[(i + 2) & 3] >> 8) & 0xff] ^ g_td[3][s[(i + 1) & 3] & 0xff] ^ rk[4 * r + i];
+        memcpy(s, t, sizeof s);
+    }
+    for (int i = 0; i < 4; i++) {
+        uint32_t v = ((uint32_t)g_isbox[s[i] >> 24] << 24) |
+                     ((uint32_t)g_isbox[(s[(i + 3) & 3] >> 16) & 0xff] << 16) |
+                     ((uint32_t)g_isbox[(s[(i + 2) & 3] >> 8) & 0xff] << 8) |
+                     (uint32_t)g_isbox[s[(i + 1) & 3] & 0xff];
+        store_be32(out + 4 * i, v ^ rk[4 * nr + i]);
+    }
+}
+
+/* CBC: base/rijndael.c:1070-1153.  Encrypt: a partial last block is the plaintext
+   zero-padded to 16 bytes (out[i] = iv[i] for i >= len, i.e. 0 ^ iv), so 16 bytes are
+   written; ivec := the last ciphertext block.  Decrypt: the last (partial) block is
+   deciphered from 16 input bytes but only `len` bytes are written; ivec := the last
+   16 input bytes. */
+void ao_cbc_encrypt(const ao_ctx *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16])
+{
+    uint8_t iv[16], blk[16];
+    memcpy(iv, ivec, 16);
+    for (size_t off = 0; off < len; off += 16) {
+        size_t n = len - off < 16 ? len - off : 16;
+        for (size_t i = 0; i < 16; i++)
+            blk[i] = (uint8_t)((i < n ? in[off + i] : 0) ^ iv[i]);
+        ao_encrypt_block(ctx, blk, out + off);
+        memcpy(iv, out + off, 16);
+    }
+    memcpy(ivec, iv, 16);
+}
+
+void ao_cbc_decrypt(const ao_ctx *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16])
+{
+    uint8_t iv[16], c[16], p[16];
+    memcpy(iv, ivec, 16);
+    for (size_t off = 0; off < len; off += 16) {
+        size_t n = len - off < 16 ? len - off : 16;
+        memcpy(c, in + off, 16); /* whole block: the cipher buffer is a multiple of 16 */
+        ao_decrypt_block(ctx, c, p);
+        for (size_t i = 0; i < n; i++)
+            out[off + i] = (uint8_t)(p[i] ^ iv[i]);
+        memcpy(iv, c, 16);
+    }
+    memcpy(ivec, iv, 16);
+}
+
+/* OFB: base/rijndael.c:1155-1169 -- keystream ivec := E(ivec) at n == 0, never fed back
+   from the data. */
+void ao_ofb(const ao_ctx *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16], size_t *num)
+{
+    size_t n = *num;
+    for (size_t k = 0; k < len; k++) {
+        if (n == 0)
+            ao_encrypt_block(ctx, ivec, ivec);
+        out[k] = (uint8_t)(in[k] ^ ivec[n]);
+        n = (n + 1) & 15;
+    }
+    *num = n;
 }
 
 /* ------------------------------------------------------------------------- */

@@ -9,6 +9,7 @@ container only).  Writes data only -- inputs and the reference's outputs:
   cfb_cases.json    random rijndael_cfb_encrypt calls (16/24/32-byte keys, pos carry)
   package_cases.json PackageEncryptor encrypt / decrypt / encrypt(std::string*) frames
   stream_cases.json StreamEncryptor call sequences (state carried across frames)
+  modes_cases.json  the rest of rijndael.h: setup_decrypt, ECB decrypt, CBC, OFB
   digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5) and
                     per-rank shard digests of the bench workloads (C2 r0-7, C4/C5 at world 1/2/4/8)
 
@@ -98,6 +99,43 @@ def gen_package_cases(ref: Oracle):
     cases.append({"key": hx(key), "iv": hx(key), "in": hx(data), "encrypt": hx(ref.package(key, key, True, data)),
                   "decrypt": hx(ref.package(key, key, False, data)), "frame": hx(ref.package_frame(key, key, data))})
     return cases
+
+
+def gen_modes_cases(ref: Oracle, n=150):
+    """The rest of rijndael.h: setup_decrypt schedules, single-block decrypt (FIPS-197
+    C.1/C.3 inverse + random), CBC encrypt/decrypt (partial last blocks) and OFB (random
+    pos carry) -- base/rijndael.c:805-850, 961-1169, run by oracle/_ref."""
+    rng = np.random.default_rng(20261016)
+    out = {"setup_decrypt": [], "ecb_decrypt": [], "cbc": [], "ofb": []}
+    for i in range(24):
+        kl = (16, 24, 32)[i % 3]
+        key = rng.bytes(kl)
+        ctx = ref.setup_decrypt(key)
+        out["setup_decrypt"].append({"key": hx(key), "nrounds": ctx.nrounds,
+                                     "rk": [int(x) for x in ctx.rk[:4 * (ctx.nrounds + 1)]]})
+    fips = [(bytes(range(16)), "69c4e0d86a7b0430d8cdb78070b4c55a"), (bytes(range(32)), "8ea2b7ca516745bfeafc49904b496089")]
+    for key, ct in fips:
+        out["ecb_decrypt"].append({"key": hx(key), "in": ct, "out": hx(ref.decrypt_block(key, bytes.fromhex(ct)))})
+    for i in range(30):
+        key = rng.bytes((16, 24, 32)[i % 3])
+        blk = rng.bytes(16)
+        out["ecb_decrypt"].append({"key": hx(key), "in": hx(blk), "out": hx(ref.decrypt_block(key, blk))})
+    lens = [0, 1, 15, 16, 17, 31, 32, 33, 48, 100, 255, 256, 1000]
+    for i in range(n):
+        key = rng.bytes((16, 24, 32)[i % 3])
+        iv = rng.bytes(16)
+        L = lens[i % len(lens)]
+        data = rng.bytes((L + 15) // 16 * 16)
+        enc = bool(i & 1)
+        res, iv2 = ref.cbc(key, enc, data[:L] if enc else data, iv, L)
+        # decrypt: the reference reads whole 16-byte blocks of ciphertext, writes len bytes
+        out["cbc"].append({"key": hx(key), "iv": hx(iv), "encrypt": enc, "len": L,
+                           "in": hx(data[:L] if enc else data), "out": hx(res), "iv_out": hx(iv2)})
+        pos = int(rng.integers(0, 16)) if i % 3 else 0
+        o, iv3, pos3 = ref.ofb(key, data[:L], iv, pos)
+        out["ofb"].append({"key": hx(key), "iv": hx(iv), "pos": pos, "in": hx(data[:L]), "out": hx(o),
+                           "iv_out": hx(iv3), "pos_out": pos3})
+    return out
 
 
 def gen_stream_cases(ref: Oracle):
@@ -239,6 +277,7 @@ def main():
     ap.add_argument("--skip-large", action="store_true")
     ap.add_argument("--shards-only", action="store_true",
                     help="only (re)compute the per-rank shard digests into digests.json")
+    ap.add_argument("--modes-only", action="store_true", help="only (re)write modes_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -249,6 +288,9 @@ def main():
             json.dump(obj, f, indent=1)
         print("wrote", name)
 
+    if args.modes_only:
+        dump("modes_cases.json", gen_modes_cases(ref))
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -259,6 +301,7 @@ def main():
     dump("cfb_cases.json", gen_cfb_cases(ref))
     dump("package_cases.json", gen_package_cases(ref))
     dump("stream_cases.json", gen_stream_cases(ref))
+    dump("modes_cases.json", gen_modes_cases(ref))
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

@@ -121,6 +121,56 @@ class Oracle:
         self._block(C.byref(ctx), _bytes_ptr(block), out)
         return bytes(out)
 
+    # -- the rest of rijndael.h (base/rijndael.c:805-850, 961-1068, 1070-1169) ---------
+    def _fn(self, port_name, ref_name):
+        return getattr(self.lib, port_name if self.kind == "port" else ref_name)
+
+    def setup_decrypt(self, key: bytes) -> Ctx:
+        ctx = Ctx()
+        f = self._fn("ao_setup_decrypt", "ref_setup_decrypt")
+        f.argtypes = [C.POINTER(Ctx), _u8p, C.c_size_t]
+        f(C.byref(ctx), _bytes_ptr(key), len(key))
+        return ctx
+
+    def decrypt_block(self, key: bytes, block: bytes) -> bytes:
+        ctx = self.setup_decrypt(key)
+        f = self._fn("ao_decrypt_block", "ref_decrypt_block")
+        f.argtypes = [C.POINTER(Ctx), _u8p, _u8p]
+        out = (C.c_uint8 * 16)()
+        f(C.byref(ctx), _bytes_ptr(block), out)
+        return bytes(out)
+
+    def cbc(self, key: bytes, encrypt: bool, data: bytes, ivec: bytes, length=None):
+        """rijndael_cbc_encrypt / _decrypt of `length` bytes (default len(data)); returns
+        (out, new_ivec).  Encrypt output is 16*ceil(len/16) bytes; decrypt reads that many
+        input bytes (data is zero-extended here) and writes len."""
+        ctx = self.setup_encrypt(key) if encrypt else self.setup_decrypt(key)
+        n = len(data) if length is None else length
+        padded = (n + 15) // 16 * 16
+        src = bytes(data[:padded]) + bytes(max(0, padded - len(data)))
+        out = (C.c_uint8 * max(1, padded))()
+        iv = (C.c_uint8 * 16)(*ivec)
+        if self.kind == "port":
+            f = self.lib.ao_cbc_encrypt if encrypt else self.lib.ao_cbc_decrypt
+            f.argtypes = [C.POINTER(Ctx), _u8p, _u8p, C.c_size_t, _u8p]
+            f(C.byref(ctx), _bytes_ptr(src), out, n, iv)
+        else:
+            f = self.lib.ref_cbc
+            f.argtypes = [C.POINTER(Ctx), C.c_int, _u8p, _u8p, C.c_size_t, _u8p]
+            f(C.byref(ctx), int(encrypt), _bytes_ptr(src), out, n, iv)
+        return bytes(out)[: padded if encrypt else n], bytes(iv)
+
+    def ofb(self, key: bytes, data: bytes, ivec: bytes, num: int = 0):
+        """rijndael_ofb_encrypt; returns (out, new_ivec, new_num)."""
+        ctx = self.setup_encrypt(key)
+        f = self._fn("ao_ofb", "ref_ofb")
+        f.argtypes = [C.POINTER(Ctx), _u8p, _u8p, C.c_size_t, _u8p, C.POINTER(C.c_size_t)]
+        iv = (C.c_uint8 * 16)(*ivec)
+        n = C.c_size_t(num)
+        out = (C.c_uint8 * max(1, len(data)))()
+        f(C.byref(ctx), _bytes_ptr(data), out, len(data), iv, C.byref(n))
+        return bytes(out)[: len(data)], bytes(iv), n.value
+
     def cfb(self, key: bytes, encrypt: bool, data: bytes, ivec: bytes, num: int = 0):
         """One rijndael_cfb_encrypt call; returns (out, new_ivec, new_num)."""
         ctx = self.setup_encrypt(key)

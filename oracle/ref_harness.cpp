@@ -35,6 +35,29 @@ void ref_encrypt_block(const rijndael_context *ctx, const uint8_t *in, uint8_t *
     rijndael_encrypt(ctx, in, out);
 }
 
+int ref_setup_decrypt(rijndael_context *ctx, const uint8_t *key, size_t keylen)
+{
+    return rijndael_setup_decrypt(ctx, key, keylen) ? 1 : 0;
+}
+
+void ref_decrypt_block(const rijndael_context *ctx, const uint8_t *in, uint8_t *out)
+{
+    rijndael_decrypt(ctx, in, out);
+}
+
+void ref_cbc(const rijndael_context *ctx, int encrypt, const uint8_t *in, uint8_t *out, size_t len, uint8_t *ivec)
+{
+    if (encrypt)
+        rijndael_cbc_encrypt(ctx, in, out, len, ivec);
+    else
+        rijndael_cbc_decrypt(ctx, in, out, len, ivec);
+}
+
+void ref_ofb(const rijndael_context *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t *ivec, size_t *num)
+{
+    rijndael_ofb_encrypt(ctx, in, out, len, ivec, num);
+}
+
 void ref_cfb(const rijndael_context *ctx, int encrypt, const uint8_t *in, uint8_t *out, size_t len,
              uint8_t *ivec, size_t *num)
 {

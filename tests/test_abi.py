@@ -151,3 +151,51 @@ def test_cpp_dropin_compiles_against_headers(tmp_path):
     """include/Encryptor.h is source-compatible with the way FPNN uses core/Encryptor.h
     (-std=c++11 -Wall -Werror, as the reference's def.mk builds it)."""
     assert os.access(build_dropin(tmp_path), os.X_OK)
+
+
+def test_setup_decrypt_matches_reference(oracle, golden):
+    """rijndael_setup_decrypt (host): the reversed, InvMixColumns'd rk[] of the reference
+    (golden modes_cases.json, generated by oracle/_ref) and of the oracle restatement."""
+    import fpnn_amd
+    for c in golden("modes_cases.json")["setup_decrypt"]:
+        key = bytes.fromhex(c["key"])
+        ours = fpnn_amd.setup_decrypt(key)
+        assert ours.nrounds == c["nrounds"] and list(ours.rk[:len(c["rk"])]) == c["rk"]
+        mirror = fpnn_amd.Schedule()
+        assert fpnn_amd.lib.rijndael_setup_decrypt(C.byref(mirror), C.cast(C.c_char_p(key), C.POINTER(C.c_uint8)),
+                                                   len(key))
+        assert list(mirror.rk[:len(c["rk"])]) == c["rk"]
+        theirs = oracle.setup_decrypt(key)
+        assert list(theirs.rk[:len(c["rk"])]) == c["rk"]
+
+
+RIJNDAEL_API = ("rijndael_setup_encrypt", "rijndael_setup_decrypt", "rijndael_encrypt", "rijndael_decrypt",
+                "rijndael_cbc_encrypt", "rijndael_cbc_decrypt", "rijndael_cfb_encrypt", "rijndael_ofb_encrypt")
+
+
+def build_rijndael_link(outdir) -> str:
+    import fpnn_amd
+    exe = os.path.join(str(outdir), "rijndael_link")
+    libdir = os.path.dirname(fpnn_amd.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "rijndael_link.cpp"), "-o", exe, "-L", libdir, "-lfpnn_aes",
+                    f"-Wl,-rpath,{libdir}"], check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_rijndael_surface_links_without_reference_object(tmp_path):
+    """Every function base/rijndael.h:22-60 declares is exported by libfpnn_aes.so, and a
+    program calling all of them links with no rijndael.o: each rijndael_* symbol is left
+    undefined in the executable and resolved from the shared library."""
+    import fpnn_amd
+    assert set(RIJNDAEL_API) <= declared_functions()
+    exe = build_rijndael_link(tmp_path)
+    undef = subprocess.run(["nm", "-u", exe], capture_output=True, text=True, check=True).stdout.split()
+    defined_in_exe = subprocess.run(["nm", "--defined-only", exe], capture_output=True, text=True,
+                                    check=True).stdout.split()
+    lib_syms = subprocess.run(["nm", "-D", "--defined-only", fpnn_amd.LIB_PATH], capture_output=True, text=True,
+                              check=True).stdout.split()
+    for name in RIJNDAEL_API:
+        assert name in undef, f"{name} not imported"
+        assert name not in defined_in_exe, f"{name} defined in the program itself"
+        assert name in lib_syms, f"{name} not exported by libfpnn_aes.so"

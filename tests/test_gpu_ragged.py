@@ -1,0 +1,177 @@
+"""K1r, the ragged decrypt (fpnn_amd/csrc/k_ragged.hip), against the oracle on the
+shapes that stress its per-wave segment window: runs of empty segments and more than 64
+segment starts inside one 64-block chunk (the per-lane search fallback), one segment
+spanning many waves, tiny totals, out_off == in_off in place -- and the queue-only
+contract: ragged calls return before their kernels finish (no host round trip)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import dev_u8, keyset, to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+
+def _package_case(engine, oracle, rng, lens, offs, keylen=32, nkeys=1, inplace=False, out_off_same=False):
+    n = len(lens)
+    total = int(max(offs + lens)) + 64 if n else 64
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+    slots = rng.integers(0, nkeys, n).astype(np.int32)
+    ks = keyset(engine, keys, keylen, ivs)
+    kw = dict(in_off=to_dev(offs.astype(np.int64)), lens=to_dev(lens.astype(np.int32)),
+              key_slot=to_dev(slots) if nkeys > 1 else None)
+    if out_off_same:
+        kw["out_off"] = to_dev(offs.astype(np.int64))  # same values, a different array
+    exp = inp.copy()
+    oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                         key_slot=slots.astype(np.uint32) if nkeys > 1 else None, keys=keys, keylen=keylen, ivs=ivs,
+                         threads=8)
+    src = to_dev(inp)
+    dst = src if inplace else to_dev(inp)
+    engine.package_decrypt(src, dst, n, ks, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(dst), exp)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_many_segment_starts_in_one_chunk(engine, oracle, inplace):
+    """Runs of 200 empty segments and of 1..3-byte segments: far more than 64 segment
+    starts fall inside single chunks, so the window re-anchors and the per-lane search
+    fallback runs."""
+    rng = np.random.default_rng(31 + inplace)
+    parts = []
+    for _ in range(40):
+        kind = rng.integers(0, 3)
+        if kind == 0:
+            parts.append(np.zeros(200, np.int64))
+        elif kind == 1:
+            parts.append(rng.integers(1, 4, 150))
+        else:
+            parts.append(rng.integers(0, 5000, 20))
+    lens = np.concatenate(parts)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64) + 16
+    _package_case(engine, oracle, rng, lens, offs, nkeys=5, inplace=inplace)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_empty_and_tiny_totals(engine, oracle, keylen):
+    rng = np.random.default_rng(keylen)
+    for lens in (np.zeros(50, np.int64), np.array([0, 0, 7, 0]), np.array([16] * 3), np.array([1]),
+                 np.array([0] * 70 + [33] + [0] * 70)):
+        offs = np.concatenate([[0], np.cumsum(lens[:-1] + 5)]).astype(np.int64)
+        _package_case(engine, oracle, rng, lens.astype(np.int64), offs, keylen=keylen)
+
+
+def test_one_segment_over_many_waves(engine, oracle):
+    """One 12 MiB + 7 B segment: every wave of the grid holds part of it, so every wave's
+    first chunk takes its predecessor block from the plan (also in place)."""
+    rng = np.random.default_rng(5)
+    lens = np.array([12 * 1024 * 1024 + 7])
+    offs = np.array([3])
+    for inplace in (False, True):
+        _package_case(engine, oracle, rng, lens, offs, inplace=inplace)
+
+
+def test_inplace_with_out_off_equal_in_off(engine, oracle):
+    """src is dst and out_off holds in_off's values in another array: still
+    in place, no wave may read a block another wave already decrypted."""
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 40000, 3000)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    _package_case(engine, oracle, rng, lens, offs, inplace=True, out_off_same=True)
+    _package_case(engine, oracle, rng, lens, offs, nkeys=3, inplace=True, out_off_same=True)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_stream_segments_random_positions(engine, oracle, keylen):
+    """Stream decrypt through K1r: 997 streams at random CFB positions with lengths from
+    0 to 70 000 B (partial first and last blocks, empties), state written back."""
+    rng = np.random.default_rng(400 + keylen)
+    n = 997
+    lens = rng.integers(0, 70000, n)
+    lens[rng.random(n) < 0.1] = 0
+    lens[rng.random(n) < 0.1] = rng.integers(1, 20, 1)[0]
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + 3)]).astype(np.int64)
+    total = int(offs[-1] + lens[-1] + 64)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    keys = rng.integers(0, 256, n * keylen, dtype=np.uint8)
+    iv_state = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    pos_state = rng.integers(0, 16, n).astype(np.uint32)
+    slots = np.arange(n, dtype=np.uint32)
+    exp = inp.copy()
+    iv_exp, pos_exp = iv_state.copy(), pos_state.copy()
+    oracle.stream_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                        lens=lens.astype(np.uint32), key_slot=slots, keys=keys, keylen=keylen, iv_state=iv_exp,
+                        pos_state=pos_exp, threads=8)
+    ks = keyset(engine, keys, keylen, np.zeros(n * 16, np.uint8))
+    for inplace in (False, True):
+        src = to_dev(inp)
+        dst = src if inplace else to_dev(inp)
+        ivd, posd = to_dev(iv_state), to_dev(pos_state.astype(np.int32))
+        engine.stream_decrypt(src, dst, n, ks, ivd, posd, in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)),
+                              key_slot=to_dev(slots.astype(np.int32)))
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(dst), exp)
+        assert np.array_equal(to_host(ivd), iv_exp)
+        assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
+
+
+# ------------------------------------------------------------------------------------
+# queue-only: the C-ABI's ragged calls must not wait for the GPU (fpnn_aes.h)
+
+
+def _big_ragged(rng, total_bytes, mean):
+    lens = rng.integers(1, 2 * mean, int(total_bytes // mean))
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    return lens.astype(np.int32), offs
+
+
+def _returns_before_done(call):
+    call()  # warm-up: scratch allocations
+    torch.cuda.synchronize()
+    call()
+    pending = not torch.cuda.current_stream().query()
+    torch.cuda.synchronize()
+    return pending
+
+
+def test_ragged_calls_do_not_block(engine):
+    import fpnn_amd
+    rng = np.random.default_rng(9)
+    lens, offs = _big_ragged(rng, 768 << 20, 3000)
+    n = len(lens)
+    buf = dev_u8(int(offs[-1] + lens[-1]) + 64)
+    ks = fpnn_amd.KeySet(engine, rng.bytes(32), 32, rng.bytes(16))
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens))
+    assert _returns_before_done(lambda: engine.package_decrypt(buf, buf, n, ks, **kw)), "package_decrypt waited"
+    # stream mode, per-stream keys and carried positions
+    keys = fpnn_amd.KeySet(engine, rng.bytes(16 * n), 16, rng.bytes(16 * n))
+    ivs = to_dev(rng.integers(0, 256, 16 * n, dtype=np.uint8))
+    pos = to_dev(rng.integers(0, 16, n).astype(np.int32))
+    slots = to_dev(np.arange(n, dtype=np.int32))
+    assert _returns_before_done(lambda: engine.stream_decrypt(buf, buf, n, keys, ivs, pos, key_slot=slots, **kw)), \
+        "stream_decrypt waited"
+    # dense whole-stream layout (the C3 shape: every stream at position 0, s * L)
+    S, L = 256, 1 << 20
+    dense = dev_u8(S * L)
+    zpos = torch.zeros(S, dtype=torch.int32, device=dense.device)
+    dkeys = fpnn_amd.KeySet(engine, rng.bytes(16 * S), 16, rng.bytes(16 * S))
+    div = to_dev(rng.integers(0, 256, 16 * S, dtype=np.uint8))
+    dslots = to_dev(np.arange(S, dtype=np.int32))
+    assert _returns_before_done(lambda: engine.stream_decrypt(dense, dense, S, dkeys, div, zpos.zero_(), stride=L,
+                                                              uniform_len=L, key_slot=dslots)), "dense stream waited"
+
+
+def test_recv_calls_do_not_block(engine):
+    import fpnn_amd
+    rng = np.random.default_rng(10)
+    conns, per, body = 8192, 64, 1020
+    seg = per * (body + 4)
+    wire = np.zeros(conns * seg, np.uint8).reshape(conns, per, body + 4)
+    wire[:, :, :4] = np.frombuffer(np.uint32(body).tobytes(), np.uint8)
+    buf = to_dev(wire.reshape(-1))
+    ks = fpnn_amd.KeySet(engine, rng.bytes(32), 32, rng.bytes(16))
+    assert _returns_before_done(lambda: engine.package_recv(buf, buf, conns, ks, 8 << 20,
+                                                            per, stride=seg, uniform_len=seg)), "package_recv waited"

@@ -186,3 +186,24 @@ def test_openssl_comparator_matches_oracle(oracle):
                              keylen=keylen, ivs=np.frombuffer(iv, np.uint8).copy())
         assert np.array_equal(tmp, exp)
         assert np.array_equal(out, inp)
+
+
+def test_golden_modes_cases(oracle, golden):
+    """The rest of rijndael.h restated (oracle/aes_oracle.c ao_setup_decrypt, ao_decrypt_block,
+    ao_cbc_*, ao_ofb) against the reference's outputs in tests/golden/modes_cases.json."""
+    g = golden("modes_cases.json")
+    for c in g["setup_decrypt"]:
+        ctx = oracle.setup_decrypt(bytes.fromhex(c["key"]))
+        assert ctx.nrounds == c["nrounds"] and list(ctx.rk[:len(c["rk"])]) == c["rk"]
+    for c in g["ecb_decrypt"]:
+        assert oracle.decrypt_block(bytes.fromhex(c["key"]), bytes.fromhex(c["in"])).hex() == c["out"]
+    for c in g["cbc"]:
+        out, iv = oracle.cbc(bytes.fromhex(c["key"]), c["encrypt"], bytes.fromhex(c["in"]), bytes.fromhex(c["iv"]),
+                             c["len"])
+        assert out.hex() == c["out"] and iv.hex() == c["iv_out"]
+    for c in g["ofb"]:
+        out, iv, pos = oracle.ofb(bytes.fromhex(c["key"]), bytes.fromhex(c["in"]), bytes.fromhex(c["iv"]), c["pos"])
+        assert (out.hex(), iv.hex(), pos) == (c["out"], c["iv_out"], c["pos_out"])
+    # FIPS-197 C.1 / C.3 inverse cipher
+    assert g["ecb_decrypt"][0]["out"] == "00112233445566778899aabbccddeeff"
+    assert g["ecb_decrypt"][1]["out"] == "00112233445566778899aabbccddeeff"

@@ -50,6 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--configs", default="C2,C3,C4,C5,U1,R1")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-memory / PCIe legs (profiling runs)")
     args = ap.parse_args()
     import fpnn_amd
     E, D = fpnn_amd.K_ENCRYPT, fpnn_amd.K_DECRYPT
@@ -68,6 +69,11 @@ def main():
         we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, stride=L, uniform_len=L), args.reps)
         wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, stride=L, uniform_len=L), args.reps)
         assert torch.equal(r, a)
+        if args.no_host:
+            out["C2"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd)}
+            print(json.dumps({"C2": out["C2"]}), flush=True)
+            todo = [t for t in todo if t != "C2"]
+    if "C2" in todo:
         # PCIe-inclusive: pinned host -> H2D -> kernel -> D2H, per direction
         h_in = torch.empty(P * L, dtype=torch.uint8, pin_memory=True)
         h_out = torch.empty_like(h_in, pin_memory=True)
@@ -182,6 +188,11 @@ def main():
         we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, **kw), args.reps)
         wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
         assert torch.equal(r, a)
+        if args.no_host:
+            out["U1"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd)}
+            print(json.dumps({"U1": out["U1"]}), flush=True)
+            todo = [t for t in todo if t != "U1"]
+    if "U1" in todo:
         src_h = a.cpu().numpy()
         dst_h = np.empty_like(src_h)
         fr = np.zeros(P, dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
@@ -260,9 +271,18 @@ def main():
             for f in range(nmax):
                 fn(src, dst, S, ks, st_iv, st_pos, in_off=d_offs[f], lens=d_lens[f], key_slot=slots)
 
-        wfe, _, _ = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), 1)
-        wfd, _, _ = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), 1)
+        wfe, kfe, nfe = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), 1)
+        wfd, kfd, nfd = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), 1)
         assert torch.equal(r, a)
+        if args.no_host:
+            out["C3"] = {"whole_stream_encrypt_kernel_GiBs": gib(S * L, ke),
+                         "whole_stream_decrypt_kernel_GiBs": gib(S * L, kd),
+                         "framed_calls": nmax, "framed_encrypt_wall_GiBs": gib(S * L, wfe),
+                         "framed_decrypt_wall_GiBs": gib(S * L, wfd),
+                         "framed_decrypt_kernel_GiBs": gib(S * L, kfd * nfd)}
+            print(json.dumps({"C3": out["C3"]}), flush=True)
+            todo = [t for t in todo if t != "C3"]
+    if "C3" in todo:
         # host frames, one stream_host call for the framed streams of a 1 GiB subset
         HS = 256
         src_h = a[:HS * L].cpu().numpy()
@@ -291,6 +311,7 @@ def main():
                      "whole_stream_decrypt_kernel_GiBs": gib(S * L, kd),
                      "framed_calls": nmax, "framed_encrypt_wall_GiBs": gib(S * L, wfe),
                      "framed_decrypt_wall_GiBs": gib(S * L, wfd),
+                     "framed_decrypt_kernel_GiBs": gib(S * L, kfd * nfd),
                      "host_frames_streams": HS, "host_frames": len(fl),
                      "host_frames_encrypt_GiBs": gib(HS * L, hse), "host_frames_decrypt_GiBs": gib(HS * L, hsd),
                      "note": "encrypt = 4096 serial CFB chains (one lane each, latency bound); "
@@ -327,8 +348,8 @@ def main():
         out["R1"] = {"frames": P, "body_bytes": P * L, "recv_wall_GiBs": gib(P * L, wr),
                      "decrypt_kernel_GiBs": gib(P * L, kr),
                      "note": "fpnn_aes_package_recv over 16384 connections x 64 wire frames (4-byte LE length + 1 KiB): "
-                             "device frame scan + decrypt of the bodies at their frame offsets (wall includes the scan "
-                             "and the host sync for the block total)"}
+                             "device frame scan + decrypt of the bodies at their frame offsets (wall includes the scan, "
+                             "the block-map scan and the plan; no host sync)"}
         del a, wire, plain
         print(json.dumps({"R1": out["R1"]}), flush=True)
 

@@ -65,6 +65,12 @@ def main():
             d["effective_clock_GHz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / statistics.mean(dur), 3)
         if "SQ_LDS_BANK_CONFLICT" in avg and "SQ_LDS_IDX_ACTIVE" in avg and avg["SQ_LDS_IDX_ACTIVE"]:
             d["lds_bank_conflict_frac"] = round(avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"], 5)
+        if "SQ_LDS_IDX_ACTIVE" in avg and "GRBM_GUI_ACTIVE" in avg and avg["GRBM_GUI_ACTIVE"]:
+            # LDS array busy: per-CU LDS-active cycles over the kernel's GPU-active cycles
+            # (SQ_ counters sum over the 256 CUs, GRBM_GUI_ACTIVE over the 8 XCDs)
+            d["lds_array_busy_frac"] = round((avg["SQ_LDS_IDX_ACTIVE"] / 256) / (avg["GRBM_GUI_ACTIVE"] / 8), 4)
+        if "SQ_INSTS_VALU" in avg and avg.get("SQ_INSTS_LDS"):
+            d["valu_per_lds_inst"] = round(avg["SQ_INSTS_VALU"] / avg["SQ_INSTS_LDS"], 3)
         if "SQ_WAVE_CYCLES" in avg:
             wc = avg["SQ_WAVE_CYCLES"]
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY",
