@@ -288,12 +288,26 @@ __device__ __forceinline__ uint4 select_bytes(uint4 m, uint4 a, uint4 b) {  // (
 }
 
 // block whose byte j = base[j] for j in [lo, hi), 0 elsewhere (base may point outside
-// the buffer; only bytes inside [lo, hi) are dereferenced)
+// the buffer; only bytes inside [lo, hi) are dereferenced).  The byte loads are
+// unconditional -- byte j reads base[clamp(j, lo, hi - 1)] and is masked afterwards -- so
+// each word's four loads go out together (one wait per word, not per byte).
 __device__ __forceinline__ uint4 load_bytes(const uint8_t *base, int lo, int hi) {
     uint32_t w[4] = {0, 0, 0, 0};
+    if (lo >= hi) return make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (j >= lo && j < hi) w[j >> 2] |= (uint32_t)base[j] << (8 * (j & 3));
+    for (int q = 0; q < 4; q++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int j = 4 * q + t;
+            v[t] = base[j < lo ? lo : j >= hi ? hi - 1 : j];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int j = 4 * q + t;
+            w[q] |= (j >= lo && j < hi ? v[t] : 0u) << (8 * t);
+        }
+    }
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 

@@ -189,8 +189,11 @@ struct fpnn_aes_engine {
     uint64_t cap_fr_slot = 0;
     RaggedPlan *d_plan = nullptr;  // K1r: one entry per wave of the decrypt grid
     uint64_t cap_plan = 0;
-    uint64_t *d_total = nullptr;  // [0] ragged block total, [1] non-contiguous segments
-    uint64_t *h_total = nullptr;  // pinned
+    uint64_t *d_desc_off = nullptr;  // K1r: materialized in_off / len of stride / uniform batches
+    uint64_t cap_desc_off = 0;
+    uint32_t *d_desc_len = nullptr;
+    uint64_t cap_desc_len = 0;
+    uint64_t *d_total = nullptr;  // ragged block total (bstart[count]), device only
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
@@ -423,6 +426,15 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
         HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         k.bstart = e->d_bstart;
+        if (!k.in_off || !k.len) {  // K1r reads descriptor arrays: materialize the missing ones
+            if (!k.in_off && (rc = grow(e->d_desc_off, e->cap_desc_off, b->count))) return rc;
+            if (!k.len && (rc = grow(e->d_desc_len, e->cap_desc_len, b->count))) return rc;
+            HIP_TRY(launch_ragged_desc(b->count, b->stride, b->uniform_len, k.in_off ? nullptr : e->d_desc_off,
+                                       k.len ? nullptr : e->d_desc_len, e->stream));
+            if (!k.in_off) k.in_off = e->d_desc_off;
+            if (!k.len) k.len = e->d_desc_len;
+        }
+        if (!k.out_off) k.out_off = k.in_off;
         EventPair *ev = nullptr;
         if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
         HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, grid, e->stream));
@@ -519,7 +531,6 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_DEC_GAPPED")) e->variant.dec_gapped = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
@@ -541,9 +552,8 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         if (err == hipSuccess) err = hipMemcpy(e->d_tables + 1280, kTables.td0le, 1024, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(e->d_tables + 2304, kTables.isbox, 256, hipMemcpyHostToDevice);
         if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
-        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), 4 * sizeof(uint64_t));  // total, contiguity, gapped
-        if (err == hipSuccess) err = hipHostMalloc(reinterpret_cast<void **>(&e->h_total), 4 * sizeof(uint64_t), 0);
-        if (err != hipSuccess) { rc = hip_fail(err, "alloc(total)"); break; }
+        err = hipMalloc(reinterpret_cast<void **>(&e->d_total), sizeof(uint64_t));
+        if (err != hipSuccess) { rc = hip_fail(err, "hipMalloc(total)"); break; }
     } while (0);
     if (rc) {
         fpnn_aes_engine_destroy(e);
@@ -569,9 +579,10 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_fr_off);
     (void)hipFree(e->d_fr_slot);
     (void)hipFree(e->d_plan);
+    (void)hipFree(e->d_desc_off);
+    (void)hipFree(e->d_desc_len);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
-    if (e->h_total) (void)hipHostFree(e->h_total);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     for (auto &v : e->ev)
         for (auto &p : v) {
@@ -1165,7 +1176,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         uint64_t state0 = si;  // stream: state index of the chunk's first segment
         uint64_t in_b = 0;
         uint32_t cnt = 0;
-        uint64_t out_b = 0, total_blocks = 0, in_pad = 0, out_pad = 0, arr = 0, out_at = 0;
+        uint64_t out_b = 0, in_pad = 0, out_pad = 0, arr = 0, out_at = 0;
         if (!stream) {
             // whole frames [si, j) with <= kChunk input bytes (at least one frame)
             uint64_t j = si;
@@ -1183,7 +1194,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             uint32_t *slots = lens + cnt;
             // frame-parallel: per-part byte sums, then offsets + arrays + gather per part
             const unsigned parts = copy_parts(e, in_b);
-            uint64_t psum[64 + 1] = {0}, pblk[64] = {0};
+            uint64_t psum[64 + 1] = {0};
             const fpnn_aes_host_frame *fr = frames + si;
             auto range = [&](unsigned p, uint32_t &a, uint32_t &b) {
                 a = (uint32_t)((uint64_t)cnt * p / parts);
@@ -1193,18 +1204,11 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             pool_of(e)->run(parts, [&](unsigned p) {
                 uint32_t a, b;
                 range(p, a, b);
-                uint64_t sum = 0, blk = 0;
-                for (uint32_t t = a; t < b; t++) {
-                    sum += fr[t].len;
-                    blk += (fr[t].len + 15ull) >> 4;
-                }
+                uint64_t sum = 0;
+                for (uint32_t t = a; t < b; t++) sum += fr[t].len;
                 psum[p + 1] = sum;
-                pblk[p] = blk;
             });
-            for (unsigned p = 0; p < parts; p++) {
-                psum[p + 1] += psum[p];
-                total_blocks += pblk[p];
-            }
+            for (unsigned p = 0; p < parts; p++) psum[p + 1] += psum[p];
             uint8_t *h_in = s.h;
             pool_of(e)->run(parts, [&](unsigned p) {
                 uint32_t a, b;
@@ -1276,7 +1280,6 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
                 in_off[t] = out_off[t] = cs[t].at;
                 lens[t] = (uint32_t)cs[t].len;
                 slots[t] = cs[t].slot;
-                total_blocks += cs[t].len ? (cs[t].pos + cs[t].len + 15) >> 4 : 0;
             }
             gather.clear();
             s.scatter.clear();

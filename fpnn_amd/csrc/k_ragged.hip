@@ -67,7 +67,7 @@ __device__ __forceinline__ uint4 predecessor_block(const KBatch &b, uint64_t s, 
 template <bool STREAM>
 __global__ __launch_bounds__(256) void k_ragged_plan(KBatch b, uint64_t nwaves, RaggedPlan *plan) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t w = __builtin_amdgcn_readfirstlane(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     if (w >= nwaves) return;
     const uint64_t total = b.bstart[b.count];
     uint64_t c0, c1;
@@ -80,26 +80,63 @@ __global__ __launch_bounds__(256) void k_ragged_plan(KBatch b, uint64_t nwaves, 
     }
 }
 
-// Segment of each lane's block in one chunk (descriptor loads issued, not waited for).
+// Segment descriptors of each lane's block in one chunk (loads issued, not waited for).
 struct RDesc {
-    uint64_t g, s, bs;
-    uint64_t io, oo;
-    uint32_t len, slot, n0;
-    bool uni;  // wave-uniform: the whole chunk lies in one segment (descriptors by scalar loads)
+    uint64_t g;  // the lane's block (clamped into the batch)
+    uint64_t bs, io, oo;
+    uint32_t s, len, slot, n0;
+    bool uni;    // wave-uniform: the whole chunk lies in segment s
 };
 
 // The chunk itself: ciphertext block + what its store and CFB fill need.
 struct RChunk {
-    uint4 x, ivs;
+    uint4 x;
+    const uint8_t *in;  // segment bases
     uint8_t *out;
     uint32_t s, bi, len, n0, slot;  // count < 2^32 (fpnn_aes_batch.count is 32-bit)
     bool valid;
-    bool simple;  // wave-uniform: one segment and whole 16-byte blocks only (no byte-granular edge)
+    bool full;  // the block is 16 whole bytes of the segment (plain 16-B load / store)
 };
 
 typedef __attribute__((address_space(4))) const DevKey ConstDevKeyR;
 typedef __attribute__((address_space(4))) const uint64_t ConstU64R;
 typedef __attribute__((address_space(4))) const uint32_t ConstU32R;
+
+// (the builtins return int: each half goes through uint32_t so the low half is not
+// sign-extended into the high one -- offsets past 2 GiB have bit 31 set)
+__device__ __forceinline__ uint64_t readfirst64(uint64_t v) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Memory-access discipline of this kernel (what keeps its prefetches in flight): every
+// load whose result is needed in the same chunk is consumed inside the (rare) branch
+// that issued it; the loads of the pipeline ring (descriptors two chunks ahead,
+// ciphertext one to DEPTH-1 chunks ahead) are issued unconditionally in straight-line
+// code -- past the wave's last chunk they re-read that chunk -- so the compiler's
+// waitcnt pass can count them exactly instead of draining the memory pipe (vmcnt(0)).
+// The host guarantees in_off, out_off and len are device arrays (launch_decrypt_ragged).
+// Round keys from the key table: the first KS words stay in SGPRs, the rest are copied to
+// VGPRs (every lane the same value).  All in SGPRs they push this kernel's scalar state
+// past the SGPR file, and the spills cost the cipher its LDS parallelism (the scheduler
+// then waits after every one or two lookups); all in VGPRs, AES-256's 60 words push the
+// vector state past the 128 VGPRs of 4 waves per SIMD.
+template <int NR, int KS = NR == 14 ? 28 : NR == 12 ? 12 : 0>
+__device__ __forceinline__ void set_keys(RoundKeys<NR> &rk, ConstDevKeyR *kp) {
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); i++) {
+        const uint32_t v = kp->rk[i];
+        if (i < KS) rk.k[i] = v;
+        else asm volatile("v_mov_b32 %0, %1" : "=v"(rk.k[i]) : "s"(v));
+    }
+}
 
 template <int NR, bool STREAM, int KM>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, const RaggedPlan *__restrict__ plan) {
@@ -109,23 +146,26 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const uint64_t w = __builtin_amdgcn_readfirstlane(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const uint64_t count = b.count;
     const uint64_t total = ((ConstU64R *)b.bstart)[count];
     uint64_t c0, c1;
     wave_chunk_range((total + 63) >> 6, nwaves, w, c0, c1);
     if (c0 >= c1) return;
 
-    // uniform key (one key slot for the batch): round keys and IV in SGPRs
+    // round keys (VGPRs): the batch's one key, or (KEY_LANE) the last slot used
     RoundKeys<NR> rku;
+    uint32_t key_slot = ~0u;
     uint4 ivu = make_uint4(0, 0, 0, 0);
     if (KM == KEY_UNIFORM) {
         ConstDevKeyR *kp = (ConstDevKeyR *)b.keys;
-#pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); i++) rku.k[i] = kp->rk[i];
+        set_keys(rku, kp);
         ConstU32R *ivp = (ConstU32R *)kp->iv;
         ivu = make_uint4(ivp[0], ivp[1], ivp[2], ivp[3]);
     }
+    const uint8_t *dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 16 readable bytes
+    // 32 writable bytes that nobody reads after the first lines below: this wave's plan entry
+    uint8_t *scratch = reinterpret_cast<uint8_t *>(const_cast<RaggedPlan *>(plan) + w);
 
     // window: wv = bstart[wb + lane] (all-ones past bstart[count])
     uint64_t wb = ((ConstU64R *)&plan[w].s0)[0];
@@ -140,40 +180,45 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         fill = make_uint4(fp[0], fp[1], fp[2], fp[3]);
     }
 
-    // --- segment of every lane's block in chunk c --------------------------------------
+    // descriptors of the segment of the last fetched single-segment chunk (SGPRs)
+    uint32_t last_s = ~0u, last_len = 0, last_slot = 0, last_n0 = 0;
+    uint64_t last_bs = 0, last_io = 0, last_oo = 0;
+
+    // --- segment of every lane's block in chunk c, descriptor loads issued ----------
     auto locate = [&](uint64_t c) -> RDesc {
         RDesc D;
         const uint64_t base = c << 6;
         D.g = base + lane < total ? base + lane : total - 1;  // lanes past the end: clamped, not stored
         const uint32_t gl = (uint32_t)(D.g - base);
+        uint32_t r0 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane >= 1 && wv <= base));
         bool slow = false;
-        uint32_t r0;
-        while (true) {
-            r0 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane >= 1 && wv <= base));
-            const uint64_t last = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(wv >> 32), 63) << 32) |
-                                  __builtin_amdgcn_readlane((uint32_t)wv, 63);
-            if (last > base + 63) break;  // every segment start in the chunk is in the window
-            if (r0 == 0) {                // >= 63 starts inside one chunk: search per lane
-                slow = true;
-                break;
+        if (readlane64(wv, 63) <= base + 63) {  // rare: segment starts past the window's end
+            while (true) {
+                if (r0 == 0) {  // 63 starts inside one chunk: search per lane below
+                    slow = true;
+                    break;
+                }
+                wb += r0;  // re-window at the segment holding the chunk's first block
+                wv = load_window();
+                r0 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane >= 1 && wv <= base));
+                if (readlane64(wv, 63) > base + 63) break;
             }
-            wb += r0;  // re-window at the segment holding the chunk's first block
-            wv = load_window();
         }
+        uint32_t s;
         uint64_t m = slow ? ~0ull : __builtin_amdgcn_ballot_w64(lane >= 1 && wv > base && wv <= base + 63);
         D.uni = m == 0;
-        if (D.uni) {  // one segment: descriptors are wave-uniform scalar loads
-            const uint64_t su = wb + r0;
-            D.s = su;
-            D.bs = ((ConstU64R *)b.bstart)[su];
-            D.io = b.in_off ? ((ConstU64R *)b.in_off)[su] : su * b.stride;
-            D.oo = b.out_off ? ((ConstU64R *)b.out_off)[su] : D.io;
-            D.len = b.len ? ((ConstU32R *)b.len)[su] : b.uniform_len;
-            D.slot = (KM == KEY_LANE && b.key_slot) ? ((ConstU32R *)b.key_slot)[su] : 0u;
-            D.n0 = STREAM ? ((ConstU32R *)b.pos_snap)[su] : 0u;
+        if (D.uni && (uint32_t)(wb + r0) == last_s) {
+            // the chunk continues the segment of the chunk fetched before it (long
+            // segments: almost every chunk): its descriptors are in SGPRs, no loads
+            D.s = last_s;
+            D.bs = last_bs;
+            D.io = last_io;
+            D.oo = last_oo;
+            D.len = last_len;
+            D.slot = last_slot;
+            D.n0 = last_n0;
             return D;
         }
-        uint64_t s;
         if (!slow) {
             uint32_t r = r0;
             while (m) {  // the segments that open inside this chunk, in order
@@ -182,21 +227,21 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 const uint32_t pos = __builtin_amdgcn_readlane((uint32_t)wv, k) - (uint32_t)base;
                 r += gl >= pos ? 1u : 0u;
             }
-            s = wb + r;
+            s = (uint32_t)(wb + r);
         } else {
             uint64_t lo = wb, hi = count - 1;  // largest s with bstart[s] <= g
             while (lo < hi) {
                 const uint64_t mid = (lo + hi + 1) >> 1;
                 if (b.bstart[mid] <= D.g) lo = mid; else hi = mid - 1;
             }
-            s = lo;
+            s = (uint32_t)lo;
         }
         D.s = s;
         D.bs = b.bstart[s];
-        D.io = b.in_off ? b.in_off[s] : s * b.stride;
-        D.oo = b.out_off ? b.out_off[s] : D.io;
-        D.len = b.len ? b.len[s] : b.uniform_len;
-        D.slot = (KM == KEY_LANE && b.key_slot) ? b.key_slot[s] : 0u;
+        D.io = b.in_off[s];
+        D.oo = b.out_off[s];
+        D.len = b.len[s];
+        D.slot = KM == KEY_LANE ? b.key_slot[s] : 0u;
         D.n0 = STREAM ? b.pos_snap[s] : 0u;
         return D;
     };
@@ -205,40 +250,49 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     auto fetch = [&](const RDesc &D, uint64_t c) -> RChunk {
         RChunk X;
         X.valid = (c << 6) + lane < total;
-        X.s = (uint32_t)D.s;
+        X.s = D.s;
         X.bi = (uint32_t)(D.g - D.bs);
         X.len = D.len;
         X.n0 = D.n0;
         X.slot = D.slot;
-        const uint8_t *in = b.in + D.io;
+        X.in = b.in + D.io;
         X.out = b.out + D.oo;
-        X.ivs = ivu;
-        if (X.bi == 0) {  // the lane opens its segment: CFB input = IV (carried IV in stream mode)
-            if (STREAM) X.ivs = b.iv_snap[X.s];
-            else if (KM == KEY_LANE) X.ivs = *reinterpret_cast<const uint4 *>(b.keys[X.slot].iv);
+        if (D.uni) {  // remember the segment (uniform values; the loads have arrived by now)
+            last_s = D.s;
+            last_bs = readfirst64(D.bs);
+            last_io = readfirst64(D.io);
+            last_oo = readfirst64(D.oo);
+            last_len = __builtin_amdgcn_readfirstlane(D.len);
+            last_slot = __builtin_amdgcn_readfirstlane(D.slot);
+            last_n0 = __builtin_amdgcn_readfirstlane(D.n0);
         }
-        // simple chunk: one segment, no partial head block (stream position) and no partial
-        // last block inside it -- every lane loads and stores one whole 16-byte block
-        X.simple = false;
-        if (D.uni) {
-            const uint32_t bi0 = __builtin_amdgcn_readfirstlane(X.bi);  // lane 0 is never clamped
-            const uint64_t nbs = seg_blocks(X.len, X.n0);
-            const bool partial_head = bi0 == 0 && X.n0 != 0;
-            const bool partial_tail = ((X.n0 + X.len) & 15u) != 0 && (uint64_t)bi0 + 63 >= nbs - 1;
-            X.simple = !partial_head && !partial_tail;
-        }
-        if (X.simple)
-            X.x = load16(in + 16ull * X.bi - X.n0);
-        else
-            X.x = load_cx(Seg{in, X.out, X.len, X.slot}, X.n0, X.bi, X.ivs);
+        const int64_t lo = 16 * (int64_t)X.bi - X.n0;  // the block's first byte in the segment
+        X.full = lo >= 0 && lo + 16 <= (int64_t)X.len;
+        X.x = load16(X.full ? X.in + lo : dummy);  // edge blocks are built in process()
         return X;
     };
 
     // --- decrypt one chunk; returns lane 63's ciphertext block (the next chunk's fill) --
-    auto process = [&](const RChunk &X, const uint4 &f) -> uint4 {
+    auto process = [&](RChunk &X, const uint4 &f) -> uint4 {
+        // lanes that open their segment take its IV (stream: the carried ivec), loaded here
+        // in a branch taken only by chunks where a segment starts (and drained inside it)
+        uint4 ivs = ivu;
+        if (STREAM || KM == KEY_LANE) {
+            if (__builtin_amdgcn_ballot_w64(X.bi == 0) != 0) {
+                if (X.bi == 0)
+                    ivs = STREAM ? b.iv_snap[X.s] : *reinterpret_cast<const uint4 *>(b.keys[X.slot].iv);
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(X.valid && !X.full) != 0) {  // segment edges: byte-exact block
+            if (X.valid && !X.full) X.x = load_cx(Seg{X.in, X.out, X.len, X.slot}, X.n0, X.bi, ivs);
+            // drain here, inside the rare branch: the merge below then carries no pending
+            // load, and the common path keeps its prefetches in flight
+            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        }
         uint4 kin = make_uint4(wave_shr1(X.x.x, f.x), wave_shr1(X.x.y, f.y), wave_shr1(X.x.z, f.z),
                                wave_shr1(X.x.w, f.w));
-        if (X.bi == 0) kin = X.ivs;
+        if (X.bi == 0) kin = ivs;
         uint4 ks;
         if (KM == KEY_UNIFORM) {
             ks = aes_encrypt_block<NR, 4>(kin, rku, T);
@@ -246,6 +300,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
             // one pass per distinct key slot in the chunk, each with wave-uniform (SGPR)
             // round keys; a lane keeps the pass of its own slot.  Chunks inside one segment
             // (the common case) take one pass; no per-lane key registers.
+            // AES-128: the round keys live in VGPRs and are reloaded only when the slot
+            // changes (a stream's or connection's chunks follow each other).  AES-192/256:
+            // scalar loads per pass (their 52-60 words fit neither register file for the
+            // whole loop beside the pipeline state).
             uint64_t todo = __builtin_amdgcn_read_exec();
             ks = make_uint4(0, 0, 0, 0);
             do {
@@ -253,58 +311,89 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 const uint32_t slotk = __builtin_amdgcn_readlane(X.slot, first);
                 const bool mine = X.slot == slotk;
                 todo &= ~__builtin_amdgcn_ballot_w64(mine);
-                RoundKeys<NR> rk;
-                ConstDevKeyR *kp = (ConstDevKeyR *)b.keys + slotk;
-#pragma unroll
-                for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = kp->rk[i];
-                const uint4 e = aes_encrypt_block<NR, 4>(kin, rk, T);
+                uint4 e;
+                if (NR == 10) {
+                    if (slotk != key_slot) {
+                        set_keys(rku, (ConstDevKeyR *)b.keys + slotk);
+                        key_slot = slotk;
+                    }
+                    e = aes_encrypt_block<NR, 4>(kin, rku, T);
+                } else {
+                    RoundKeys<NR> rk;
+                    set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
+                    e = aes_encrypt_block<NR, 4>(kin, rk, T);
+                }
                 if (mine) ks = e;
             } while (todo);
         }
-        if (STREAM && X.bi == 0 && X.n0 != 0) ks = X.ivs;  // keystream bytes already in the carried ivec
-        if (X.valid) {
-            if (X.simple)
-                store16(X.out + 16ull * X.bi - X.n0, X.x ^ ks);
-            else
-                store_cx(Seg{nullptr, X.out, X.len, X.slot}, X.n0, X.bi, X.x ^ ks);
-            if (STREAM && (uint64_t)X.bi + 1 == seg_blocks(X.len, X.n0)) {  // last block: export (ivec, pos)
-                const uint32_t pos = (X.n0 + X.len) & 15u;
-                const uint4 nv = pos ? select_bytes(byte_mask(0, (int)pos), X.x, ks) : X.x;
-                *reinterpret_cast<uint4 *>(b.iv_state + 16ull * X.s) = nv;
-                b.pos_state[X.s] = pos;
+        if (STREAM && X.bi == 0 && X.n0 != 0) ks = ivs;  // keystream bytes already in the carried ivec
+        // Stores are unconditional (lanes with nothing to store write the wave's scratch
+        // slot), so the waitcnt pass always knows how many are in flight; the byte-exact
+        // edge stores run in a rare branch that drains before it rejoins.
+        const uint4 pt = X.x ^ ks;
+        store16(X.valid && X.full ? X.out + (16ull * X.bi - X.n0) : scratch, pt);
+        if (__builtin_amdgcn_ballot_w64(X.valid && !X.full) != 0) {
+            if (X.valid && !X.full) store_cx(Seg{X.in, X.out, X.len, X.slot}, X.n0, X.bi, pt);
+            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        }
+        if (STREAM) {  // the segment's last block exports (ivec, pos) (base/rijndael.c:1171-1201)
+            const bool last = X.valid && (uint64_t)X.bi + 1 == seg_blocks(X.len, X.n0);
+            if (__builtin_amdgcn_ballot_w64(last) != 0) {  // once per segment: a rare branch
+                if (last) {
+                    const uint32_t pos = (X.n0 + X.len) & 15u;
+                    *reinterpret_cast<uint4 *>(b.iv_state + 16ull * X.s) =
+                        pos ? select_bytes(byte_mask(0, (int)pos), X.x, ks) : X.x;
+                    b.pos_state[X.s] = pos;
+                }
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
             }
         }
         return readlane63(X.x);
     };
 
-    // pipeline: while chunk c is enciphered, the ciphertext of chunks c+1 .. c+DEPTH-1 and
-    // the descriptors of the next chunk to fetch are in flight (a ring of DEPTH chunk
-    // buffers, one descriptor buffer)
-    constexpr int DEPTH = 3;
-    RChunk X[DEPTH];
-    RDesc D = locate(c0);
-    uint64_t next = c0;  // next chunk to fetch; D = its descriptors
-#pragma unroll
-    for (int j = 0; j < DEPTH; j++) {
-        if (next < c1) {
-            X[j] = fetch(D, next);
-            next++;
-            if (next < c1) D = locate(next);
-        }
-    }
-    uint64_t c = c0;
+    // Pipeline.  The vector-memory counter retires in issue order, so a wait for a load
+    // also waits for everything issued before it.  Each half of the loop body issues the
+    // next chunk's ciphertext load and the descriptor loads of the chunk after it, THEN
+    // enciphers the current chunk: the current chunk's ciphertext was issued one cipher
+    // earlier, and the back edge follows a cipher, so the loop header (where the compiler
+    // rotates its registers and must wait for their loads) only waits for loads issued
+    // one cipher ago.  Indices past the wave's range are clamped to its last chunk
+    // (re-read, never stored).
+    const uint64_t clast = c1 - 1;
+    auto cl = [&](uint64_t x) { return x < clast ? x : clast; };
+    RDesc D1, D0 = locate(c0);
+    RChunk X1, X0 = fetch(D0, c0);
+    D1 = locate(cl(c0 + 1));
+    uint64_t c = c0;  // X0 = chunk c, D1 = descriptors of chunk c + 1
     while (true) {
-#pragma unroll
-        for (int j = 0; j < DEPTH; j++) {  // X[j] holds chunk c
-            fill = process(X[j], fill);
-            if (next < c1) {
-                X[j] = fetch(D, next);
-                next++;
-                if (next < c1) D = locate(next);
-            }
-            if (++c >= c1) return;
-        }
+        X1 = fetch(D1, cl(c + 1));
+        D0 = locate(cl(c + 2));
+        fill = process(X0, fill);
+        if (++c >= c1) return;
+        X0 = fetch(D0, cl(c + 1));
+        D1 = locate(cl(c + 2));
+        fill = process(X1, fill);
+        if (++c >= c1) return;
     }
+}
+
+// For K1r every segment needs in_off / out_off / len arrays: missing ones are written here
+// from the stride / uniform length (out_off missing = in_off).
+__global__ __launch_bounds__(256) void k_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len,
+                                                     uint64_t *in_off, uint32_t *len) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < count;
+         s += (uint64_t)gridDim.x * blockDim.x) {
+        if (in_off) in_off[s] = s * stride;
+        if (len) len[s] = uniform_len;
+    }
+}
+
+hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len, uint64_t *in_off, uint32_t *len,
+                              hipStream_t st) {
+    if (count && (in_off || len))
+        hipLaunchKernelGGL(k_ragged_desc, dim3(grid_for(count, 256, 4096)), dim3(256), 0, st, count, stride,
+                           uniform_len, in_off, len);
+    return hipGetLastError();
 }
 
 template <int NR>

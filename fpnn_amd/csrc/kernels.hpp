@@ -61,7 +61,6 @@ struct Variant {
     int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
-    int dec_gapped = 1;    // decrypt, ragged whole-block segments with gaps: K1d ragged + address deltas
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
@@ -121,8 +120,12 @@ struct RaggedPlan {
     uint64_t pad;
     uint4 fill;   // ciphertext block before it (same segment), saved before any write
 };
+// b.in_off, b.out_off and b.len must be device arrays (launch_ragged_desc writes the missing
+// ones from stride / uniform_len; out_off may be in_off).
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, int grid,
                                  hipStream_t st);
+hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len, uint64_t *in_off, uint32_t *len,
+                              hipStream_t st);
 // In-place K1 / K1d: save the ciphertext block before every 64-block chunk.
 hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchunks, hipStream_t st);
 // General-layout block map: bstart[0..count] (bstart[count] = *total = total blocks, both

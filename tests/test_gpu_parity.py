@@ -330,9 +330,8 @@ def test_contiguous_ragged_decrypt(engine, oracle, layout):
 @pytest.mark.parametrize("inplace", [False, True])
 def test_gapped_ragged_decrypt(engine, oracle, gaps, inplace):
     """Ragged whole-block package segments with gaps between them (the receive path:
-    bodies behind 4-byte length prefixes), empty segments interleaved: K1d ragged with
-    per-segment address deltas ('reversed': segments in descending memory order, so the
-    deltas are negative).  'odd_len' has one partial block and must fall back to K1."""
+    bodies behind 4-byte length prefixes), empty segments interleaved, through K1r
+    ('reversed': segments in descending memory order; 'odd_len': one partial block)."""
     if inplace and gaps == "shifted_out":
         pytest.skip("shifted output is out of place")
     rng = np.random.default_rng(["wire4", "random", "reversed", "shifted_out", "odd_len"].index(gaps) + 31 * inplace)

@@ -175,3 +175,46 @@ def test_recv_calls_do_not_block(engine):
     ks = fpnn_amd.KeySet(engine, rng.bytes(32), 32, rng.bytes(16))
     assert _returns_before_done(lambda: engine.package_recv(buf, buf, conns, ks, 8 << 20,
                                                             per, stride=seg, uniform_len=seg)), "package_recv waited"
+
+
+@pytest.mark.parametrize("stream", [False, True])
+def test_offsets_beyond_2gib(engine, oracle, stream):
+    """Segments at byte offsets across and past 2^31 in a 2.3 GB buffer, long enough that
+    each wave walks many chunks of one segment (the descriptor cache): 64-bit offsets
+    must survive every cross-lane move (a sign-extended low half once faulted on C4)."""
+    rng = np.random.default_rng(2031 + stream)
+    base = (1 << 31) - (48 << 20)
+    n = 1500
+    lens = rng.integers(1, 200_000, n)
+    offs_rel = np.concatenate([[0], np.cumsum(lens[:-1] + rng.integers(0, 40, n - 1))]).astype(np.int64)
+    span = int(offs_rel[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, span, dtype=np.uint8)
+    keys = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    ivs = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    slots = np.arange(n, dtype=np.uint32)
+    exp = host.copy()
+    if stream:
+        pos = rng.integers(0, 16, n).astype(np.uint32)
+        iv_exp, pos_exp = ivs.copy(), pos.copy()
+        oracle.stream_batch(False, host, exp, n, in_off=offs_rel.astype(np.uint64), out_off=offs_rel.astype(np.uint64),
+                            lens=lens.astype(np.uint32), key_slot=slots, keys=keys, keylen=16, iv_state=iv_exp,
+                            pos_state=pos_exp, threads=8)
+    else:
+        oracle.package_batch(False, host, exp, n, in_off=offs_rel.astype(np.uint64), lens=lens.astype(np.uint32),
+                             key_slot=slots, keys=keys, keylen=16, ivs=ivs, threads=8)
+    big = torch.empty(base + span, dtype=torch.uint8, device="cuda:0")
+    big[base:].copy_(torch.from_numpy(host))
+    kw = dict(in_off=to_dev(offs_rel + base), lens=to_dev(lens.astype(np.int32)), key_slot=to_dev(slots.astype(np.int32)))
+    if stream:
+        ks = keyset(engine, keys, 16, np.zeros(n * 16, np.uint8))
+        ivd, posd = to_dev(ivs), to_dev(pos.astype(np.int32))
+        engine.stream_decrypt(big, big, n, ks, ivd, posd, **kw)
+    else:
+        ks = keyset(engine, keys, 16, ivs)
+        engine.package_decrypt(big, big, n, ks, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(big[base:].cpu().numpy(), exp)
+    if stream:
+        assert np.array_equal(to_host(ivd), iv_exp) and np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
+    del big
+    torch.cuda.empty_cache()

@@ -153,6 +153,27 @@ def main():
         del a, b, r, h_in, h_out
         print(json.dumps({"C2": out["C2"]}), flush=True)
 
+    if "C2R" in todo:
+        # C2's packets described as a ragged batch (offset / length arrays): the general
+        # decrypt K1r on the exact data K1d decrypts in C2 -- isolates K1r's own cost
+        c = W.C2
+        P, L = c["packets"], c["length"]
+        key, iv = W.single_key(c)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, c["payload_seed"])
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        eng.package_encrypt(a, b, P, ks, stride=L, uniform_len=L)
+        kw = dict(in_off=torch.arange(P, dtype=torch.int64, device="cuda") * L,
+                  lens=torch.full((P,), L, dtype=torch.int32, device="cuda"))
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
+        assert torch.equal(r, a)
+        wu, ku, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, stride=L, uniform_len=L), args.reps)
+        out["C2R"] = {"ragged_decrypt_kernel_GiBs": gib(P * L, kd), "ragged_decrypt_wall_GiBs": gib(P * L, wd),
+                      "dense_decrypt_kernel_GiBs": gib(P * L, ku), "ragged_kernel": eng.last_kernel(D)}
+        del a, b, r
+        print(json.dumps({"C2R": out["C2R"]}), flush=True)
+
     if "C5" in todo:
         c = W.C5
         P, L = c["packets"], c["length"]
