@@ -10,6 +10,8 @@ container only).  Writes data only -- inputs and the reference's outputs:
   package_cases.json PackageEncryptor encrypt / decrypt / encrypt(std::string*) frames
   stream_cases.json StreamEncryptor call sequences (state carried across frames)
   modes_cases.json  the rest of rijndael.h: setup_decrypt, ECB decrypt, CBC, OFB
+  framing_cases.json wire streams through the reference's EncryptedPackageReceiver /
+                    EncryptedStreamReceiver (oracle/_ref/framing_ref): frames, plaintexts, verdicts
   digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5) and
                     per-rank shard digests of the bench workloads (C2 r0-7, C4/C5 at world 1/2/4/8)
 
@@ -158,6 +160,128 @@ def gen_stream_cases(ref: Oracle):
     return cases
 
 
+FRAMING_REF = os.path.join(HERE, "_ref", "framing_ref")
+MAX_DEFAULT = 8 * 1024 * 1024  # FPNN_DEFAULT_MAX_PACKAGE_LEN, core/Config.h:14
+
+
+def fp_message(rng, mtype: int, ss: int, payload: int, magic=b"FPNN", psize=None) -> bytes:
+    """An FPNN TCP message (proto/FPMessage.h:56-63 header; FPQuest/FPAnswer::raw() body
+    order): header, seq (two-way quest / answer), method (quest, ss bytes), payload."""
+    ps = payload if psize is None else psize
+    hdr = magic + bytes([1, 0x80, mtype, ss]) + (ps & 0xFFFFFFFF).to_bytes(4, "little")
+    seq = rng.integers(0, 1 << 32).item().to_bytes(4, "little") if mtype in (1, 2) else b""
+    method = bytes(rng.choice(list(b"abcdefghijklmnopqrstuvwxyz_"), ss).tolist()) if mtype in (0, 1) else b""
+    return hdr + seq + method + rng.bytes(payload)
+
+
+def _valid_messages(rng, n, max_payload):
+    out = []
+    for _ in range(n):
+        mt = int(rng.integers(0, 3))
+        ss = int(rng.integers(1, 40)) if mt != 2 else int(rng.integers(0, 2))
+        out.append(fp_message(rng, mt, ss, int(rng.integers(1, max_payload + 1))))
+    return out
+
+
+def run_framing_ref(mode: str, key: bytes, iv: bytes, max_len: int, piece: int, wire: bytes):
+    """Feed `wire` to the reference receiver (oracle/framing_ref.cpp) -> (events, end)."""
+    import struct
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        cin, cout = os.path.join(d, "case.bin"), os.path.join(d, "out.jsonl")
+        with open(cin, "wb") as f:
+            f.write(b"FRG1" + struct.pack("<II", 0 if mode == "package" else 1, len(key)) + key + iv
+                    + struct.pack("<iIQ", max_len, piece, len(wire)) + wire)
+        subprocess.run([FRAMING_REF, cin, cout], check=True, timeout=120, stdout=subprocess.DEVNULL)
+        with open(cout) as f:
+            lines = [json.loads(x) for x in f]
+    assert lines and "end" in lines[-1], lines
+    return lines[:-1], lines[-1]
+
+
+def gen_framing_cases(ref: Oracle):
+    """Wire streams run through the reference's own EncryptedPackageReceiver /
+    EncryptedStreamReceiver (core/EncryptedPackageReceiver.cpp:60-150,
+    core/EncryptedStreamReceiver.cpp:72-163, with proto/FPMessage.cpp:27-44 BodyLen) over a
+    socketpair: every complete frame, the plaintext the receiver decoded (FPQuest/FPAnswer
+    raw()), and its verdict at the end of the data.  Each wire is fed in three piece sizes
+    and must give identical events (arrival chunking does not change framing)."""
+    rng = np.random.default_rng(20261017)
+    cases = []
+
+    def add(name, mode, kl, max_len, wire_fn, expect):
+        key, iv = rng.bytes(kl), rng.bytes(16)
+        wire = wire_fn(key, iv)
+        runs = [run_framing_ref(mode, key, iv, max_len, p, wire) for p in (1, 7, 65536)]
+        for r in runs[1:]:
+            assert r[0] == runs[0][0] and r[1]["end"] == runs[0][1]["end"], name
+        ev, end = runs[-1]
+        cases.append({"name": name, "mode": mode, "key": hx(key), "iv": hx(iv), "max_len": max_len,
+                      "wire": hx(wire), "frames": ev, "end": end, "expect": expect})
+        print(f"  framing {name}: {len(ev)} frames, end {end}")
+
+    def pkg(msgs, tail=b""):
+        def wire(key, iv):
+            w = b"".join(len(m).to_bytes(4, "little") + ref.package(key, iv, True, m) for m in msgs)
+            return w + (tail(key, iv) if callable(tail) else tail)
+        return wire
+
+    def stream(msgs):
+        return lambda key, iv: ref.cfb(key, True, b"".join(msgs), iv, 0)[0]
+
+    # ---- package mode: [htole32(n)][n bytes of PackageEncryptor::encrypt] ----
+    add("pkg_valid_aes256", "package", 32, MAX_DEFAULT, pkg(_valid_messages(rng, 24, 900)), "ok")
+    add("pkg_valid_aes128", "package", 16, MAX_DEFAULT, pkg(_valid_messages(rng, 16, 300)), "ok")
+    m = _valid_messages(rng, 6, 400)
+    last = _valid_messages(rng, 1, 500)[0]
+    add("pkg_partial_body", "package", 32, MAX_DEFAULT,
+        pkg(m, lambda key, iv: len(last).to_bytes(4, "little") + ref.package(key, iv, True, last)[:len(last) // 2]),
+        "ok")
+    add("pkg_partial_prefix", "package", 16, MAX_DEFAULT, pkg(_valid_messages(rng, 5, 200), b"\x10\x02"), "ok")
+    add("pkg_only_prefix", "package", 32, MAX_DEFAULT, pkg([], (777).to_bytes(4, "little")), "ok")
+    cap_msg = fp_message(rng, 1, 8, 4096 - 12 - 4 - 8)  # exactly max_len bytes
+    add("pkg_cap_boundary", "package", 32, 4096,
+        pkg(_valid_messages(rng, 3, 300) + [cap_msg], (4097).to_bytes(4, "little") + rng.bytes(64)), "too_large")
+    add("pkg_default_cap", "package", 16, MAX_DEFAULT,
+        pkg(_valid_messages(rng, 4, 300), (MAX_DEFAULT + 1).to_bytes(4, "little") + rng.bytes(32)), "too_large")
+    add("pkg_huge_prefix", "package", 32, MAX_DEFAULT,
+        pkg(_valid_messages(rng, 2, 100), b"\xff\xff\xff\xff"), "too_large")
+    garbage = [rng.bytes(int(rng.integers(1, 700))) for _ in range(10)]  # bodies that decode to nothing
+    add("pkg_undecodable_bodies", "package", 32, MAX_DEFAULT, pkg(garbage), "ok")
+
+    # ---- stream mode: one CFB stream over concatenated FPNN messages ----
+    add("stream_valid_aes256", "stream", 32, MAX_DEFAULT, stream(_valid_messages(rng, 24, 900)), "ok")
+    add("stream_valid_aes128", "stream", 16, MAX_DEFAULT, stream(_valid_messages(rng, 16, 300)), "ok")
+    m = _valid_messages(rng, 6, 400)
+    part = _valid_messages(rng, 1, 600)[0]
+    add("stream_partial_body", "stream", 32, MAX_DEFAULT, stream(m + [part[:len(part) // 2]]), "ok")
+    add("stream_partial_header", "stream", 16, MAX_DEFAULT, stream(_valid_messages(rng, 4, 200) + [part[:7]]), "ok")
+    add("stream_bad_magic", "stream", 32, MAX_DEFAULT,
+        stream(_valid_messages(rng, 3, 200) + [fp_message(rng, 1, 4, 30, magic=b"FPNX")]), "bad_magic")
+    add("stream_http_magic", "stream", 16, MAX_DEFAULT,
+        stream(_valid_messages(rng, 2, 200) + [b"POST / HTTP/1.1\r\n\r\n"]), "bad_magic")
+    add("stream_bad_mtype", "stream", 32, MAX_DEFAULT,
+        stream(_valid_messages(rng, 2, 200) + [b"FPNN" + bytes([1, 0x80, 3, 0]) + bytes(20)]), "bad_mtype")
+    add("stream_zero_bodylen", "stream", 16, MAX_DEFAULT,
+        stream(_valid_messages(rng, 2, 100) + [b"FPNN" + bytes([1, 0x80, 0, 0]) + bytes(4) + bytes(8)]),
+        "bad_length")
+    add("stream_wrapping_bodylen", "stream", 32, MAX_DEFAULT,
+        stream(_valid_messages(rng, 2, 100) + [fp_message(rng, 2, 0, 3, psize=0xFFFFFFF8)]), "bad_length")
+    add("stream_uint32_wrap", "stream", 16, MAX_DEFAULT,  # BodyLen = 0xFFFFFFFF + 4 wraps to 3
+        stream(_valid_messages(rng, 2, 100) + [fp_message(rng, 2, 0, 0, psize=0xFFFFFFFF)[:15]]
+               + _valid_messages(rng, 2, 100)), "ok")
+    add("stream_negative_int", "stream", 16, MAX_DEFAULT,
+        stream(_valid_messages(rng, 1, 100) + [fp_message(rng, 0, 0, 3, psize=0x80000000)]), "bad_length")
+    cap = fp_message(rng, 2, 0, 4096 - 12 - 4)  # exactly max_len bytes
+    add("stream_cap_boundary", "stream", 32, 4096,
+        stream(_valid_messages(rng, 3, 300) + [cap, fp_message(rng, 2, 0, 4096 - 12 - 4 + 1)]), "too_large")
+    add("stream_default_cap", "stream", 16, MAX_DEFAULT,
+        stream(_valid_messages(rng, 2, 300) + [fp_message(rng, 1, 5, 40, psize=MAX_DEFAULT)]), "too_large")
+    return {"source": "reference receivers run by oracle/_ref/framing_ref (make -C oracle framing), "
+                      "fed over a socketpair in 1-, 7- and 65536-byte pieces", "cases": cases}
+
+
 def ref_buf(b):
     import ctypes as C
     return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8))
@@ -278,6 +402,7 @@ def main():
     ap.add_argument("--shards-only", action="store_true",
                     help="only (re)compute the per-rank shard digests into digests.json")
     ap.add_argument("--modes-only", action="store_true", help="only (re)write modes_cases.json")
+    ap.add_argument("--framing-only", action="store_true", help="only (re)write framing_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -291,6 +416,9 @@ def main():
     if args.modes_only:
         dump("modes_cases.json", gen_modes_cases(ref))
         return
+    if args.framing_only:
+        dump("framing_cases.json", gen_framing_cases(ref))
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -302,6 +430,7 @@ def main():
     dump("package_cases.json", gen_package_cases(ref))
     dump("stream_cases.json", gen_stream_cases(ref))
     dump("modes_cases.json", gen_modes_cases(ref))
+    dump("framing_cases.json", gen_framing_cases(ref))
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

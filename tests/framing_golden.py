@@ -1,0 +1,39 @@
+"""Expected scan results of the reference-generated framing fixtures
+(tests/golden/framing_cases.json, made by oracle/gen_golden.py with oracle/_ref/framing_ref,
+i.e. the reference's own EncryptedPackageReceiver / EncryptedStreamReceiver).
+
+The receivers report every complete frame with its length (Receiver::_total) and the
+plaintext they decoded, then a verdict at the end of the data: "incomplete" (the rest is a
+partial frame kept for the next read), "closed" (recvPackage returned false: the frame is
+above Config::_max_recv_package_length, or the stream header is not an FPNN message /
+has length <= 0) or "exception" (FPMessage::BodyLen threw on an unknown mtype).  These map
+onto the fpnn_aes_frame_scan of the batch receive calls."""
+import json
+import os
+
+SCAN_OK, SCAN_FULL, SCAN_TOO_LARGE, SCAN_BAD_MAGIC, SCAN_BAD_MTYPE, SCAN_BAD_LENGTH = range(6)
+_EXPECT = {"ok": SCAN_OK, "too_large": SCAN_TOO_LARGE, "bad_magic": SCAN_BAD_MAGIC, "bad_mtype": SCAN_BAD_MTYPE,
+           "bad_length": SCAN_BAD_LENGTH}
+_VERDICT = {"ok": "incomplete", "too_large": "closed", "bad_magic": "closed", "bad_length": "closed",
+            "bad_mtype": "exception"}
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_cases():
+    with open(os.path.join(HERE, "golden", "framing_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+def expected(case):
+    """-> ([(offset, length)], status, consumed, [raw plaintext or None]) for one case.
+    Package mode: offset of the body (after its 4-byte prefix) within the wire;
+    stream mode: offset of the message within the plaintext stream."""
+    assert case["end"]["end"] == _VERDICT[case["expect"]], case["name"]  # generator intent == reference verdict
+    pre = 4 if case["mode"] == "package" else 0
+    frames, raws, at = [], [], 0
+    for ev in case["frames"]:
+        frames.append((at + pre, ev["total"]))
+        raws.append(bytes.fromhex(ev["raw"]) if ev["fetch"] else None)
+        at += pre + ev["total"]
+    return frames, _EXPECT[case["expect"]], at, raws

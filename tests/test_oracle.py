@@ -161,6 +161,31 @@ def test_framing_restatement_known_answers():
     assert P.scan_stream(msg(0, 0, 100, 100), 112, 8) == ([(0, 112)], P.SCAN_OK, 112)
 
 
+def test_framing_restatement_vs_reference_receivers(oracle):
+    """The framing restatement (ao_scan_package / ao_scan_stream) against the reference's
+    own receivers (tests/golden/framing_cases.json, oracle/_ref/framing_ref): the same
+    frames, verdicts and consumed bytes, and the oracle's decryption of each frame equals
+    the plaintext the reference receiver decoded."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as P
+    from framing_golden import expected, load_cases
+    cases = load_cases()
+    assert {c["expect"] for c in cases} == {"ok", "too_large", "bad_magic", "bad_mtype", "bad_length"}
+    for c in cases:
+        key, iv, wire = bytes.fromhex(c["key"]), bytes.fromhex(c["iv"]), bytes.fromhex(c["wire"])
+        frames, status, consumed, raws = expected(c)
+        if c["mode"] == "package":
+            got = P.scan_package(wire, c["max_len"], 64)
+            plain = [oracle.package(key, iv, False, wire[o:o + n]) for o, n in frames]
+        else:
+            stream = oracle.cfb(key, False, wire, iv, 0)[0]
+            got = P.scan_stream(stream, c["max_len"], 64)
+            plain = [stream[o:o + n] for o, n in frames]
+        assert got == (frames, status, consumed), c["name"]
+        for j, (p, r) in enumerate(zip(plain, raws)):
+            assert r is None or p == r, (c["name"], j)
+
+
 def test_openssl_comparator_matches_oracle(oracle):
     """The bench's OpenSSL EVP cfb128 comparator (oracle/openssl_cfb.c) computes the same
     package-mode bytes as the restatement (so its timing is of the same work)."""
