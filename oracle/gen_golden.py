@@ -12,6 +12,8 @@ container only).  Writes data only -- inputs and the reference's outputs:
   modes_cases.json  the rest of rijndael.h: setup_decrypt, ECB decrypt, CBC, OFB
   framing_cases.json wire streams through the reference's EncryptedPackageReceiver /
                     EncryptedStreamReceiver (oracle/_ref/framing_ref): frames, plaintexts, verdicts
+  ecdh_cases.json   ECCKeyExchange / ECCKeysMaker (core/KeyExchange.cpp + micro-ecc) on the
+                    four curves (oracle/_ref/ecdh_ref): public keys, derived keys and IVs
   digests.json      SHA-256 digests of full-size synthetic config batches (C2, C3, C5) and
                     per-rank shard digests of the bench workloads (C2 r0-7, C4/C5 at world 1/2/4/8)
 
@@ -282,6 +284,87 @@ def gen_framing_cases(ref: Oracle):
                       "fed over a socketpair in 1-, 7- and 65536-byte pieces", "cases": cases}
 
 
+ECDH_REF = os.path.join(HERE, "_ref", "ecdh_ref")
+
+
+def gen_ecdh_cases():
+    """core/KeyExchange.cpp + core/micro-ecc run by oracle/_ref/ecdh_ref: per curve, client
+    key pairs (ECCKeysMaker::publicKey with a chosen private key) and the keys both sides
+    derive (ECCKeysMaker::calcKey / ECCKeyExchange::calcKey), plus edge inputs: degenerate
+    private keys (1 fails in the co-Z ladder), keys >= n, off-curve / zero / non-reduced
+    peer points and wrong lengths."""
+    import subprocess
+    from ecdh_oracle import CURVES
+    rng = np.random.default_rng(20261018)
+    lines, meta = [], []
+
+    def run(reqs):
+        r = subprocess.run([ECDH_REF], input="\n".join(reqs) + "\n", capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+        res = [ln[2:] for ln in r.stdout.splitlines() if ln.startswith("R ")]
+        assert len(res) == len(reqs), (len(res), len(reqs))
+        return res
+
+    def rand_below(top):
+        while True:
+            v = int.from_bytes(rng.bytes((top.bit_length() + 7) // 8), "big") >> (8 - top.bit_length() % 8) % 8
+            if 0 < v < top:
+                return v
+
+    out = {"source": "oracle/_ref/ecdh_ref: the reference's core/KeyExchange.cpp + core/micro-ecc/uECC.c",
+           "curves": []}
+    for name, c in CURVES.items():
+        nb, pb = c.num_bytes, c.private_bytes
+        words = (c.num_n_bits + 63) // 64  # uECC_generate_random_int draws whole 64-bit words (x86-64)
+        server = rand_below(c.n).to_bytes(pb, "big")
+        # the server's public key, as a client of itself would compute it
+        lines.append(f"C {name} {int.from_bytes(server, 'big').to_bytes(8 * words, 'little').hex()} - 16")
+        meta.append(("server_pub",))
+        privs = [rand_below(c.n) for _ in range(10)] + [2, c.n - 1, c.n - 2, (c.n - 1) // 2]
+        for j, k in enumerate(privs):
+            lines.append(f"C {name} {k.to_bytes(8 * words, 'little').hex()} SERVERPUB {(16, 32)[j % 2]}")
+            meta.append(("client", k, (16, 32)[j % 2]))
+        ent = {"curve": name, "server_private": server.hex(), "clients": [], "server": []}
+        out["curves"].append(ent)
+        # resolve the server public key first
+        server_pub = run(lines[:1])[0].split()[0]
+        ent["server_public"] = server_pub
+        req = [ln.replace("SERVERPUB", server_pub) for ln in lines[1:]]
+        res = run(req)
+        for (_, k, kl), r in zip(meta[1:], res):
+            pub, priv, ok, key, iv = r.split()
+            ent["clients"].append({"private": priv, "public": pub, "keylen": kl, "ok": int(ok),
+                                   "key": "" if key == "-" else key, "iv": "" if iv == "-" else iv})
+        lines, meta = [], []
+        # server side: every client's public key, then edge inputs
+        peers = [(cl["public"], cl["keylen"]) for cl in ent["clients"]]
+        p = c.p
+        offc = (rng.bytes(2 * nb).hex(), 32)
+        nonreduced = (p + 1).to_bytes(nb, "big").hex() + ent["clients"][0]["public"][2 * nb:]  # x = p + 1
+        peers += [offc, ("00" * (2 * nb), 16), (nonreduced, 32),
+                  (ent["clients"][1]["public"][:-2], 32),              # one byte short
+                  (ent["clients"][2]["public"], 24)]                   # unsupported keylen
+        for peer, kl in peers:
+            lines.append(f"S {name} {server.hex()} {peer} {kl}")
+        extra = [((1).to_bytes(pb, "big"), ent["clients"][3]["public"], 32),
+                 ((c.n).to_bytes(pb, "big") if c.n < 1 << (8 * pb) else b"\xff" * pb, ent["clients"][4]["public"], 32),
+                 (b"\xff" * pb, ent["clients"][5]["public"], 16),
+                 (server[:-1], ent["clients"][6]["public"], 32)]        # private key one byte short
+        for priv, peer, kl in extra:
+            lines.append(f"S {name} {priv.hex() if priv else '-'} {peer} {kl}")
+        res = run(lines)
+        privs_used = [server.hex()] * len(peers) + [e[0].hex() for e in extra]
+        reqs = peers + [(e[1], e[2]) for e in extra]
+        for (peer, kl), priv, r in zip(reqs, privs_used, res):
+            init_ok, ok, key, iv = r.split()
+            ent["server"].append({"private": priv, "peer": peer, "keylen": kl, "init_ok": int(init_ok),
+                                  "ok": int(ok), "key": "" if key == "-" else key, "iv": "" if iv == "-" else iv})
+        lines, meta = [], []
+        print(f"  ecdh {name}: {len(ent['clients'])} clients, {len(ent['server'])} server calls, "
+              f"{sum(s['ok'] for s in ent['server'])} ok")
+    return out
+
+
 def ref_buf(b):
     import ctypes as C
     return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8))
@@ -403,6 +486,7 @@ def main():
                     help="only (re)compute the per-rank shard digests into digests.json")
     ap.add_argument("--modes-only", action="store_true", help="only (re)write modes_cases.json")
     ap.add_argument("--framing-only", action="store_true", help="only (re)write framing_cases.json")
+    ap.add_argument("--ecdh-only", action="store_true", help="only (re)write ecdh_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -419,6 +503,9 @@ def main():
     if args.framing_only:
         dump("framing_cases.json", gen_framing_cases(ref))
         return
+    if args.ecdh_only:
+        dump("ecdh_cases.json", gen_ecdh_cases())
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -431,6 +518,7 @@ def main():
     dump("stream_cases.json", gen_stream_cases(ref))
     dump("modes_cases.json", gen_modes_cases(ref))
     dump("framing_cases.json", gen_framing_cases(ref))
+    dump("ecdh_cases.json", gen_ecdh_cases())
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

@@ -5,6 +5,7 @@
 2. Golden fixtures produced by the compiled reference (oracle/gen_golden.py).
 3. Live randomized comparison with oracle/_ref when it is built (this container).
 """
+import json
 import os
 import sys
 
@@ -232,3 +233,28 @@ def test_golden_modes_cases(oracle, golden):
     # FIPS-197 C.1 / C.3 inverse cipher
     assert g["ecb_decrypt"][0]["out"] == "00112233445566778899aabbccddeeff"
     assert g["ecb_decrypt"][1]["out"] == "00112233445566778899aabbccddeeff"
+
+
+def test_ecdh_restatement_vs_reference():
+    """oracle/ecdh_oracle.py against core/KeyExchange.cpp + core/micro-ecc run by
+    oracle/_ref/ecdh_ref (tests/golden/ecdh_cases.json): client public keys, the keys and
+    IVs both sides derive, degenerate scalars and malformed peers on all four curves."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ecdh_oracle as E
+    with open(os.path.join(ROOT, "tests", "golden", "ecdh_cases.json")) as f:
+        g = json.load(f)
+    assert {c["curve"] for c in g["curves"]} == set(E.CURVES)
+    fails = 0
+    for cv in g["curves"]:
+        c = E.CURVES[cv["curve"]]
+        for cl in cv["clients"]:
+            ok, pub = E.public_key(c, bytes.fromhex(cl["private"]))
+            assert ok and pub.hex() == cl["public"], cv["curve"]
+            ok, key, iv = E.calc_key(cv["curve"], bytes.fromhex(cl["private"]), bytes.fromhex(cv["server_public"]),
+                                     cl["keylen"])
+            assert (int(ok), key.hex(), iv.hex()) == (cl["ok"], cl["key"], cl["iv"]), cv["curve"]
+        for s in cv["server"]:
+            ok, key, iv = E.calc_key(cv["curve"], bytes.fromhex(s["private"]), bytes.fromhex(s["peer"]), s["keylen"])
+            assert (int(ok), key.hex(), iv.hex()) == (s["ok"], s["key"], s["iv"]), (cv["curve"], s)
+            fails += 1 - s["ok"]
+    assert fails >= 4 * 5  # zero point, short peer, bad keylen, private 1, short private per curve
