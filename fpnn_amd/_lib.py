@@ -112,6 +112,19 @@ SIGNATURES = {
     "fpnn_aes_engine_kernel_stats": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "fpnn_aes_engine_reset_stats": (C.c_int, [_vp]),
     "fpnn_aes_engine_last_kernel": (C.c_char_p, [_vp, C.c_int]),
+    # fpnn_ecdh.h (include/fpnn_ecdh.h)
+    "fpnn_ecdh_curve": (C.c_int, [C.c_char_p]),
+    "fpnn_ecdh_secret_len": (C.c_int, [C.c_int]),
+    "fpnn_ecdh_private_len": (C.c_int, [C.c_int]),
+    "fpnn_ecdh_calc_keys": (C.c_int, [_vp, C.c_int, C.c_char_p, _vp, C.c_uint32, C.c_int, _vp, _vp, _vp]),
+    "fpnn_ecdh_calc_keys_client": (C.c_int, [_vp, C.c_int, _vp, C.c_char_p, C.c_uint32, C.c_int, _vp, _vp, _vp]),
+    "fpnn_ecdh_public_keys": (C.c_int, [_vp, C.c_int, _vp, C.c_uint32, _vp, _vp]),
+    "fpnn_ecdh_keyset": (C.c_int, [_vp, C.c_int, C.c_char_p, _vp, C.c_uint32, C.c_int, _vp, C.POINTER(_vp)]),
+    "fpnn_ecdh_calc_keys_host": (C.c_int, [_vp, C.c_int, C.c_char_p, C.c_char_p, C.c_uint32, C.c_int, _vp, _vp,
+                                           _vp]),
+    "fpnn_ecdh_calc_key_host": (C.c_int, [_vp, C.c_char_p, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int,
+                                          _vp, _vp]),
+    "fpnn_ecdh_public_key_host": (C.c_int, [_vp, C.c_int, C.c_char_p, _vp]),
     # rijndael.h (include/rijndael.h)
     "rijndael_setup_encrypt": (C.c_bool, [C.POINTER(Schedule), _u8p, C.c_size_t]),
     "rijndael_setup_decrypt": (C.c_bool, [C.POINTER(Schedule), _u8p, C.c_size_t]),

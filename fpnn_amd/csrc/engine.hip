@@ -21,6 +21,8 @@
 #include <vector>
 
 #include "../../include/fpnn_aes.h"
+#include "../../include/fpnn_ecdh.h"
+#include "ecc.hpp"
 #include "aes_common.hpp"
 #include "kernels.hpp"
 
@@ -1418,6 +1420,204 @@ int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e) {
     if (!e) return FPNN_AES_ERR_ARG;
     e->ev_used[0] = e->ev_used[1] = 0;
     return FPNN_AES_OK;
+}
+
+}  // extern "C"
+
+// ---- ECDH key derivation (include/fpnn_ecdh.h, k_ecdh.hip) -------------------------------
+namespace {
+
+int ecdh_const(int curve, EccConst &c) {
+    if (!ecc_fill_const(curve, c)) {
+        g_last_error = "unknown ECDH curve";
+        return FPNN_AES_ERR_ARG;
+    }
+    return FPNN_AES_OK;
+}
+
+bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
+
+int ecdh_launch(fpnn_aes_engine *e, int curve, const EccConst &c, const EcdhJob &j) {
+    if (j.count == 0) return FPNN_AES_OK;
+    if (!aligned4(j.priv) || !aligned4(j.pub) || !aligned4(j.key_out) || !aligned4(j.iv_out) ||
+        !aligned4(j.pub_out)) {
+        g_last_error = "ECDH device buffers must be 4-byte aligned";
+        return FPNN_AES_ERR_ARG;
+    }
+    DeviceGuard g(e->device);
+    HIP_TRY(launch_ecdh(c, j, curve, e->stream));
+    return FPNN_AES_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fpnn_ecdh_curve(const char *name) {
+    if (!name) return -1;
+    for (int i = 0; i < ECC_NCURVES; i++)
+        if (strcmp(name, ecc_curve_info(i).name) == 0) return i;
+    return -1;
+}
+
+int fpnn_ecdh_secret_len(int curve) {
+    return curve >= 0 && curve < ECC_NCURVES ? ecc_curve_info(curve).num_bytes : -1;
+}
+
+int fpnn_ecdh_private_len(int curve) {
+    return curve >= 0 && curve < ECC_NCURVES ? (ecc_curve_info(curve).num_n_bits + 7) / 8 : -1;
+}
+
+int fpnn_ecdh_calc_keys(fpnn_aes_engine *e, int curve, const uint8_t *private_key, const uint8_t *peer_public,
+                        uint32_t count, int keylen, uint8_t *keys, uint8_t *ivs, uint8_t *ok) {
+    if (!e || !private_key || (count && (!peer_public || !keys || !ivs || !ok))) return FPNN_AES_ERR_ARG;
+    if (keylen != 16 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
+    EccConst c;
+    int rc = ecdh_const(curve, c);
+    if (rc) return rc;
+    ecc_set_uniform_scalar(c, private_key);
+    EcdhJob j{};
+    j.pub = peer_public;
+    j.count = count;
+    j.mode = ECDH_KEYS;
+    j.keylen = keylen;
+    j.key_out = keys;
+    j.iv_out = ivs;
+    j.ok_out = ok;
+    return ecdh_launch(e, curve, c, j);
+}
+
+int fpnn_ecdh_calc_keys_client(fpnn_aes_engine *e, int curve, const uint8_t *private_keys,
+                               const uint8_t *server_public, uint32_t count, int keylen, uint8_t *keys,
+                               uint8_t *ivs, uint8_t *ok) {
+    if (!e || !server_public || (count && (!private_keys || !keys || !ivs || !ok))) return FPNN_AES_ERR_ARG;
+    if (keylen != 16 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
+    EccConst c;
+    int rc = ecdh_const(curve, c);
+    if (rc) return rc;
+    ecc_set_uniform_point(c, server_public);
+    EcdhJob j{};
+    j.priv = private_keys;
+    j.count = count;
+    j.mode = ECDH_KEYS;
+    j.keylen = keylen;
+    j.key_out = keys;
+    j.iv_out = ivs;
+    j.ok_out = ok;
+    return ecdh_launch(e, curve, c, j);
+}
+
+int fpnn_ecdh_public_keys(fpnn_aes_engine *e, int curve, const uint8_t *private_keys, uint32_t count,
+                          uint8_t *public_keys, uint8_t *ok) {
+    if (!e || (count && (!private_keys || !public_keys || !ok))) return FPNN_AES_ERR_ARG;
+    EccConst c;
+    int rc = ecdh_const(curve, c);  // px, py = G
+    if (rc) return rc;
+    EcdhJob j{};
+    j.priv = private_keys;
+    j.count = count;
+    j.mode = ECDH_PUBLIC;
+    j.pub_out = public_keys;
+    j.ok_out = ok;
+    return ecdh_launch(e, curve, c, j);
+}
+
+int fpnn_ecdh_keyset(fpnn_aes_engine *e, int curve, const uint8_t *private_key, const uint8_t *peer_public,
+                     uint32_t count, int keylen, uint8_t *ok, fpnn_aes_keyset **out) {
+    if (!e || !out || count == 0) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    if (keylen != 16 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
+    DeviceGuard g(e->device);
+    uint8_t *tmp = nullptr;  // keys | ivs | ok
+    const size_t kb = (size_t)count * keylen, ib = (size_t)count * 16;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&tmp), kb + ib + count));
+    int rc = fpnn_ecdh_calc_keys(e, curve, private_key, peer_public, count, keylen, tmp, tmp + kb,
+                                 ok ? ok : tmp + kb + ib);
+    if (!rc) rc = fpnn_aes_keyset_create(e, count, (size_t)keylen, tmp, tmp + kb, 0, out);  // synchronizes
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int fpnn_ecdh_calc_keys_host(fpnn_aes_engine *e, int curve, const uint8_t *private_key, const uint8_t *peer_public,
+                             uint32_t count, int keylen, uint8_t *keys, uint8_t *ivs, uint8_t *ok) {
+    if (!e || !private_key || (count && (!peer_public || !keys || !ivs || !ok))) return FPNN_AES_ERR_ARG;
+    if (keylen != 16 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
+    const int sl = fpnn_ecdh_secret_len(curve);
+    if (sl < 0) return FPNN_AES_ERR_ARG;
+    if (count == 0) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    const size_t pb = (size_t)count * 2 * sl, kb = (size_t)count * keylen, ib = (size_t)count * 16;
+    uint8_t *d = nullptr;  // peers | keys | ivs | ok
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), pb + kb + ib + count));
+    int rc = FPNN_AES_OK;
+    do {
+        hipError_t err = hipMemcpyAsync(d, peer_public, pb, hipMemcpyHostToDevice, e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
+        if ((rc = fpnn_ecdh_calc_keys(e, curve, private_key, d, count, keylen, d + pb, d + pb + kb,
+                                      d + pb + kb + ib)))
+            break;
+        err = hipMemcpyAsync(keys, d + pb, kb, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipMemcpyAsync(ivs, d + pb + kb, ib, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipMemcpyAsync(ok, d + pb + kb + ib, count, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
+    } while (0);
+    (void)hipFree(d);
+    return rc;
+}
+
+int fpnn_ecdh_calc_key_host(fpnn_aes_engine *e, const char *curve, const uint8_t *private_key, size_t private_len,
+                            const uint8_t *peer_public, size_t peer_len, int keylen, uint8_t *key, uint8_t *iv) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    // ECCKeyExchange::init + calcKey's own checks, in the reference's order
+    const int cv = fpnn_ecdh_curve(curve);
+    if (cv < 0 || (int)private_len != fpnn_ecdh_private_len(cv) || !private_key) return 0;
+    if ((int)peer_len != 2 * fpnn_ecdh_secret_len(cv) || !peer_public) return 0;
+    if (keylen != 16 && keylen != 32) return 0;
+    if (!key || !iv) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    uint8_t *d = nullptr;  // peer (<= 64) | key (32) | iv (16) | ok
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), 64 + 32 + 16 + 16));
+    int rc = FPNN_AES_OK;
+    uint8_t res[32 + 16 + 1];
+    do {
+        hipError_t err = hipMemcpyAsync(d, peer_public, peer_len, hipMemcpyHostToDevice, e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
+        if ((rc = fpnn_ecdh_calc_keys(e, cv, private_key, d, 1, keylen, d + 64, d + 96, d + 112))) break;
+        err = hipMemcpyAsync(res, d + 64, sizeof res, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
+    } while (0);
+    (void)hipFree(d);
+    if (rc) return rc;
+    if (!res[48]) return 0;
+    memcpy(key, res, (size_t)keylen);
+    memcpy(iv, res + 32, 16);
+    return 1;
+}
+
+int fpnn_ecdh_public_key_host(fpnn_aes_engine *e, int curve, const uint8_t *private_key, uint8_t *public_key) {
+    if (!e || !private_key || !public_key) return FPNN_AES_ERR_ARG;
+    const int pl = fpnn_ecdh_private_len(curve), sl = fpnn_ecdh_secret_len(curve);
+    if (pl < 0) return FPNN_AES_ERR_ARG;
+    DeviceGuard g(e->device);
+    uint8_t *d = nullptr;  // private (<= 32) | public (<= 64) | ok
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), 32 + 64 + 16));
+    int rc = FPNN_AES_OK;
+    uint8_t res[64 + 1];
+    do {
+        hipError_t err = hipMemcpyAsync(d, private_key, (size_t)pl, hipMemcpyHostToDevice, e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
+        if ((rc = fpnn_ecdh_public_keys(e, curve, d, 1, d + 32, d + 96))) break;
+        err = hipMemcpyAsync(res, d + 32, 64, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipMemcpyAsync(res + 64, d + 96, 1, hipMemcpyDeviceToHost, e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
+    } while (0);
+    (void)hipFree(d);
+    if (rc) return rc;
+    memcpy(public_key, res, (size_t)(2 * sl));
+    return res[64] ? 1 : 0;
 }
 
 }  // extern "C"

@@ -1,0 +1,652 @@
+// k_ecdh.hip -- batched ECDH key derivation on the device (§8f row 4).
+//
+// Reference: ECCKeyExchange::calcKey (core/KeyExchange.cpp:87-127) over the vendored
+// micro-ecc: uECC_shared_secret (core/micro-ecc/uECC.c:1034-1077) = co-Z Montgomery ladder
+// (uECC.c:857-900; Rivain, eprint 2011/338) on the regularized scalar (uECC.c:902-913),
+// then key = secret[0:16] | secret[0:32] | sha256(secret), iv = md5(secret).  The public
+// half of uECC_make_key (EccPoint_compute_public_key, uECC.c:915-933) is the same ladder
+// from G.  One lane per connection; field arithmetic in ecc.hpp's Montgomery form.
+#include <string.h>
+
+#include "ecc.hpp"
+
+namespace fpnn_aes {
+
+namespace {
+
+template <int NW>
+struct Fe {
+    uint32_t v[NW];
+};
+
+// t[0..NW] (t < 2p) -> t mod p
+template <int NW>
+__device__ __forceinline__ Fe<NW> reduce_once(const uint32_t *t, uint32_t top, const EccConst &c) {
+    Fe<NW> d;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint64_t s = (uint64_t)t[j] - c.p[j] - borrow;
+        d.v[j] = (uint32_t)s;
+        borrow = (uint32_t)(s >> 63);
+    }
+    const bool use_d = top != 0 || borrow == 0;
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < NW; j++) r.v[j] = use_d ? d.v[j] : t[j];
+    return r;
+}
+
+// Montgomery product a*b/R mod p (CIOS; a, b < p)
+template <int NW>
+__device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
+    uint32_t t[NW + 2];
+#pragma unroll
+    for (int j = 0; j < NW + 2; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + carry;
+            t[j] = (uint32_t)s;
+            carry = (uint32_t)(s >> 32);
+        }
+        uint64_t s = (uint64_t)t[NW] + carry;
+        t[NW] = (uint32_t)s;
+        t[NW + 1] = (uint32_t)(s >> 32);
+        const uint32_t m = t[0] * c.n0inv;
+        s = (uint64_t)m * c.p[0] + t[0];
+        carry = (uint32_t)(s >> 32);
+#pragma unroll
+        for (int j = 1; j < NW; j++) {
+            s = (uint64_t)m * c.p[j] + t[j] + carry;
+            t[j - 1] = (uint32_t)s;
+            carry = (uint32_t)(s >> 32);
+        }
+        s = (uint64_t)t[NW] + carry;
+        t[NW - 1] = (uint32_t)s;
+        t[NW] = t[NW + 1] + (uint32_t)(s >> 32);
+    }
+    return reduce_once<NW>(t, t[NW], c);
+}
+
+template <int NW>
+__device__ __forceinline__ Fe<NW> fsqr(const Fe<NW> &a, const EccConst &c) {
+    return fmul<NW>(a, a, c);
+}
+
+template <int NW>
+__device__ __forceinline__ Fe<NW> fadd(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
+    uint32_t t[NW];
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint64_t s = (uint64_t)a.v[j] + b.v[j] + carry;
+        t[j] = (uint32_t)s;
+        carry = (uint32_t)(s >> 32);
+    }
+    return reduce_once<NW>(t, carry, c);
+}
+
+template <int NW>
+__device__ __forceinline__ Fe<NW> fsub(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
+    Fe<NW> d, r;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint64_t s = (uint64_t)a.v[j] - b.v[j] - borrow;
+        d.v[j] = (uint32_t)s;
+        borrow = (uint32_t)(s >> 63);
+    }
+    const uint32_t mask = 0u - borrow;  // a < b: add p back
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint64_t s = (uint64_t)d.v[j] + (c.p[j] & mask) + carry;
+        r.v[j] = (uint32_t)s;
+        carry = (uint32_t)(s >> 32);
+    }
+    return r;
+}
+
+// a/2 mod p: (a + p)/2 when a is odd (curve-specific.inc:76-82 / 1130-1136)
+template <int NW>
+__device__ __forceinline__ Fe<NW> fhalf(const Fe<NW> &a, const EccConst &c) {
+    const uint32_t mask = 0u - (a.v[0] & 1u);
+    uint32_t t[NW];
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint64_t s = (uint64_t)a.v[j] + (c.p[j] & mask) + carry;
+        t[j] = (uint32_t)s;
+        carry = (uint32_t)(s >> 32);
+    }
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < NW - 1; j++) r.v[j] = (t[j] >> 1) | (t[j + 1] << 31);
+    r.v[NW - 1] = (t[NW - 1] >> 1) | (carry << 31);
+    return r;
+}
+
+template <int NW>
+__device__ __forceinline__ Fe<NW> fsel(bool s, const Fe<NW> &a, const Fe<NW> &b) {
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < NW; j++) r.v[j] = s ? a.v[j] : b.v[j];
+    return r;
+}
+
+template <int NW>
+__device__ __forceinline__ Fe<NW> fconst(const uint32_t *k) {
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < NW; j++) r.v[j] = k[j];
+    return r;
+}
+
+// a^(p-2) = 1/a (0 -> 0, as uECC_vli_modInv); the exponent is public: uniform branches
+template <int NW>
+__device__ Fe<NW> finv(const Fe<NW> &a, const EccConst &c) {
+    Fe<NW> r = fconst<NW>(c.r1);
+    for (int w = NW - 1; w >= 0; w--) {
+        const uint32_t e = c.pm2[w];
+        for (int b = 31; b >= 0; b--) {
+            r = fsqr<NW>(r, c);
+            if ((e >> b) & 1u) r = fmul<NW>(r, a, c);
+        }
+    }
+    return r;
+}
+
+// double_jacobian (curve-specific.inc:50-95 a = -3; :1110-1141 secp256k1, a = 0), z != 0
+template <int NW, bool AM3>
+__device__ __forceinline__ void dbl_jacobian(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &Z1, const EccConst &c) {
+    if (AM3) {
+        Fe<NW> t4 = fsqr<NW>(Y1, c);
+        Fe<NW> t5 = fmul<NW>(X1, t4, c);
+        t4 = fsqr<NW>(t4, c);
+        Y1 = fmul<NW>(Y1, Z1, c);
+        Z1 = fsqr<NW>(Z1, c);
+        X1 = fadd<NW>(X1, Z1, c);
+        Z1 = fadd<NW>(Z1, Z1, c);
+        Z1 = fsub<NW>(X1, Z1, c);
+        X1 = fmul<NW>(X1, Z1, c);
+        Z1 = fadd<NW>(X1, X1, c);
+        X1 = fadd<NW>(X1, Z1, c);
+        X1 = fhalf<NW>(X1, c);
+        Z1 = fsqr<NW>(X1, c);
+        Z1 = fsub<NW>(Z1, t5, c);
+        Z1 = fsub<NW>(Z1, t5, c);
+        t5 = fsub<NW>(t5, Z1, c);
+        X1 = fmul<NW>(X1, t5, c);
+        t4 = fsub<NW>(X1, t4, c);
+        X1 = Z1;
+        Z1 = Y1;
+        Y1 = t4;
+    } else {
+        Fe<NW> t5 = fsqr<NW>(Y1, c);
+        Fe<NW> t4 = fmul<NW>(X1, t5, c);
+        X1 = fsqr<NW>(X1, c);
+        t5 = fsqr<NW>(t5, c);
+        Z1 = fmul<NW>(Y1, Z1, c);
+        Y1 = fadd<NW>(X1, X1, c);
+        Y1 = fadd<NW>(Y1, X1, c);
+        Y1 = fhalf<NW>(Y1, c);
+        X1 = fsqr<NW>(Y1, c);
+        X1 = fsub<NW>(X1, t4, c);
+        X1 = fsub<NW>(X1, t4, c);
+        t4 = fsub<NW>(t4, X1, c);
+        Y1 = fmul<NW>(Y1, t4, c);
+        Y1 = fsub<NW>(Y1, t5, c);
+    }
+}
+
+// (x, y) -> (x z^2, y z^3)  (uECC.c:748-758)
+template <int NW>
+__device__ __forceinline__ void apply_z(Fe<NW> &X, Fe<NW> &Y, const Fe<NW> &Z, const EccConst &c) {
+    Fe<NW> t = fsqr<NW>(Z, c);
+    X = fmul<NW>(X, t, c);
+    t = fmul<NW>(t, Z, c);
+    Y = fmul<NW>(Y, t, c);
+}
+
+// XYcZ_add (uECC.c:788-813): (P, Q) co-Z -> P into P', Q into P + Q
+template <int NW>
+__device__ __forceinline__ void xycz_add(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
+    Fe<NW> t5 = fsub<NW>(X2, X1, c);
+    t5 = fsqr<NW>(t5, c);
+    X1 = fmul<NW>(X1, t5, c);
+    X2 = fmul<NW>(X2, t5, c);
+    Y2 = fsub<NW>(Y2, Y1, c);
+    t5 = fsqr<NW>(Y2, c);
+    t5 = fsub<NW>(t5, X1, c);
+    t5 = fsub<NW>(t5, X2, c);
+    X2 = fsub<NW>(X2, X1, c);
+    Y1 = fmul<NW>(Y1, X2, c);
+    X2 = fsub<NW>(X1, t5, c);
+    Y2 = fmul<NW>(Y2, X2, c);
+    Y2 = fsub<NW>(Y2, Y1, c);
+    X2 = t5;
+}
+
+// XYcZ_addC (uECC.c:819-854): (P, Q) co-Z -> P into P - Q, Q into P + Q
+template <int NW>
+__device__ __forceinline__ void xycz_addc(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
+    Fe<NW> t5 = fsub<NW>(X2, X1, c);
+    t5 = fsqr<NW>(t5, c);
+    X1 = fmul<NW>(X1, t5, c);
+    X2 = fmul<NW>(X2, t5, c);
+    t5 = fadd<NW>(Y2, Y1, c);
+    Y2 = fsub<NW>(Y2, Y1, c);
+    Fe<NW> t6 = fsub<NW>(X2, X1, c);
+    Y1 = fmul<NW>(Y1, t6, c);
+    t6 = fadd<NW>(X1, X2, c);
+    X2 = fsqr<NW>(Y2, c);
+    X2 = fsub<NW>(X2, t6, c);
+    Fe<NW> t7 = fsub<NW>(X1, X2, c);
+    Y2 = fmul<NW>(Y2, t7, c);
+    Y2 = fsub<NW>(Y2, Y1, c);
+    t7 = fsqr<NW>(t5, c);
+    t7 = fsub<NW>(t7, t6, c);
+    t6 = fsub<NW>(t7, X1, c);
+    t6 = fmul<NW>(t6, t5, c);
+    Y1 = fsub<NW>(t6, Y1, c);
+    X1 = t7;
+}
+
+template <int NW>
+__device__ __forceinline__ void cswap(bool s, Fe<NW> &a, Fe<NW> &b) {
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint32_t x = (a.v[j] ^ b.v[j]) & (0u - (uint32_t)s);
+        a.v[j] ^= x;
+        b.v[j] ^= x;
+    }
+}
+
+// EccPoint_mult (uECC.c:857-900): P (Montgomery form), scalar of nbits bits (top bit 1)
+// -> affine result (Montgomery form).  Registers (A, B) hold (R[bit], R[!bit]) of the
+// step; `sw` records whether they currently hold (R0, R1) so that swaps happen only
+// when consecutive bits differ.
+template <int NW, bool AM3>
+__device__ void ladder(Fe<NW> &rx, Fe<NW> &ry, const Fe<NW> &xp, const Fe<NW> &yp, const uint32_t *s, int nbits,
+                       const EccConst &c) {
+    Fe<NW> ax = xp, ay = yp;  // R1
+    Fe<NW> bx = xp, by = yp;  // R0
+    Fe<NW> z = fconst<NW>(c.r1);
+    dbl_jacobian<NW, AM3>(ax, ay, z, c);  // XYcZ_initial_double: R1 = 2P, R0 = P co-Z
+    apply_z<NW>(bx, by, z, c);
+    bool sw = false;  // (A, B) == (R1, R0)
+    uint32_t word = 0;
+    for (int i = nbits - 2; i >= 0; --i) {
+        if (i == nbits - 2 || (i & 31) == 31) {
+            word = s[0];
+#pragma unroll
+            for (int j = 1; j <= NW; j++) word = (i >> 5) == j ? s[j] : word;
+        }
+        const bool bit = (word >> (i & 31)) & 1u;
+        const bool want = !bit;  // A must be R[bit]: R0 when the bit is 0
+        cswap<NW>(want != sw, ax, bx);
+        cswap<NW>(want != sw, ay, by);
+        sw = want;
+        xycz_addc<NW>(ax, ay, bx, by, c);  // R[bit] - R[!bit], R[bit] + R[!bit]
+        if (i == 0) break;
+        xycz_add<NW>(bx, by, ax, ay, c);
+    }
+    // 1/Z = yP * Xb / (xP * Yb * (X1 - X0)), b = bit 0 (A holds R[b])
+    const Fe<NW> x1 = fsel<NW>(sw, bx, ax), x0 = fsel<NW>(sw, ax, bx);
+    Fe<NW> zi = fsub<NW>(x1, x0, c);
+    zi = fmul<NW>(zi, ay, c);
+    zi = fmul<NW>(zi, xp, c);
+    zi = finv<NW>(zi, c);
+    zi = fmul<NW>(zi, yp, c);
+    zi = fmul<NW>(zi, ax, c);
+    xycz_add<NW>(bx, by, ax, ay, c);
+    rx = fsel<NW>(sw, ax, bx);  // R0
+    ry = fsel<NW>(sw, ay, by);
+    apply_z<NW>(rx, ry, zi, c);
+}
+
+// big-endian bytes (4-byte aligned, nbytes = 4*NW) -> limbs
+template <int NW>
+__device__ __forceinline__ Fe<NW> load_be(const uint8_t *p) {
+    Fe<NW> r;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+    for (int j = 0; j < NW; j++) r.v[j] = __builtin_bswap32(w[NW - 1 - j]);
+    return r;
+}
+
+template <int NW>
+__device__ __forceinline__ void store_be(uint8_t *p, const Fe<NW> &a) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(p);
+#pragma unroll
+    for (int j = 0; j < NW; j++) w[NW - 1 - j] = __builtin_bswap32(a.v[j]);
+}
+
+// ---- MD5 (RFC 1321) and SHA-256 (FIPS 180-4) of one short message (< 56 bytes) ----
+__constant__ uint32_t kMd5K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// msg: nw32 words as they sit in memory (little-endian loads of the bytes), 4*nw32 bytes
+__device__ void md5_short(const uint32_t *mem, int nw32, uint32_t out[4]) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = 0;
+    for (int i = 0; i < nw32; i++) m[i] = mem[i];
+    m[nw32] = 0x80u;
+    m[14] = (uint32_t)(nw32 * 32);
+    uint32_t a = 0x67452301, b = 0xefcdab89, c = 0x98badcfe, d = 0x10325476;
+    const int sh[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t f;
+        int g;
+        if (i < 16) {
+            f = (b & c) | (~b & d);
+            g = i;
+        } else if (i < 32) {
+            f = (d & b) | (~d & c);
+            g = (5 * i + 1) & 15;
+        } else if (i < 48) {
+            f = b ^ c ^ d;
+            g = (3 * i + 5) & 15;
+        } else {
+            f = c ^ (b | ~d);
+            g = (7 * i) & 15;
+        }
+        const uint32_t t = d;
+        d = c;
+        c = b;
+        b = b + rotl(a + f + kMd5K[i] + m[g], sh[i >> 4][i & 3]);
+        a = t;
+    }
+    out[0] = 0x67452301 + a;
+    out[1] = 0xefcdab89 + b;
+    out[2] = 0x98badcfe + c;
+    out[3] = 0x10325476 + d;  // little-endian words = digest bytes in order
+}
+
+__device__ void sha256_short(const uint32_t *mem, int nw32, uint32_t out[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = 0;
+    for (int i = 0; i < nw32; i++) w[i] = __builtin_bswap32(mem[i]);  // big-endian message words
+    w[nw32] = 0x80000000u;
+    w[15] = (uint32_t)(nw32 * 32);
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            wi = w[i & 15] = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+        }
+        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t t1 = hh + S1 + ch + kSha256K[i] + wi;
+        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        const uint32_t t2 = S0 + mj;
+        hh = g;
+        g = f;
+        f = e;
+        e = d + t1;
+        d = c;
+        c = b;
+        b = a;
+        a = t1 + t2;
+    }
+    out[0] = h[0] + a;
+    out[1] = h[1] + b;
+    out[2] = h[2] + c;
+    out[3] = h[3] + d;
+    out[4] = h[4] + e;
+    out[5] = h[5] + f;
+    out[6] = h[6] + g;
+    out[7] = h[7] + hh;  // big-endian words of the digest
+}
+
+template <int NW, bool AM3>
+__global__ __launch_bounds__(256) void k_ecdh(EccConst c, EcdhJob j) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= j.count) return;  // lanes never exchange data: an early exit is safe
+    // the point (reduced once: every coordinate < 2^(32*NW) < 2p), to Montgomery form
+    Fe<NW> x, y;
+    if (j.pub) {
+        x = load_be<NW>(j.pub + (size_t)i * 8 * NW);
+        y = load_be<NW>(j.pub + (size_t)i * 8 * NW + 4 * NW);
+    } else {
+        x = fconst<NW>(c.px);
+        y = fconst<NW>(c.py);
+    }
+    x = reduce_once<NW>(x.v, 0, c);
+    y = reduce_once<NW>(y.v, 0, c);
+    const Fe<NW> r2 = fconst<NW>(c.r2);
+    const Fe<NW> xp = fmul<NW>(x, r2, c), yp = fmul<NW>(y, r2, c);
+    // the scalar: regularize_k (uECC.c:902-913) -> k + n if that reaches 2^num_n_bits, else k + 2n
+    uint32_t s[NW + 1];
+    if (j.priv) {
+        const Fe<NW> k = load_be<NW>(j.priv + (size_t)i * 4 * NW);
+        uint32_t k0[NW + 1], k1[NW + 1], carry = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint64_t t = (uint64_t)k.v[w] + c.n[w] + carry;
+            k0[w] = (uint32_t)t;
+            carry = (uint32_t)(t >> 32);
+        }
+        k0[NW] = carry;
+        carry = 0;
+#pragma unroll
+        for (int w = 0; w <= NW; w++) {
+            const uint64_t t = (uint64_t)k0[w] + (w < NW ? c.n[w] : 0u) + carry;
+            k1[w] = (uint32_t)t;
+            carry = (uint32_t)(t >> 32);
+        }
+        const bool hi = k0[NW] & 1u;  // bit num_n_bits: num_n_bits == 32 * NW on all four curves
+#pragma unroll
+        for (int w = 0; w <= NW; w++) s[w] = hi ? k0[w] : k1[w];
+    } else {
+#pragma unroll
+        for (int w = 0; w <= NW; w++) s[w] = c.k[w];
+    }
+    Fe<NW> rx, ry;
+    ladder<NW, AM3>(rx, ry, xp, yp, s, c.num_n_bits + 1, c);
+    Fe<NW> one;
+#pragma unroll
+    for (int w = 0; w < NW; w++) one.v[w] = w == 0;
+    rx = fmul<NW>(rx, one, c);  // out of Montgomery form
+    ry = fmul<NW>(ry, one, c);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) nz |= rx.v[w] | ry.v[w];
+    j.ok_out[i] = nz != 0;
+    if (j.mode == ECDH_PUBLIC) {
+        store_be<NW>(j.pub_out + (size_t)i * 8 * NW, rx);
+        store_be<NW>(j.pub_out + (size_t)i * 8 * NW + 4 * NW, ry);
+        return;
+    }
+    // secret = x, big-endian; key / iv as ECCKeyExchange::calcKey
+    uint32_t sec[NW];  // the secret bytes as little-endian words (memory order)
+#pragma unroll
+    for (int w = 0; w < NW; w++) sec[w] = __builtin_bswap32(rx.v[NW - 1 - w]);
+    uint32_t iv[4];
+    md5_short(sec, NW, iv);
+    uint32_t *ivo = reinterpret_cast<uint32_t *>(j.iv_out + (size_t)i * 16);
+#pragma unroll
+    for (int w = 0; w < 4; w++) ivo[w] = iv[w];
+    uint32_t *ko = reinterpret_cast<uint32_t *>(j.key_out + (size_t)i * j.keylen);
+    if (j.keylen == 16 || NW == 8) {
+        for (int w = 0; w < j.keylen / 4; w++) ko[w] = sec[w];
+    } else {
+        uint32_t h[8];
+        sha256_short(sec, NW, h);
+#pragma unroll
+        for (int w = 0; w < 8; w++) ko[w] = __builtin_bswap32(h[w]);
+    }
+}
+
+// ---- host: curve table -----------------------------------------------------------------
+// SEC 2 v2 domain parameters (big-endian hex).
+struct CurveHex {
+    EccCurveInfo info;
+    const char *p, *n, *gx, *gy;
+};
+const CurveHex kCurves[ECC_NCURVES] = {
+    {{"secp256k1", 8, 32, 256, false},
+     "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFC2F",
+     "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141",
+     "79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798",
+     "483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8"},
+    {{"secp256r1", 8, 32, 256, true},
+     "FFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF",
+     "FFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551",
+     "6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296",
+     "4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5"},
+    {{"secp224r1", 7, 28, 224, true},
+     "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFF000000000000000000000001",
+     "FFFFFFFFFFFFFFFFFFFFFFFFFFFF16A2E0B8F03E13DD29455C5C2A3D",
+     "B70E0CBD6BB4BF7F321390B94A03C1D356C21122343280D6115C1D21",
+     "BD376388B5F723FB4C22DFE6CD4375A05A07476444D5819985007E34"},
+    {{"secp192r1", 6, 24, 192, true},
+     "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFFFFFFFFFFFF",
+     "FFFFFFFFFFFFFFFFFFFFFFFF99DEF836146BC9B1B4D22831",
+     "188DA80EB03090F67CBF20EB43A18800F4FF0AFD82FF1012",
+     "07192B95FFC8DA78631011ED6B24CDD573F977A11E794811"},
+};
+
+void hex_limbs(const char *h, uint32_t out[8]) {
+    memset(out, 0, 8 * sizeof(uint32_t));
+    const int n = (int)strlen(h);
+    for (int i = 0; i < n; i++) {
+        const char ch = h[n - 1 - i];
+        const uint32_t d = ch <= '9' ? (uint32_t)(ch - '0') : (uint32_t)((ch | 0x20) - 'a' + 10);
+        out[i / 8] |= d << (4 * (i % 8));
+    }
+}
+
+// r = 2r mod p over nw limbs (r < p)
+void dbl_mod(uint32_t *r, const uint32_t *p, int nw) {
+    uint32_t t[9], carry = 0;
+    for (int j = 0; j < nw; j++) {
+        const uint64_t s = ((uint64_t)r[j] << 1) | carry;
+        t[j] = (uint32_t)s;
+        carry = (uint32_t)(s >> 32);
+    }
+    uint32_t d[8], borrow = 0;
+    for (int j = 0; j < nw; j++) {
+        const uint64_t s = (uint64_t)t[j] - p[j] - borrow;
+        d[j] = (uint32_t)s;
+        borrow = (uint32_t)(s >> 63);
+    }
+    const bool use_d = carry || !borrow;
+    for (int j = 0; j < nw; j++) r[j] = use_d ? d[j] : t[j];
+}
+
+void be_to_limbs(const uint8_t *be, int nbytes, uint32_t *out, int nlimbs) {
+    memset(out, 0, nlimbs * sizeof(uint32_t));
+    for (int i = 0; i < nbytes; i++) out[i / 4] |= (uint32_t)be[nbytes - 1 - i] << (8 * (i % 4));
+}
+
+template <int NW, bool AM3>
+void launch_nw(const EccConst &c, const EcdhJob &j, hipStream_t st) {
+    hipLaunchKernelGGL((k_ecdh<NW, AM3>), dim3((j.count + 255) / 256), dim3(256), 0, st, c, j);
+}
+
+}  // namespace
+
+const EccCurveInfo &ecc_curve_info(int curve) { return kCurves[curve].info; }
+
+bool ecc_fill_const(int curve, EccConst &c) {
+    if (curve < 0 || curve >= ECC_NCURVES) return false;
+    const CurveHex &h = kCurves[curve];
+    memset(&c, 0, sizeof c);
+    const int nw = h.info.nw;
+    c.nw = nw;
+    c.num_bytes = h.info.num_bytes;
+    c.num_n_bits = h.info.num_n_bits;
+    c.private_bytes = (h.info.num_n_bits + 7) / 8;
+    if (c.num_n_bits != 32 * nw || c.num_bytes != 4 * nw) return false;  // the kernel relies on both
+    hex_limbs(h.p, c.p);
+    hex_limbs(h.n, c.n);
+    hex_limbs(h.gx, c.px);
+    hex_limbs(h.gy, c.py);
+    uint32_t borrow = 2;  // pm2 = p - 2 (secp224r1's low limb is 1: the borrow runs on)
+    for (int j = 0; j < 8; j++) {
+        const uint64_t s = (uint64_t)c.p[j] - borrow;
+        c.pm2[j] = (uint32_t)s;
+        borrow = (uint32_t)(s >> 63);
+    }
+    uint32_t inv = 1;  // p^-1 mod 2^32 by Newton iteration
+    for (int i = 0; i < 5; i++) inv *= 2u - c.p[0] * inv;
+    c.n0inv = 0u - inv;
+    uint32_t r[8] = {1};
+    for (int i = 0; i < 32 * nw; i++) dbl_mod(r, c.p, nw);  // R mod p
+    memcpy(c.r1, r, sizeof r);
+    for (int i = 0; i < 32 * nw; i++) dbl_mod(r, c.p, nw);  // R^2 mod p
+    memcpy(c.r2, r, sizeof r);
+    return true;
+}
+
+void ecc_set_uniform_scalar(EccConst &c, const uint8_t *priv_be) {
+    uint32_t k[9];
+    be_to_limbs(priv_be, c.private_bytes, k, 9);
+    uint32_t k0[9], k1[9], carry = 0;
+    for (int w = 0; w < 9; w++) {
+        const uint64_t t = (uint64_t)k[w] + (w < 8 ? c.n[w] : 0u) + carry;
+        k0[w] = (uint32_t)t;
+        carry = (uint32_t)(t >> 32);
+    }
+    carry = 0;
+    for (int w = 0; w < 9; w++) {
+        const uint64_t t = (uint64_t)k0[w] + (w < 8 ? c.n[w] : 0u) + carry;
+        k1[w] = (uint32_t)t;
+        carry = (uint32_t)(t >> 32);
+    }
+    const bool hi = (k0[c.num_n_bits >> 5] >> (c.num_n_bits & 31)) & 1u;
+    memcpy(c.k, hi ? k0 : k1, sizeof c.k);
+}
+
+void ecc_set_uniform_point(EccConst &c, const uint8_t *pub_be) {
+    be_to_limbs(pub_be, c.num_bytes, c.px, 8);
+    be_to_limbs(pub_be + c.num_bytes, c.num_bytes, c.py, 8);
+}
+
+hipError_t launch_ecdh(const EccConst &c, const EcdhJob &j, int curve, hipStream_t st) {
+    if (j.count == 0) return hipSuccess;
+    switch (curve) {
+        case ECC_SECP256K1: launch_nw<8, false>(c, j, st); break;
+        case ECC_SECP256R1: launch_nw<8, true>(c, j, st); break;
+        case ECC_SECP224R1: launch_nw<7, true>(c, j, st); break;
+        case ECC_SECP192R1: launch_nw<6, true>(c, j, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace fpnn_aes

@@ -1,0 +1,141 @@
+// keyexchange.cpp -- fpnn::ECCKeyExchange / ECCKeysMaker (include/KeyExchange.h) over the
+// GPU ECDH of include/fpnn_ecdh.h.  Mirrors core/KeyExchange.cpp:49-187 check for check;
+// the scalar multiplications and hashes run in k_ecdh.hip.
+#include <errno.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <string>
+
+#include "../../include/Encryptor.h"
+#include "../../include/KeyExchange.h"
+#include "../../include/fpnn_ecdh.h"
+#include "ecc.hpp"
+#include "thread_engine.hpp"
+
+namespace {
+
+fpnn_aes_engine *engine_or_throw() {
+    int rc;
+    fpnn_aes_engine *e = fpnn_aes::thread_engine(&rc);
+    if (!e) throw fpnn::EncryptorError(std::string("fpnn_aes ECDH: no GPU engine: ") + fpnn_aes_strerror(rc));
+    return e;
+}
+
+void throw_if_error(int rc, const char *what) {
+    if (rc < 0) {
+        std::string m = std::string("fpnn_aes ECDH ") + what + ": " + fpnn_aes_strerror(rc);
+        const char *d = fpnn_aes_last_error();
+        if (d && *d) m += std::string(" (") + d + ")";
+        throw fpnn::EncryptorError(m);
+    }
+}
+
+const char *curve_name(int curve) { return fpnn_aes::ecc_curve_info(curve).name; }
+
+// uECC_generate_random_int (core/micro-ecc/uECC.c:980-1002): 0 < k < n, drawn with the
+// top word masked to n's bit length; big-endian private_len bytes out.
+bool random_below_n(int curve, uint8_t *out) {
+    fpnn_aes::EccConst c;
+    if (!fpnn_aes::ecc_fill_const(curve, c)) return false;
+    const int nw = c.nw, bits = c.num_n_bits;
+    for (int tries = 0; tries < 64; tries++) {
+        uint32_t k[8] = {0};
+        size_t got = 0;
+        while (got < sizeof(uint32_t) * nw) {
+            const ssize_t r = getrandom(reinterpret_cast<uint8_t *>(k) + got, sizeof(uint32_t) * nw - got, 0);
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                return false;
+            }
+            got += (size_t)r;
+        }
+        if (bits < 32 * nw) k[nw - 1] &= 0xFFFFFFFFu >> (32 * nw - bits);
+        bool zero = true, below = false, decided = false;
+        for (int w = nw - 1; w >= 0; w--) {
+            zero = zero && k[w] == 0;
+            if (!decided && k[w] != c.n[w]) {
+                below = k[w] < c.n[w];
+                decided = true;
+            }
+        }
+        if (zero || !below) continue;
+        const int pb = c.private_bytes;
+        for (int i = 0; i < pb; i++) out[i] = (uint8_t)(k[(pb - 1 - i) / 4] >> (8 * ((pb - 1 - i) % 4)));
+        return true;
+    }
+    return false;
+}
+
+}  // namespace
+
+namespace fpnn {
+
+bool ECCKeyExchange::init(const std::string &curve, const std::string &privateKey) {
+    const int cv = fpnn_ecdh_curve(curve.c_str());
+    if (cv < 0) return false;  // "Unsupported ECC curve."
+    _curve = cv;
+    _secertLen = fpnn_ecdh_secret_len(cv);
+    if ((int)privateKey.length() != fpnn_ecdh_private_len(cv)) return false;  // "Private length missmatched."
+    _privateKey = privateKey;
+    return true;
+}
+
+bool ECCKeyExchange::calcKey(uint8_t *key, uint8_t *iv, int keylen, const std::string &peerPublicKey) {
+    if (_curve < 0) return false;  // "ECC Private Key Config ERROR."
+    if ((int)peerPublicKey.length() != _secertLen * 2) return false;
+    const int r = fpnn_ecdh_calc_key_host(engine_or_throw(), curve_name(_curve),
+                                          reinterpret_cast<const uint8_t *>(_privateKey.data()), _privateKey.size(),
+                                          reinterpret_cast<const uint8_t *>(peerPublicKey.data()),
+                                          peerPublicKey.size(), keylen, key, iv);
+    throw_if_error(r, "calcKey");
+    return r == 1;
+}
+
+bool ECCKeyExchange::calcKeys(size_t count, const uint8_t *peerPublicKeys, int keylen, uint8_t *keys, uint8_t *ivs,
+                              uint8_t *ok) {
+    if (_curve < 0 || (keylen != 16 && keylen != 32)) return false;
+    if ((int)_privateKey.size() != fpnn_ecdh_private_len(_curve)) {
+        memset(ok, 0, count);
+        return true;
+    }
+    const int rc = fpnn_ecdh_calc_keys_host(engine_or_throw(), _curve,
+                                            reinterpret_cast<const uint8_t *>(_privateKey.data()), peerPublicKeys,
+                                            (uint32_t)count, keylen, keys, ivs, ok);
+    throw_if_error(rc, "calcKeys");
+    return true;
+}
+
+bool ECCKeysMaker::setCurve(const std::string &curve) {
+    const int cv = fpnn_ecdh_curve(curve.c_str());
+    if (cv < 0) return false;
+    _curve = cv;
+    _secertLen = fpnn_ecdh_secret_len(cv);
+    _publicKey.clear();
+    _privateKey.clear();
+    return true;
+}
+
+std::string ECCKeysMaker::publicKey(bool reGen) {
+    if (_curve < 0) return std::string();  // "ECC Private Key Config ERROR."
+    if (_publicKey.empty() || reGen) {
+        // uECC_make_key (core/micro-ecc/uECC.c:1004-1032): up to 64 draws of a private key
+        // whose public key is not the point at infinity
+        fpnn_aes_engine *e = engine_or_throw();
+        uint8_t priv[32], pub[64];
+        for (int tries = 0; tries < 64; tries++) {
+            if (!random_below_n(_curve, priv)) return std::string();  // "Gen public key & private key failed."
+            const int r = fpnn_ecdh_public_key_host(e, _curve, priv, pub);
+            throw_if_error(r, "publicKey");
+            if (r == 1) {
+                _publicKey.assign(reinterpret_cast<char *>(pub), _secertLen * 2);
+                _privateKey.assign(reinterpret_cast<char *>(priv), _secertLen);
+                return _publicKey;
+            }
+        }
+        return std::string();
+    }
+    return _publicKey;
+}
+
+}  // namespace fpnn

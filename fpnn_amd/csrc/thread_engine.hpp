@@ -1,0 +1,30 @@
+// thread_engine.hpp -- the per-thread engine behind the reference-shaped C++ classes
+// (Encryptor, EncryptorBatch, ECCKeyExchange).  Internal; not installed.
+#pragma once
+
+#include <stdlib.h>
+
+#include "../../include/fpnn_aes.h"
+
+namespace fpnn_aes {
+
+// One engine (HIP stream + pinned staging) per calling thread: an Encryptor is used
+// by one thread at a time (core/IOBuffer.h:49-62, core/IOBuffer.cpp:219-245), and
+// may migrate between IO and worker threads, which then use their own engines.
+struct ThreadEngine {
+    fpnn_aes_engine *e = nullptr;
+    int status = FPNN_AES_OK;
+    ThreadEngine() {
+        const char *dev = getenv("FPNN_AES_DEVICE");
+        status = fpnn_aes_engine_create(dev ? atoi(dev) : 0, FPNN_AES_OWN_STREAM, &e);
+    }
+    ~ThreadEngine() { fpnn_aes_engine_destroy(e); }
+};
+
+inline fpnn_aes_engine *thread_engine(int *status) {
+    thread_local ThreadEngine te;
+    *status = te.status;
+    return te.e;
+}
+
+}  // namespace fpnn_aes

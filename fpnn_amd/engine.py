@@ -259,6 +259,66 @@ class Engine:
                                        max_frames, _ptr(off), _ptr(ln), _ptr(scan)), "stream_recv")
         return off, ln, scan
 
+    # -- ECDH key derivation (include/fpnn_ecdh.h) -------------------------------------------
+    @staticmethod
+    def ecdh_curve(name: str) -> int:
+        cv = lib.fpnn_ecdh_curve(name.encode())
+        if cv < 0:
+            raise ValueError(f"unsupported ECC curve {name!r}")
+        return cv
+
+    def ecdh_calc_keys(self, curve: str, private_key: bytes, peer_public: torch.Tensor, keylen: int):
+        """Server side, many peers (ECCKeyExchange::calcKey per connection) -> device
+        tensors (keys [n, keylen], ivs [n, 16], ok [n] uint8).  Queued, no host wait."""
+        cv = self.ecdh_curve(curve)
+        n = peer_public.numel() // (2 * lib.fpnn_ecdh_secret_len(cv))
+        keys = torch.empty((n, keylen), dtype=torch.uint8, device=peer_public.device)
+        ivs = torch.empty((n, 16), dtype=torch.uint8, device=peer_public.device)
+        ok = torch.empty(n, dtype=torch.uint8, device=peer_public.device)
+        check(lib.fpnn_ecdh_calc_keys(self._h, cv, bytes(private_key), _ptr(peer_public), n, keylen, _ptr(keys),
+                                      _ptr(ivs), _ptr(ok)), "ecdh_calc_keys")
+        return keys, ivs, ok
+
+    def ecdh_calc_keys_client(self, curve: str, private_keys: torch.Tensor, server_public: bytes, keylen: int):
+        """Client side (ECCKeysMaker::calcKey) for many clients of one server."""
+        cv = self.ecdh_curve(curve)
+        n = private_keys.numel() // lib.fpnn_ecdh_private_len(cv)
+        keys = torch.empty((n, keylen), dtype=torch.uint8, device=private_keys.device)
+        ivs = torch.empty((n, 16), dtype=torch.uint8, device=private_keys.device)
+        ok = torch.empty(n, dtype=torch.uint8, device=private_keys.device)
+        check(lib.fpnn_ecdh_calc_keys_client(self._h, cv, _ptr(private_keys), bytes(server_public), n, keylen,
+                                             _ptr(keys), _ptr(ivs), _ptr(ok)), "ecdh_calc_keys_client")
+        return keys, ivs, ok
+
+    def ecdh_public_keys(self, curve: str, private_keys: torch.Tensor):
+        """Public keys (x || y) of many private keys -> (public [n, 2*secret_len], ok [n])."""
+        cv = self.ecdh_curve(curve)
+        n = private_keys.numel() // lib.fpnn_ecdh_private_len(cv)
+        pub = torch.empty((n, 2 * lib.fpnn_ecdh_secret_len(cv)), dtype=torch.uint8, device=private_keys.device)
+        ok = torch.empty(n, dtype=torch.uint8, device=private_keys.device)
+        check(lib.fpnn_ecdh_public_keys(self._h, cv, _ptr(private_keys), n, _ptr(pub), _ptr(ok)),
+              "ecdh_public_keys")
+        return pub, ok
+
+    def ecdh_keyset(self, curve: str, private_key: bytes, peer_public: torch.Tensor, keylen: int):
+        """Derive every connection's (key, iv) and expand them into a KeySet -> (KeySet, ok)."""
+        cv = self.ecdh_curve(curve)
+        n = peer_public.numel() // (2 * lib.fpnn_ecdh_secret_len(cv))
+        ok = torch.empty(n, dtype=torch.uint8, device=peer_public.device)
+        h = C.c_void_p()
+        check(lib.fpnn_ecdh_keyset(self._h, cv, bytes(private_key), _ptr(peer_public), n, keylen, _ptr(ok),
+                                   C.byref(h)), "ecdh_keyset")
+        return KeySet.adopt(self, h, n, keylen), ok
+
+    def ecdh_calc_key_host(self, curve: str, private_key: bytes, peer_public: bytes, keylen: int):
+        """One connection, exactly ECCKeyExchange::init + calcKey -> (ok, key, iv)."""
+        key, iv = C.create_string_buffer(32), C.create_string_buffer(16)
+        r = lib.fpnn_ecdh_calc_key_host(self._h, curve.encode(), bytes(private_key), len(private_key),
+                                        bytes(peer_public), len(peer_public), keylen, key, iv)
+        if r < 0:
+            check(r, "ecdh_calc_key_host")
+        return (True, key.raw[:keylen], iv.raw) if r == 1 else (False, b"", b"")
+
     # -- batches ----------------------------------------------------------------------------
     def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,
               key_slot=None, flags=0) -> BatchDesc:
@@ -318,6 +378,15 @@ class KeySet:
         self.count = count
         self.keylen = keylen
         self.engine = engine
+
+    @classmethod
+    def adopt(cls, engine: Engine, h, count: int, keylen: int) -> "KeySet":
+        """Wrap a key set the library created (e.g. fpnn_ecdh_keyset)."""
+        ks = cls.__new__(cls)
+        ks._h = h
+        _live_keysets.add(ks)
+        ks.count, ks.keylen, ks.engine = count, keylen, engine
+        return ks
 
     @property
     def handle(self):

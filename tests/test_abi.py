@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = ["fpnn_aes.h", "rijndael.h"]
+HEADERS = ["fpnn_aes.h", "rijndael.h", "fpnn_ecdh.h"]
 
 
 def declared_functions():
