@@ -37,38 +37,58 @@ __device__ __forceinline__ Fe<NW> reduce_once(const uint32_t *t, uint32_t top, c
     return r;
 }
 
-// Montgomery product a*b/R mod p (CIOS; a, b < p)
+// (hi:lo) += x * y with the carry out of the 64-bit accumulate into hi: one v_mad_u64_u32
+// (its carry-out operand) and one v_addc per product.  Written out because the compiler
+// otherwise rebuilds the carry with a 64-bit compare and select (4-5 instructions).
+__device__ __forceinline__ void mac(uint64_t &lo, uint32_t &hi, uint32_t x, uint32_t y) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "+v"(lo), "+v"(hi)
+        : "v"(x), "v"(y)
+        : "vcc");
+}
+// the same with a wave-uniform second factor (the modulus limbs, SGPRs)
+__device__ __forceinline__ void mac_s(uint64_t &lo, uint32_t &hi, uint32_t x, uint32_t ys) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+        : "+v"(lo), "+v"(hi)
+        : "v"(x), "s"(ys)
+        : "vcc");
+}
+
+// Montgomery product a*b/R mod p (a, b < p), product scanning with the reduction
+// interleaved column by column (Koc, Acar, Kaliski: "FIPS"): every one of the 2*NW^2
+// partial products goes into one 96-bit column accumulator, two VALU instructions each.
+// (Splitting the a*b and m*p products over two accumulators for more ILP measured 12 %
+// slower: the kernel is VALU-issue-bound, not latency-bound.)
 template <int NW>
 __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
-    uint32_t t[NW + 2];
-#pragma unroll
-    for (int j = 0; j < NW + 2; j++) t[j] = 0;
+    uint32_t m[NW], r[NW];
+    uint64_t lo = 0;
+    uint32_t hi = 0;
 #pragma unroll
     for (int i = 0; i < NW; i++) {
-        uint32_t carry = 0;
 #pragma unroll
-        for (int j = 0; j < NW; j++) {
-            const uint64_t s = (uint64_t)a.v[j] * b.v[i] + t[j] + carry;
-            t[j] = (uint32_t)s;
-            carry = (uint32_t)(s >> 32);
+        for (int j = 0; j < i; j++) {
+            mac(lo, hi, a.v[j], b.v[i - j]);
+            mac_s(lo, hi, m[j], c.p[i - j]);
         }
-        uint64_t s = (uint64_t)t[NW] + carry;
-        t[NW] = (uint32_t)s;
-        t[NW + 1] = (uint32_t)(s >> 32);
-        const uint32_t m = t[0] * c.n0inv;
-        s = (uint64_t)m * c.p[0] + t[0];
-        carry = (uint32_t)(s >> 32);
-#pragma unroll
-        for (int j = 1; j < NW; j++) {
-            s = (uint64_t)m * c.p[j] + t[j] + carry;
-            t[j - 1] = (uint32_t)s;
-            carry = (uint32_t)(s >> 32);
-        }
-        s = (uint64_t)t[NW] + carry;
-        t[NW - 1] = (uint32_t)s;
-        t[NW] = t[NW + 1] + (uint32_t)(s >> 32);
+        mac(lo, hi, a.v[i], b.v[0]);
+        m[i] = (uint32_t)lo * c.n0inv;
+        mac_s(lo, hi, m[i], c.p[0]);  // the column's low word becomes 0
+        lo = (lo >> 32) | ((uint64_t)hi << 32);
+        hi = 0;
     }
-    return reduce_once<NW>(t, t[NW], c);
+#pragma unroll
+    for (int i = NW; i < 2 * NW; i++) {
+#pragma unroll
+        for (int j = i - NW + 1; j < NW; j++) {
+            mac(lo, hi, a.v[j], b.v[i - j]);
+            mac_s(lo, hi, m[j], c.p[i - j]);
+        }
+        r[i - NW] = (uint32_t)lo;
+        lo = (lo >> 32) | ((uint64_t)hi << 32);
+        hi = 0;
+    }
+    return reduce_once<NW>(r, (uint32_t)lo, c);  // < 2p
 }
 
 template <int NW>

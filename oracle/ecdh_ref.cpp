@@ -12,6 +12,8 @@
 // stdin, one request per line (hex without spaces):
 //   S <curve> <server_private> <peer_public> <keylen>   ECCKeyExchange::init + calcKey
 //       -> "R <init_ok> <calc_ok> <key> <iv>"   (FPLog writes its records to stdout too)
+//   T <curve> <server_private> <peer_public> <reps>     time `reps` calcKey calls (CPU baseline)
+//       -> "R <seconds> <calc_ok>"
 //   C <curve> <rng_bytes> <server_public> <keylen>      ECCKeysMaker: setCurve, publicKey
 //       (private key drawn from rng_bytes), setPeerPublicKey, calcKey
 //       -> "R <public> <private> <calc_ok> <key> <iv>"
@@ -20,6 +22,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <iostream>
 #include <string>
 #include <vector>
@@ -85,6 +88,15 @@ int main() {
             const bool ok = init_ok && ex.calcKey(key, iv, keylen, unhex(b));
             printf("R %d %d %s %s\n", init_ok ? 1 : 0, ok ? 1 : 0, hex(key, ok ? keylen : 0).c_str(),
                    hex(iv, ok ? 16 : 0).c_str());
+        } else if (op == "T") {
+            ECCKeyExchange ex;
+            ex.init(curve, unhex(a));
+            const std::string peer = unhex(b);
+            const auto t0 = std::chrono::steady_clock::now();
+            bool ok = true;
+            for (int r = 0; r < keylen; r++) ok = ex.calcKey(key, iv, 32, peer) && ok;
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            printf("R %.6f %d\n", dt, ok ? 1 : 0);
         } else if (op == "C") {
             const std::string q = unhex(a);
             g_queue.assign(q.begin(), q.end());

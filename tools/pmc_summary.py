@@ -20,7 +20,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"fpnn_aes::(\w+)(<[^>]*>)?", name)
+    m = re.search(r"fpnn_aes::(?:\(anonymous namespace\)::)?(k_\w+)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")).replace(" ", "") if m else name
 
 

@@ -18,12 +18,17 @@ run() {  # run <dir> <name> <timeout> <cmd...>
 for cfg in $CFGS; do
   OUT=gpurun_out/prof/$TAG/$cfg
   mkdir -p "$OUT"
-  run "$OUT" trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 tools/bench_configs.py --configs $cfg --no-host --reps 3
+  if [ "$cfg" = ECDH ]; then  # tools/bench_ecdh.py: the device ECDH derivation (k_ecdh)
+    CMD="python3 tools/bench_ecdh.py --curves secp256k1 --no-cpu --reps 3"; RX='k_ecdh'
+  else
+    CMD="python3 tools/bench_configs.py --configs $cfg --no-host --reps 3"; RX='cfb_'
+  fi
+  run "$OUT" trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $CMD
   i=0
   IFS="|" read -ra PGROUPS <<< "$PASSES"
   for g in "${PGROUPS[@]}"; do
     i=$((i+1))
-    run "$OUT" "pmc$i" 300 rocprofv3 --kernel-trace --pmc ${g//,/ } --kernel-include-regex 'cfb_' --output-format csv -d "$OUT/pmc$i" -o run -- python3 tools/bench_configs.py --configs $cfg --no-host --reps 2
+    run "$OUT" "pmc$i" 300 rocprofv3 --kernel-trace --pmc ${g//,/ } --kernel-include-regex "$RX" --output-format csv -d "$OUT/pmc$i" -o run -- $CMD
   done
 done
 echo done
