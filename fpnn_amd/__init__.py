@@ -7,7 +7,8 @@ include/Encryptor.h, and this thin Python host layer.
 """
 from ._lib import (LIB_PATH, FpnnAesError, Schedule, build, check, lib, OK, ERR_ARG, ERR_HIP, ERR_KEYLEN, ERR_NODEV,
                    ERR_RANGE, F_WIRE_PREFIX, K_DECRYPT, K_ENCRYPT)
-from .engine import Engine, KeySet, PackageEncryptor, StreamEncryptor, device_count, setup_decrypt, setup_encrypt
+from .engine import (Engine, KeySet, PackageEncryptor, StreamEncryptor, device_count, package_host_multi, setup_decrypt,
+                     setup_encrypt, stream_host_multi)
 
 __all__ = [
     "LIB_PATH", "FpnnAesError", "Schedule", "build", "check", "lib", "Engine", "KeySet", "PackageEncryptor",

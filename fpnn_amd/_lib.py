@@ -94,6 +94,9 @@ SIGNATURES = {
     "fpnn_aes_keyset_create": (C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int, C.POINTER(_vp)]),
     "fpnn_aes_keyset_from_schedules": (C.c_int, [_vp, C.c_uint32, C.POINTER(Schedule), _vp, C.POINTER(_vp)]),
     "fpnn_aes_keyset_destroy": (C.c_int, [_vp]),
+    "fpnn_aes_keyset_reserve": (C.c_int, [_vp, C.c_uint32, C.c_int, C.POINTER(_vp)]),
+    "fpnn_aes_keyset_set": (C.c_int, [_vp, C.c_uint32, C.c_uint32, C.POINTER(Schedule), _vp]),
+    "fpnn_aes_keyset_count": (C.c_uint32, [_vp]),
     "fpnn_aes_keyset_nrounds": (C.c_int, [_vp]),
     "fpnn_aes_keyset_get_schedule": (C.c_int, [_vp, C.c_uint32, C.POINTER(Schedule)]),
     "fpnn_aes_package_encrypt": (C.c_int, [_vp, C.POINTER(BatchDesc)]),
@@ -104,6 +107,10 @@ SIGNATURES = {
                                     C.POINTER(C.c_size_t)]),
     "fpnn_aes_package_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, C.c_uint32]),
     "fpnn_aes_stream_host": (C.c_int, [_vp, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp, _vp, _vp]),
+    "fpnn_aes_package_host_multi": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(HostFrame), C.c_uint32,
+                                              C.c_uint32]),
+    "fpnn_aes_stream_host_multi": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp,
+                                             _vp]),
     "fpnn_aes_package_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), C.c_uint32, C.c_uint32, _vp, _vp, _vp]),
     "fpnn_aes_stream_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
                                        _vp]),

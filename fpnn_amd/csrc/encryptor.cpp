@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -184,16 +185,39 @@ void EncryptorBatch::decrypt(Encryptor *enc, uint8_t *dest, uint8_t *src, int le
     add(enc, false, dest, src, len, nullptr);
 }
 
-namespace {
-
-struct KeySetGuard {
+// Persistent per-key-length table: slot per Encryptor serial, uploaded once
+// (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
+// like the table, so a flush never touches more than its own connections.
+struct EncryptorBatch::KeyTable {
+    fpnn_aes_engine *e = nullptr;
     fpnn_aes_keyset *ks = nullptr;
-    ~KeySetGuard() {
+    std::unordered_map<uint64_t, uint32_t> slot;
+    uint32_t next = 0;
+    std::vector<uint8_t> iv;
+    std::vector<uint32_t> pos;
+    ~KeyTable() {
         if (ks) fpnn_aes_keyset_destroy(ks);
     }
 };
 
+namespace {
+
+// A table past this many slots starts over (slots of dead connections are not tracked).
+constexpr uint32_t kTableMaxSlots = 1u << 20;
+
 }  // namespace
+
+EncryptorBatch::~EncryptorBatch() {
+    for (KeyTable *&t : _tables) {
+        delete t;
+        t = nullptr;
+    }
+}
+
+uint64_t encryptor_serial() {
+    static std::atomic<uint64_t> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
 
 void EncryptorBatch::flush() {
     std::vector<Op> ops;
@@ -231,31 +255,71 @@ void EncryptorBatch::flush() {
         groups[g].idx.push_back(i);
     }
     for (const Group &gr : groups) {
-        std::unordered_map<const Encryptor *, uint32_t> slot_of;
-        std::vector<fpnn_aes_schedule> scheds;
-        std::vector<uint8_t> ivs;
-        std::vector<const Encryptor *> members;
+        // ---- this key length's table: new connections get slots, uploaded in one copy ----
+        KeyTable *&tp = _tables[(gr.nrounds - 10) / 2];
+        if (tp && tp->e != e) {  // flushed from another thread (engine): start a table there
+            delete tp;
+            tp = nullptr;
+        }
+        if (!tp) {
+            tp = new KeyTable();
+            tp->e = e;
+            rc = fpnn_aes_keyset_reserve(e, 1024, gr.nrounds, &tp->ks);
+            if (rc != FPNN_AES_OK) {
+                delete tp;
+                tp = nullptr;
+                throw EncryptorError("EncryptorBatch: key table: " + describe(rc));
+            }
+        }
+        KeyTable &t = *tp;
+        std::vector<const Encryptor *> members;  // first use in this group, in order
+        std::vector<uint32_t> slots(gr.idx.size());
+        for (int attempt = 0;; attempt++) {
+            std::vector<fpnn_aes_schedule> scheds;
+            std::vector<uint8_t> ivs;
+            const uint32_t first_new = t.next;
+            members.clear();
+            std::unordered_map<uint64_t, bool> seen;
+            for (size_t k = 0; k < gr.idx.size(); k++) {
+                const Encryptor *enc = ops[gr.idx[k]].enc;
+                auto ins = t.slot.emplace(enc->_serial, t.next);
+                if (ins.second) {
+                    const rijndael_context &ctx = gr.stream ? static_cast<const StreamEncryptor *>(enc)->_ctx
+                                                            : static_cast<const PackageEncryptor *>(enc)->_ctx;
+                    scheds.push_back(*reinterpret_cast<const fpnn_aes_schedule *>(&ctx));
+                    ivs.insert(ivs.end(), enc->_iv, enc->_iv + 16);
+                    t.next++;
+                }
+                slots[k] = ins.first->second;
+                if (seen.emplace(enc->_serial, true).second) members.push_back(enc);
+            }
+            if (t.next > kTableMaxSlots && attempt == 0) {  // start over with this group's connections only
+                t.slot.clear();
+                t.next = 0;
+                continue;
+            }
+            rc = fpnn_aes_keyset_set(t.ks, first_new, (uint32_t)scheds.size(), scheds.data(), ivs.data());
+            if (rc != FPNN_AES_OK) {
+                // the slots handed out above were not uploaded: forget the table
+                delete tp;
+                tp = nullptr;
+                throw EncryptorError("EncryptorBatch: key table upload: " + describe(rc));
+            }
+            break;
+        }
         std::vector<fpnn_aes_host_frame> frames(gr.idx.size());
         std::vector<std::string> framed;  // package std::string outputs (len + 4)
         if (gr.prefix) framed.resize(gr.idx.size());
-        for (size_t t = 0; t < gr.idx.size(); t++) {
-            Op &op = ops[gr.idx[t]];
-            auto ins = slot_of.emplace(op.enc, (uint32_t)members.size());
-            if (ins.second) {
-                const rijndael_context &ctx = gr.stream ? static_cast<StreamEncryptor *>(op.enc)->_ctx
-                                                        : static_cast<PackageEncryptor *>(op.enc)->_ctx;
-                scheds.push_back(*reinterpret_cast<const fpnn_aes_schedule *>(&ctx));
-                ivs.insert(ivs.end(), op.enc->_iv, op.enc->_iv + 16);
-                members.push_back(op.enc);
-            }
-            fpnn_aes_host_frame &f = frames[t];
+        for (size_t k = 0; k < gr.idx.size(); k++) {
+            Op &op = ops[gr.idx[k]];
+            fpnn_aes_host_frame &f = frames[k];
             f.len = op.len;
-            f.key_slot = ins.first->second;
+            f.key_slot = slots[k];
             if (op.buffer) {
                 f.src = reinterpret_cast<const uint8_t *>(op.buffer->data());
                 if (gr.prefix) {
-                    framed[t].assign(op.len + sizeof(uint32_t), '\0');
-                    f.dst = reinterpret_cast<uint8_t *>(&framed[t][0]);
+                    framed[k].assign(op.len + sizeof(uint32_t), '\0');
+                    f.dst = reinterpret_cast<uint8_t *>(&framed[k][0]);
                 } else {
                     f.dst = reinterpret_cast<uint8_t *>(&(*op.buffer)[0]);  // in place, same length
                 }
@@ -264,27 +328,32 @@ void EncryptorBatch::flush() {
                 f.dst = op.dest;
             }
         }
-        KeySetGuard ks;
-        rc = fpnn_aes_keyset_from_schedules(e, (uint32_t)members.size(), scheds.data(), ivs.data(), &ks.ks);
-        if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: key set: " + describe(rc));
         if (!gr.stream) {
-            rc = fpnn_aes_package_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), ks.ks,
+            rc = fpnn_aes_package_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                        gr.prefix ? FPNN_AES_F_WIRE_PREFIX : 0);
             if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: package batch: " + describe(rc));
             if (gr.prefix)
-                for (size_t t = 0; t < gr.idx.size(); t++) ops[gr.idx[t]].buffer->swap(framed[t]);
+                for (size_t k = 0; k < gr.idx.size(); k++) ops[gr.idx[k]].buffer->swap(framed[k]);
         } else {
-            std::vector<uint8_t> iv_state(ivs);
-            std::vector<uint32_t> pos_state(members.size());
-            for (size_t m = 0; m < members.size(); m++)
-                pos_state[m] = (uint32_t)static_cast<const StreamEncryptor *>(members[m])->_pos;
-            rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), ks.ks,
-                                      iv_state.data(), pos_state.data());
+            const uint32_t cnt = fpnn_aes_keyset_count(t.ks);
+            if (t.pos.size() < cnt) {
+                t.iv.resize(16 * (size_t)cnt);
+                t.pos.resize(cnt);
+            }
+            for (const Encryptor *m : members) {  // the touched streams' current (iv, pos)
+                const StreamEncryptor *se = static_cast<const StreamEncryptor *>(m);
+                const uint32_t sl = t.slot[m->_serial];
+                memcpy(&t.iv[16 * (size_t)sl], se->_iv, 16);
+                t.pos[sl] = (uint32_t)se->_pos;
+            }
+            rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
+                                      t.iv.data(), t.pos.data());
             if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: stream batch: " + describe(rc));
-            for (size_t m = 0; m < members.size(); m++) {
-                StreamEncryptor *se = const_cast<StreamEncryptor *>(static_cast<const StreamEncryptor *>(members[m]));
-                memcpy(se->_iv, &iv_state[16 * m], 16);
-                se->_pos = pos_state[m];
+            for (const Encryptor *m : members) {
+                StreamEncryptor *se = const_cast<StreamEncryptor *>(static_cast<const StreamEncryptor *>(m));
+                const uint32_t sl = t.slot[m->_serial];
+                memcpy(se->_iv, &t.iv[16 * (size_t)sl], 16);
+                se->_pos = t.pos[sl];
             }
         }
     }

@@ -18,11 +18,13 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fpnn_aes.h"
 #include "../../include/fpnn_ecdh.h"
 #include "ecc.hpp"
+#include "hostcopy.hpp"
 #include "aes_common.hpp"
 #include "kernels.hpp"
 
@@ -129,7 +131,8 @@ public:
             while (p < want && acc >= total * p / want) cut[p++] = i + 1;
         }
         run(want, [&](unsigned q) {
-            for (size_t i = cut[q]; i < cut[q + 1]; i++) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+            for (size_t i = cut[q]; i < cut[q + 1]; i++) copy_streaming(jobs[i].dst, jobs[i].src, jobs[i].n);
+            copy_fence();
         });
     }
 
@@ -201,7 +204,7 @@ struct fpnn_aes_engine {
     uint8_t *d_stage = nullptr;
     uint64_t cap_stage = 0;
     // host-frame pipeline
-    HostSlot hs[2];
+    HostSlot hs[3];  // chunk i on slot i % 3: gather(i) runs beside scatter(i - 2)
     std::unique_ptr<HostPool> pool;  // created on first use
     // instrumentation
     bool timing = false;
@@ -217,6 +220,12 @@ struct fpnn_aes_keyset {
     uint32_t count = 0;
     int nrounds = 0;
     uint32_t keylen = 0;
+    // updatable tables (fpnn_aes_keyset_reserve / _set)
+    uint32_t capacity = 0;
+    DevKey *h_up = nullptr;    // pinned upload staging
+    uint32_t cap_up = 0;       // DevKeys
+    hipEvent_t up_done = nullptr;  // last upload out of h_up
+    bool up_pending = false;
 };
 
 namespace {
@@ -702,13 +711,93 @@ int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpn
 
 int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks) {
     if (!ks) return FPNN_AES_OK;
-    if (ks->d_keys) {  // hipFree waits for outstanding work on the device
-        DeviceGuard g(ks->device);
-        (void)hipFree(ks->d_keys);
+    DeviceGuard g(ks->device);
+    if (ks->up_done) {
+        if (ks->up_pending) (void)hipEventSynchronize(ks->up_done);
+        (void)hipEventDestroy(ks->up_done);
     }
+    if (ks->h_up) (void)hipHostFree(ks->h_up);
+    if (ks->d_keys) (void)hipFree(ks->d_keys);  // hipFree waits for outstanding work on the device
     delete ks;
     return FPNN_AES_OK;
 }
+
+int fpnn_aes_keyset_reserve(fpnn_aes_engine *e, uint32_t capacity, int nrounds, fpnn_aes_keyset **out) {
+    if (!e || !out) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    if (nrounds != 10 && nrounds != 12 && nrounds != 14) return FPNN_AES_ERR_KEYLEN;
+    capacity = std::max<uint32_t>(capacity, 1);
+    DeviceGuard g(e->device);
+    fpnn_aes_keyset *ks = new fpnn_aes_keyset();
+    ks->e = e;
+    ks->device = e->device;
+    ks->nrounds = nrounds;
+    ks->keylen = (uint32_t)(nrounds - 6) * 4;
+    ks->capacity = capacity;
+    hipError_t err = hipMalloc(reinterpret_cast<void **>(&ks->d_keys), sizeof(DevKey) * (size_t)capacity);
+    if (err == hipSuccess) err = hipMemsetAsync(ks->d_keys, 0, sizeof(DevKey) * (size_t)capacity, e->stream);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&ks->up_done, hipEventDisableTiming);
+    if (err != hipSuccess) {
+        const int rc = hip_fail(err, "keyset_reserve");
+        fpnn_aes_keyset_destroy(ks);
+        return rc;
+    }
+    *out = ks;
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_keyset_set(fpnn_aes_keyset *ks, uint32_t first, uint32_t count, const fpnn_aes_schedule *ctx,
+                        const uint8_t *ivs) {
+    if (!ks || !ks->e || (count && !ctx) || !ks->up_done) return FPNN_AES_ERR_ARG;
+    if (count == 0) return FPNN_AES_OK;
+    if ((uint64_t)first + count > 0xffffffffull) return FPNN_AES_ERR_RANGE;
+    for (uint32_t i = 0; i < count; i++)
+        if (ctx[i].nrounds != ks->nrounds) return FPNN_AES_ERR_KEYLEN;
+    fpnn_aes_engine *e = ks->e;
+    DeviceGuard g(ks->device);
+    const uint32_t need = first + count;
+    if (need > ks->capacity) {  // grow, keeping the table (queued after everything before it)
+        uint32_t cap = ks->capacity;
+        while (cap < need) cap = cap > 0x7fffffffu ? need : 2 * cap;
+        DevKey *nk = nullptr;
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&nk), sizeof(DevKey) * (size_t)cap));
+        HIP_TRY(hipMemsetAsync(nk + ks->capacity, 0, sizeof(DevKey) * (size_t)(cap - ks->capacity), e->stream));
+        HIP_TRY(hipMemcpyAsync(nk, ks->d_keys, sizeof(DevKey) * (size_t)ks->capacity, hipMemcpyDeviceToDevice,
+                               e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));  // the old table may still be read by queued kernels
+        (void)hipFree(ks->d_keys);
+        ks->d_keys = nk;
+        ks->capacity = cap;
+    }
+    if (ks->up_pending) {  // the staging still feeds the previous upload
+        HIP_TRY(hipEventSynchronize(ks->up_done));
+        ks->up_pending = false;
+    }
+    if (count > ks->cap_up) {
+        if (ks->h_up) (void)hipHostFree(ks->h_up);
+        ks->h_up = nullptr;
+        ks->cap_up = 0;
+        const uint32_t c = std::max<uint32_t>(count, 256);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ks->h_up), sizeof(DevKey) * (size_t)c, 0));
+        ks->cap_up = c;
+    }
+    for (uint32_t i = 0; i < count; i++) {
+        DevKey &d = ks->h_up[i];
+        memset(&d, 0, sizeof d);
+        for (int k = 0; k < 4 * (ks->nrounds + 1); k++) d.rk[k] = bswap32(ctx[i].rk[k]);
+        d.nrounds = (uint32_t)ks->nrounds;
+        d.keylen = ks->keylen;
+        if (ivs) memcpy(d.iv, ivs + 16 * (size_t)i, 16);
+    }
+    HIP_TRY(hipMemcpyAsync(ks->d_keys + first, ks->h_up, sizeof(DevKey) * (size_t)count, hipMemcpyHostToDevice,
+                           e->stream));
+    HIP_TRY(hipEventRecord(ks->up_done, e->stream));
+    ks->up_pending = true;
+    ks->count = std::max(ks->count, need);
+    return FPNN_AES_OK;
+}
+
+uint32_t fpnn_aes_keyset_count(const fpnn_aes_keyset *ks) { return ks ? ks->count : 0; }
 
 int fpnn_aes_keyset_nrounds(const fpnn_aes_keyset *ks) { return ks ? ks->nrounds : 0; }
 
@@ -1030,6 +1119,17 @@ struct HostStats {
     }
 };
 
+// part p of `parts` of a package chunk's scatter (whole frames, straight from the staged
+// out_off array)
+void scatter_frames_part(const HostSlot &s, unsigned p, unsigned parts) {
+    const uint32_t a = (uint32_t)((uint64_t)s.count * p / parts), b = (uint32_t)((uint64_t)s.count * (p + 1) / parts);
+    for (uint32_t t = a; t < b; t++) {
+        const fpnn_aes_host_frame &f = s.frames[s.first + t];
+        copy_streaming(f.dst, s.h + s.out_at + s.out_off[t], f.len + s.pre);
+    }
+    copy_fence();
+}
+
 // wait for a slot's chunk and scatter its outputs to the callers' buffers
 int slot_drain(fpnn_aes_engine *e, HostSlot &s, HostStats &st) {
     if (!s.busy) return FPNN_AES_OK;
@@ -1039,13 +1139,7 @@ int slot_drain(fpnn_aes_engine *e, HostSlot &s, HostStats &st) {
     const double t1 = st.on ? HostStats::now() : 0;
     if (s.frames) {
         const unsigned parts = copy_parts(e, s.scatter_bytes);
-        pool_of(e)->run(parts, [&](unsigned p) {
-            const uint32_t a = (uint32_t)((uint64_t)s.count * p / parts), b = (uint32_t)((uint64_t)s.count * (p + 1) / parts);
-            for (uint32_t t = a; t < b; t++) {
-                const fpnn_aes_host_frame &f = s.frames[s.first + t];
-                if (f.len + s.pre) memcpy(f.dst, s.h + s.out_at + s.out_off[t], f.len + s.pre);
-            }
-        });
+        pool_of(e)->run(parts, [&](unsigned p) { scatter_frames_part(s, p, parts); });
         s.frames = nullptr;
     } else {
         parallel_copy(e, s.scatter, s.scatter_bytes);
@@ -1164,9 +1258,23 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
     HostSlot *prev = nullptr;
     std::vector<Piece> pieces;
     std::vector<CopyJob> gather;
+    const int kSlots = (int)(sizeof(e->hs) / sizeof(e->hs[0]));
     while (si < nseg && rc == FPNN_AES_OK) {
         HostSlot &s = e->hs[k];
-        if ((rc = slot_drain(e, s, hst))) break;
+        if ((rc = slot_drain(e, s, hst))) break;  // package: already scattered beside a gather
+        // package: the chunk two back is scattered by half the copy threads while the other
+        // half gathers this one (host memory, not one thread group, is the limit)
+        HostSlot *sc = nullptr;
+        if (!stream) {
+            HostSlot &o = e->hs[(k + 1) % kSlots];
+            if (o.busy && o.frames) {
+                const double tw = hst.on ? HostStats::now() : 0;
+                HIP_TRY(hipEventSynchronize(o.done));
+                if (hst.on) hst.wait += HostStats::now() - tw;
+                o.busy = false;
+                sc = &o;
+            }
+        }
         // ---- choose this chunk's segments / pieces ----
         pieces.clear();
         struct CSeg {
@@ -1195,7 +1303,9 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
             uint32_t *slots = lens + cnt;
             // frame-parallel: per-part byte sums, then offsets + arrays + gather per part
-            const unsigned parts = copy_parts(e, in_b);
+            const unsigned all = pool_of(e)->parts();
+            const unsigned sparts = sc ? std::max(1u, all / 2) : 0;
+            const unsigned parts = sc ? std::max(1u, all - sparts) : copy_parts(e, in_b);
             uint64_t psum[64 + 1] = {0};
             const fpnn_aes_host_frame *fr = frames + si;
             auto range = [&](unsigned p, uint32_t &a, uint32_t &b) {
@@ -1212,7 +1322,11 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             });
             for (unsigned p = 0; p < parts; p++) psum[p + 1] += psum[p];
             uint8_t *h_in = s.h;
-            pool_of(e)->run(parts, [&](unsigned p) {
+            pool_of(e)->run(parts + sparts, [&](unsigned p) {
+                if (p >= parts) {
+                    scatter_frames_part(*sc, p - parts, sparts);
+                    return;
+                }
                 uint32_t a, b;
                 range(p, a, b);
                 uint64_t io = psum[p], oo = psum[p] + pre * a;
@@ -1222,12 +1336,14 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
                     out_off[t] = oo;
                     lens[t] = f.len;
                     slots[t] = f.key_slot;
-                    if (f.len) memcpy(h_in + io, f.src, f.len);
+                    copy_streaming(h_in + io, f.src, f.len);
                     io += f.len;
                     oo += f.len + pre;
                 }
+                copy_fence();
             });
             if (hst.on) hst.gather += HostStats::now() - tg;
+            if (sc) sc->frames = nullptr;
             s.frames = frames;
             s.first = (uint32_t)si;
             s.count = cnt;
@@ -1322,7 +1438,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         HIP_TRY(hipEventRecord(s.done, s.st));
         s.busy = true;
         prev = &s;
-        k ^= 1;
+        k = (k + 1) % kSlots;
     }
     for (auto &sl : e->hs) {
         const int r2 = slot_drain(e, sl, hst);
@@ -1381,6 +1497,87 @@ int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_fr
     if (n && (!iv_state || !pos_state)) return FPNN_AES_ERR_ARG;
     if (!n) return FPNN_AES_OK;
     return host_pipeline(e, encrypt != 0, true, frames, n, keys, 0, iv_state, pos_state);
+}
+
+// ---- one host batch over several engines (GPUs) ------------------------------------------
+// Each engine runs its share through its own host_pipeline in its own thread; errors are
+// collected and the first one (by engine index) is returned, with its message.
+static int run_multi(int n_engines, const std::function<int(int)> &fn) {
+    std::vector<int> rc(n_engines, FPNN_AES_OK);
+    std::vector<std::string> msg(n_engines);
+    std::vector<std::thread> th;
+    for (int k = 1; k < n_engines; k++)
+        th.emplace_back([&, k] {
+            rc[k] = fn(k);
+            if (rc[k]) msg[k] = g_last_error;
+        });
+    rc[0] = fn(0);
+    if (rc[0]) msg[0] = g_last_error;
+    for (auto &t : th) t.join();
+    for (int k = 0; k < n_engines; k++)
+        if (rc[k]) {
+            g_last_error = "engine " + std::to_string(k) + ": " + msg[k];
+            return rc[k];
+        }
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_package_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_keyset *const *keys, int n_engines,
+                                int encrypt, const fpnn_aes_host_frame *frames, uint32_t n, uint32_t flags) {
+    if (!engines || !keys || n_engines < 1 || (n && !frames)) return FPNN_AES_ERR_ARG;
+    for (int k = 0; k < n_engines; k++)
+        if (!engines[k] || !keys[k] || keys[k]->count != keys[0]->count || keys[k]->nrounds != keys[0]->nrounds)
+            return FPNN_AES_ERR_ARG;
+    if (n_engines == 1 || n < 2) return fpnn_aes_package_host(engines[0], encrypt, frames, n, keys[0], flags);
+    // byte-balanced contiguous ranges of frames
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += frames[i].len;
+    std::vector<uint32_t> cut(n_engines + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int p = 1;
+    for (uint32_t i = 0; i < n && p < n_engines; i++) {
+        acc += frames[i].len;
+        while (p < n_engines && acc * n_engines >= total * p) cut[p++] = i + 1;
+    }
+    return run_multi(n_engines, [&](int k) {
+        return fpnn_aes_package_host(engines[k], encrypt, frames + cut[k], cut[k + 1] - cut[k], keys[k], flags);
+    });
+}
+
+int fpnn_aes_stream_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_keyset *const *keys, int n_engines,
+                               int encrypt, const fpnn_aes_host_frame *frames, uint32_t n, uint8_t *iv_state,
+                               uint32_t *pos_state) {
+    if (!engines || !keys || n_engines < 1 || (n && (!frames || !iv_state || !pos_state))) return FPNN_AES_ERR_ARG;
+    for (int k = 0; k < n_engines; k++)
+        if (!engines[k] || !keys[k] || keys[k]->count != keys[0]->count || keys[k]->nrounds != keys[0]->nrounds)
+            return FPNN_AES_ERR_ARG;
+    if (n_engines == 1 || n < 2)
+        return fpnn_aes_stream_host(engines[0], encrypt, frames, n, keys[0], iv_state, pos_state);
+    // whole streams to engines, longest first onto the least-loaded engine (a stream's frames
+    // stay in order on one engine: its CFB state chains through them)
+    std::unordered_map<uint32_t, uint64_t> bytes;
+    for (uint32_t i = 0; i < n; i++) bytes[frames[i].key_slot] += frames[i].len;
+    std::vector<std::pair<uint64_t, uint32_t>> order;
+    order.reserve(bytes.size());
+    for (const auto &kv : bytes) order.push_back({kv.second, kv.first});
+    std::sort(order.begin(), order.end(), [](const std::pair<uint64_t, uint32_t> &a,
+                                             const std::pair<uint64_t, uint32_t> &b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    std::vector<uint64_t> load(n_engines, 0);
+    std::unordered_map<uint32_t, int> owner;
+    for (const auto &o : order) {
+        const int k = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        owner[o.second] = k;
+        load[k] += o.first;
+    }
+    std::vector<std::vector<fpnn_aes_host_frame>> part(n_engines);
+    for (uint32_t i = 0; i < n; i++) part[owner[frames[i].key_slot]].push_back(frames[i]);
+    return run_multi(n_engines, [&](int k) {
+        return fpnn_aes_stream_host(engines[k], encrypt, part[k].data(), (uint32_t)part[k].size(), keys[k], iv_state,
+                                    pos_state);
+    });
 }
 
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset) {

@@ -357,6 +357,27 @@ class Engine:
         check(lib.fpnn_aes_stream_decrypt(self._h, C.byref(d), _ptr(iv_state), _ptr(pos_state)), "stream_decrypt")
 
 
+def package_host_multi(engines, keysets, encrypt: bool, frames_np, wire_prefix: bool = False):
+    """fpnn_aes_package_host_multi: one host-frame batch split byte-balanced over engines
+    (keysets[k] on engines[k])."""
+    n = len(engines)
+    eh = (C.c_void_p * n)(*[e.handle.value for e in engines])
+    kh = (C.c_void_p * n)(*[k.handle.value for k in keysets])
+    ptr = C.cast(C.c_void_p(frames_np.ctypes.data), C.POINTER(HostFrame))
+    check(lib.fpnn_aes_package_host_multi(eh, kh, n, int(encrypt), ptr, len(frames_np),
+                                          F_WIRE_PREFIX if wire_prefix else 0), "package_host_multi")
+
+
+def stream_host_multi(engines, keysets, encrypt: bool, frames_np, iv_state: np.ndarray, pos_state: np.ndarray):
+    """fpnn_aes_stream_host_multi: whole streams to engines, state arrays updated in place."""
+    n = len(engines)
+    eh = (C.c_void_p * n)(*[e.handle.value for e in engines])
+    kh = (C.c_void_p * n)(*[k.handle.value for k in keysets])
+    ptr = C.cast(C.c_void_p(frames_np.ctypes.data), C.POINTER(HostFrame))
+    check(lib.fpnn_aes_stream_host_multi(eh, kh, n, int(encrypt), ptr, len(frames_np), iv_state.ctypes.data,
+                                         pos_state.ctypes.data), "stream_host_multi")
+
+
 class KeySet:
     """Per-connection (key, IV) table on the device, expanded by the GPU."""
 

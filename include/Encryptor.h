@@ -29,6 +29,11 @@ namespace fpnn {
 
 class EncryptorBatch;  // EncryptorBatch.h: runs queued calls of many encryptors in one GPU pass
 
+/* libfpnn_aes.so: a process-unique number per constructed Encryptor -- the key of its
+   slot in an EncryptorBatch's persistent device key table (an address can be reused by
+   a later Encryptor, a serial cannot). */
+uint64_t encryptor_serial();
+
 class EncryptorError : public std::runtime_error {
 public:
     explicit EncryptorError(const std::string &what) : std::runtime_error(what) {}
@@ -41,12 +46,14 @@ protected:
     uint8_t _iv[16];
     uint8_t _key[32];
     size_t _keyLen;
+    uint64_t _serial;
 
 public:
     Encryptor(uint8_t *key, size_t key_len, uint8_t *iv) {
         memcpy(_key, key, key_len);
         memcpy(_iv, iv, 16);
         _keyLen = key_len;
+        _serial = encryptor_serial();
     }
     virtual ~Encryptor() {}
 

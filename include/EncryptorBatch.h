@@ -33,7 +33,7 @@ namespace fpnn {
 class EncryptorBatch {
 public:
     EncryptorBatch() {}
-    ~EncryptorBatch() {}
+    ~EncryptorBatch();
     EncryptorBatch(const EncryptorBatch &) = delete;
     EncryptorBatch &operator=(const EncryptorBatch &) = delete;
 
@@ -65,6 +65,10 @@ private:
     };
     std::vector<Op> _ops;
     size_t _bytes = 0;
+    // Persistent device key tables, one per key length (AES-128/192/256): a slot per
+    // Encryptor seen, uploaded once; a flush only adds its new connections.
+    struct KeyTable;
+    KeyTable *_tables[3] = {nullptr, nullptr, nullptr};
     void add(Encryptor *enc, bool encrypt, uint8_t *dest, const uint8_t *src, int len, std::string *buffer);
 };
 

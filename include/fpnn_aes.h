@@ -87,6 +87,17 @@ int fpnn_aes_keyset_create(fpnn_aes_engine *e, uint32_t count, size_t keylen, co
  * rijndael_setup_encrypt (all with the same nrounds). */
 int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpnn_aes_schedule *ctx,
                                    const uint8_t *ivs, fpnn_aes_keyset **out);
+/* A key table updated in place -- the collector's persistent per-connection table
+ * (fpnn::EncryptorBatch): `capacity` slots of one key length (nrounds 10/12/14), all zero.
+ * fpnn_aes_keyset_set writes host schedules (+ IVs, NULL => zero) into slots
+ * [first, first + count), growing the table when needed (contents kept); it is queued on
+ * the engine stream through pinned staging, so a flush that adds a few connections
+ * costs one small copy and no allocation.  The key set's count becomes
+ * max(count, first + count). */
+int fpnn_aes_keyset_reserve(fpnn_aes_engine *e, uint32_t capacity, int nrounds, fpnn_aes_keyset **out);
+int fpnn_aes_keyset_set(fpnn_aes_keyset *ks, uint32_t first, uint32_t count, const fpnn_aes_schedule *ctx,
+                        const uint8_t *ivs);
+uint32_t fpnn_aes_keyset_count(const fpnn_aes_keyset *ks);
 int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks);
 int fpnn_aes_keyset_nrounds(const fpnn_aes_keyset *ks);
 /* Copy the expanded schedule of slot i back to the host (rijndael_context layout). */
@@ -187,6 +198,19 @@ int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_f
  * that many successive calls.  Synchronous. */
 int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                          const fpnn_aes_keyset *keys, uint8_t *iv_state, uint32_t *pos_state);
+
+/* One host-frame batch over several engines -- e.g. one per GPU of the node, each
+ * with its own copy of the key set (keys[k] created on engines[k], same count and key
+ * length).  Package mode splits the frames into byte-balanced contiguous ranges; stream
+ * mode gives whole streams (all frames of a key slot, in order) to engines, longest first
+ * onto the least-loaded one.  Every engine runs its share through its own pipeline in
+ * its own host thread; results are as from one call of fpnn_aes_package_host /
+ * fpnn_aes_stream_host.  Synchronous. */
+int fpnn_aes_package_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_keyset *const *keys, int n_engines,
+                                int encrypt, const fpnn_aes_host_frame *frames, uint32_t n, uint32_t flags);
+int fpnn_aes_stream_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_keyset *const *keys, int n_engines,
+                               int encrypt, const fpnn_aes_host_frame *frames, uint32_t n, uint8_t *iv_state,
+                               uint32_t *pos_state);
 
 /* ---- receive side: wire framing on the device (§8f row 3) --------------------------- */
 /* Per received segment (the bytes one connection delivered), the outcome of walking its

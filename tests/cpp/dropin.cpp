@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <iostream>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -64,6 +65,9 @@ int main() {
     std::string line;
     fpnn::EncryptorBatch batch;
     Queued q;
+    // connections that live across flushes (the batch's persistent key table)
+    std::map<std::string, std::unique_ptr<fpnn::Encryptor>> named;
+    std::map<std::string, bool> named_dir;
     while (std::getline(std::cin, line)) {
         std::istringstream is(line);
         std::string kind;
@@ -91,6 +95,30 @@ int main() {
                 auto data = unhex(f);
                 std::vector<uint8_t> *src = q.keep(data), *o = q.keep(data);
                 if (dir == "E")
+                    batch.encrypt(enc, o->data(), src->data(), (int)data.size());
+                else
+                    batch.decrypt(enc, o->data(), src->data(), (int)data.size());
+                outs.push_back({o, data.size(), nullptr});
+            }
+            q.lines.push_back(outs);
+        } else if (kind == "NS" || kind == "NP") {  // NS <name> <E|D> <key> <iv> / NP <name> - <key> <iv>
+            std::string name, dir, k, v;
+            is >> name >> dir >> k >> v;
+            auto key = unhex(k), iv = unhex(v);
+            if (kind == "NS")
+                named[name].reset(new fpnn::StreamEncryptor(key.data(), key.size(), iv.data()));
+            else
+                named[name].reset(new fpnn::PackageEncryptor(key.data(), key.size(), iv.data()));
+            named_dir[name] = dir != "D";
+        } else if (kind == "NF") {  // NF <name> <frame>...: queue frames on a named connection
+            std::string name, f;
+            is >> name;
+            fpnn::Encryptor *enc = named.at(name).get();
+            std::vector<Queued::Out> outs;
+            while (is >> f) {
+                auto data = unhex(f);
+                std::vector<uint8_t> *src = q.keep(data), *o = q.keep(data);
+                if (named_dir[name])
                     batch.encrypt(enc, o->data(), src->data(), (int)data.size());
                 else
                     batch.decrypt(enc, o->data(), src->data(), (int)data.size());

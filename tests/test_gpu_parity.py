@@ -972,3 +972,91 @@ def test_udp_datagram_batches(engine, oracle):
             o, iv2, p2 = oracle.cfb(k, True, data[offs[i]:offs[i] + lens[i]].tobytes(), *st[conn[i]])
             st[conn[i]] = (iv2, p2)
             assert dst[offs[i]:offs[i] + lens[i]].tobytes() == o, i
+
+
+def test_cpp_encryptor_batch_persistent_table_across_flushes(tmp_path, oracle):
+    """EncryptorBatch's persistent device key table: 64 connections that live across 6
+    flushes (stream state carried between flushes, package connections re-used), each
+    flush touching a random subset plus short-lived connections created and destroyed in
+    between (so addresses are reused by new keys), mixed key lengths; every output
+    against the oracle."""
+    from test_abi import build_dropin
+    exe = build_dropin(tmp_path)
+    rng = np.random.default_rng(777)
+    conns = {}
+    lines, expect = [], []
+    for c in range(64):
+        kl = (16, 24, 32)[c % 3]
+        key, iv = rng.bytes(kl), rng.bytes(16)
+        stream = c % 2 == 0
+        enc = bool(c % 4) if stream else True
+        conns[f"c{c}"] = dict(key=key, iv=iv, stream=stream, enc=enc, st_iv=iv, st_pos=0)
+        lines.append(f"{'NS' if stream else 'NP'} c{c} {'E' if enc else 'D'} {key.hex()} {iv.hex()}")
+    for fl in range(6):
+        for name in rng.choice(sorted(conns), 40, replace=False):
+            cc = conns[name]
+            frames = [rng.bytes(int(rng.integers(0, 900))) for _ in range(int(rng.integers(1, 4)))]
+            lines.append(f"NF {name} " + " ".join(f.hex() or "-" for f in frames))
+            outs = []
+            for f in frames:
+                if cc["stream"]:
+                    o, cc["st_iv"], cc["st_pos"] = oracle.cfb(cc["key"], cc["enc"], f, cc["st_iv"], cc["st_pos"])
+                else:
+                    o = oracle.package(cc["key"], cc["iv"], True, f)
+                outs.append(o.hex() or "-")
+            expect.append(" ".join(outs))
+        for t in range(20):  # short-lived connections
+            kl = (16, 32)[t % 2]
+            key, iv = rng.bytes(kl), rng.bytes(16)
+            data = rng.bytes(int(rng.integers(0, 600)))
+            lines.append(f"BP {key.hex()} {iv.hex()} {data.hex() or '-'}")
+            expect.append(f"{oracle.package(key, iv, True, data).hex() or '-'} "
+                          f"{oracle.package(key, iv, False, data).hex() or '-'} {oracle.package_frame(key, iv, data).hex()}")
+        lines.append("F")
+    import subprocess
+    res = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout.strip().split("\n") == expect
+
+
+def test_host_frames_over_two_engines(engine, oracle):
+    """fpnn_aes_package_host_multi / fpnn_aes_stream_host_multi with two engines (the
+    multi-GPU host path, here two engines on one GPU): byte-balanced package split and
+    whole-stream assignment give exactly the one-engine / oracle results."""
+    import fpnn_amd
+    rng = np.random.default_rng(4242)
+    e2 = fpnn_amd.Engine(0)
+    nconn, kl = 97, 32
+    keys = rng.bytes(nconn * kl)
+    ivs = rng.bytes(nconn * 16)
+    ks = [fpnn_amd.KeySet(engine, keys, kl, ivs), fpnn_amd.KeySet(e2, keys, kl, ivs)]
+    n = 3000
+    lens = rng.integers(0, 5000, n).astype(np.uint32)
+    src = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    dst = np.zeros_like(src)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    fr = np.zeros(n, dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
+    fr["src"] = src.ctypes.data + offs
+    fr["dst"] = dst.ctypes.data + offs
+    fr["len"] = lens
+    fr["key_slot"] = rng.integers(0, nconn, n)
+    fpnn_amd.package_host_multi([engine, e2], ks, True, fr)
+    for i in range(0, n, 7):
+        s = int(fr["key_slot"][i])
+        k, v = keys[s * kl:(s + 1) * kl], ivs[s * 16:(s + 1) * 16]
+        seg = src[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+        assert dst[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes() == oracle.package(k, v, True, seg), i
+    # stream mode: 97 streams, frames interleaved; state carried in the shared arrays
+    iv_state = np.frombuffer(ivs, dtype=np.uint8).copy()
+    pos_state = rng.integers(0, 16, nconn).astype(np.uint32)
+    iv0, pos0 = iv_state.copy(), pos_state.copy()
+    dst[:] = 0
+    fpnn_amd.stream_host_multi([engine, e2], ks, False, fr, iv_state, pos_state)
+    for s in range(nconn):
+        idx = np.nonzero(fr["key_slot"] == s)[0]
+        data = b"".join(src[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes() for i in idx)
+        exp, iv_end, pos_end = oracle.cfb(keys[s * kl:(s + 1) * kl], False, data, iv0[16 * s:16 * s + 16].tobytes(),
+                                          int(pos0[s]))
+        got = b"".join(dst[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes() for i in idx)
+        assert got == exp, s
+        assert (iv_state[16 * s:16 * s + 16].tobytes(), int(pos_state[s])) == (iv_end, pos_end), s

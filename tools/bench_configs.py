@@ -141,8 +141,21 @@ def main():
         eng.package_host_array(False, fr, ks)
         hbd = time.perf_counter() - t0
         assert np.array_equal(dst_h, src_h)
+        # the same frames over two engines (fpnn_aes_package_host_multi; on one GPU this
+        # measures the split's overhead -- the multi-GPU host path of SURVEY 8(e))
+        fr["src"] = src_h.ctypes.data + np.arange(P, dtype=np.uint64) * L
+        e2 = fpnn_amd.Engine(0)
+        ks2 = fpnn_amd.KeySet(e2, key, len(key), iv)
+        fpnn_amd.package_host_multi([eng, e2], [ks, ks2], True, fr)
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            fpnn_amd.package_host_multi([eng, e2], [ks, ks2], True, fr)
+        hm = (time.perf_counter() - t0) / args.reps
+        assert np.array_equal(dst_h, r.cpu().numpy())
+        del ks2, e2
         out["C2"] = {"encrypt_kernel_GiBs": gib(P * L, ke), "decrypt_kernel_GiBs": gib(P * L, kd),
                      "host_frames_encrypt_GiBs": gib(P * L, hb), "host_frames_decrypt_GiBs": gib(P * L, hbd),
+                     "host_frames_encrypt_2engines_GiBs": gib(P * L, hm),
                      "encrypt_wall_GiBs": gib(P * L, we), "decrypt_wall_GiBs": gib(P * L, wd),
                      "pcie_inclusive_encrypt_GiBs": gib(P * L, pe),
                      "pcie_inclusive_overlapped_encrypt_GiBs": gib(P * L, po), "h2d_GiBs": gib(P * L, h2d),
