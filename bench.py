@@ -38,8 +38,10 @@ import workloads as W  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 METRIC = "AES-256 GiB/s on device-resident packet batch; 1/2/4/8-GPU scaling"  # BASELINE.json "metric"
 # newest committed PMC summary of the bench command (tools/pmc_summary.py output), per workload
-PMC_SUMMARIES = {"C2": "profiles/r02/c2/pmc_summary.json", "C4": "profiles/r02/c4/pmc_summary.json",
-                 "C5": "profiles/r02/c5/pmc_summary.json"}
+# (C2: profiles of this bench command, tools/profile_session.sh; C4 / C5: tools/profile_configs.sh
+# runs of the same kernels on the same batches through tools/bench_configs.py)
+PMC_SUMMARIES = {"C2": "profiles/r02/bench/pmc_summary.json", "C4": "profiles/r02/C4/pmc_summary.json",
+                 "C5": "profiles/r02/C5/pmc_summary.json"}
 
 
 def parse():
@@ -159,6 +161,17 @@ def load_traffic(kernel: str, workload: str):
         if v is not None:
             return v, path
     return None, None
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def host_cpus():

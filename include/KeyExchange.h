@@ -7,9 +7,11 @@
 // plus ECCKeyExchange::calcKeys, the batch form a server uses for many accepted
 // connections at once.
 //
-// Not here: init() and init(const char* proto) (core/KeyExchange.cpp:10-47), which read
-// FPNN's Setting and a key file and then call init(curve, privateKey); they stay in
-// FPNN.  The curve is held as an index instead of a uECC_Curve.
+// init() and init(const char* proto) are declared (FPNN's servers call them,
+// core/TCPEpollServer.epoll.cpp:126, core/UDPEpollServer.epoll.cpp:84) but defined by
+// FPNN itself: they read its Setting and key file and call init(curve, privateKey) --
+// keep core/KeyExchange.cpp:10-47.  The curve is held as an index
+// instead of a uECC_Curve.
 // Failures of the device itself throw fpnn::EncryptorError (Encryptor.h) -- there is no
 // CPU fallback.
 #ifndef FPNN_AMD_KeyExchange_h
@@ -33,6 +35,8 @@ public:
     ECCKeyExchange() : _secertLen(0), _curve(-1) {}
     virtual ~ECCKeyExchange() {}
 
+    bool init();                    // defined by FPNN (core/KeyExchange.cpp:10-26)
+    bool init(const char *proto);   // defined by FPNN (core/KeyExchange.cpp:28-47)
     bool init(const std::string &curve, const std::string &privateKey);
     /*
         key: OUT. Key buffer length is equal to keylen.

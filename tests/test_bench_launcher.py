@@ -75,3 +75,27 @@ def test_shard_digests_cover_every_rank():
         d = json.load(f)
     assert shards["C2/r0"] == d["C2"]["cipher_sha256"]
     assert shards["C5/w1/r0"] == d["C5"]["cipher_sha256"]
+
+
+def test_cpu_baseline_leg_runs_on_cpu():
+    """bench.cpu_baseline end to end on a small sample (the leg the GPU bench runs on rank 0):
+    every field of the JSON object is produced and the CPU output is checked against the
+    expected ciphertext (here the oracle's, standing in for the GPU's)."""
+    import numpy as np
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle
+    P, L = 256, 1024
+    rng = np.random.default_rng(5)
+    plain = rng.integers(0, 256, P * L, dtype=np.uint8)
+    key, iv = bytes(range(32)), bytes(range(16))
+    expect = np.empty_like(plain)
+    o = Oracle("port")
+    o.package_batch(True, plain, expect, P, in_off=np.arange(P, dtype=np.uint64) * L,
+                    lens=np.full(P, L, np.uint32), key_slot=np.zeros(P, np.uint32), keys=np.frombuffer(key, np.uint8),
+                    keylen=32, ivs=np.frombuffer(iv, np.uint8), threads=4)
+    res = bench.cpu_baseline(plain, P, L, key, iv, 0.05, expect)
+    assert res["value"] > 0 and res["cores"] >= 1 and res["kind"] in ("reference", "port")
+    assert "matches GPU output: True" in res["sample"]
+    assert res["host"]["cpu_model"] and res["host"]["affinity_cpus"] >= 1
+    json.dumps(res)
