@@ -387,11 +387,15 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
+    // small ragged batches: block map (+ stream snapshot) in one single-workgroup kernel
+    const bool small_map = b->count <= block_map_small_max();
     if (stream) {  // snapshot the incoming (iv, pos) state, see KBatch::iv_snap
         if ((rc = grow(e->d_snap_iv, e->cap_snap_iv, b->count))) return rc;
         if ((rc = grow(e->d_snap_pos, e->cap_snap_pos, b->count))) return rc;
-        HIP_TRY(hipMemcpyAsync(e->d_snap_iv, iv_state, 16ull * b->count, hipMemcpyDeviceToDevice, e->stream));
-        HIP_TRY(hipMemcpyAsync(e->d_snap_pos, pos_state, 4ull * b->count, hipMemcpyDeviceToDevice, e->stream));
+        if (!small_map) {  // (stream batches always take the general layout below)
+            HIP_TRY(hipMemcpyAsync(e->d_snap_iv, iv_state, 16ull * b->count, hipMemcpyDeviceToDevice, e->stream));
+            HIP_TRY(hipMemcpyAsync(e->d_snap_pos, pos_state, 4ull * b->count, hipMemcpyDeviceToDevice, e->stream));
+        }
         k.iv_snap = e->d_snap_iv;
         k.pos_snap = e->d_snap_pos;
     }
@@ -435,7 +439,11 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
         const int grid = e->num_cus;
         if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
-        HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
+        if (small_map)
+            HIP_TRY(launch_block_map_small(k, stream, iv_state, pos_state, e->d_snap_iv, e->d_snap_pos, e->d_bstart,
+                                           e->d_total, e->stream));
+        else
+            HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         k.bstart = e->d_bstart;
         if (!k.in_off || !k.len) {  // K1r reads descriptor arrays: materialize the missing ones
             if (!k.in_off && (rc = grow(e->d_desc_off, e->cap_desc_off, b->count))) return rc;

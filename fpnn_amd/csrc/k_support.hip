@@ -78,6 +78,75 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_add(uint64_t *bstart, con
     if (i < count) bstart[i] += wg_sums[i / kScanTile];
 }
 
+// Batches of up to kSmallScanMax segments (C3's 4 096 streams, R1's 16 384 connections):
+// the whole block map in ONE workgroup -- and, for stream batches, the (iv, pos) snapshot
+// the decrypt kernels read -- instead of three scan launches plus two copies; a framed
+// call is launch-bound, so this is most of its fixed cost.  The snapshot is written
+// here but the block counts read the live state (nothing has changed it yet).
+constexpr int kSmallScanThreads = 1024;
+constexpr int kSmallScanItems = 16;
+constexpr uint64_t kSmallScanMax = (uint64_t)kSmallScanThreads * kSmallScanItems;
+
+template <bool STREAM>
+__global__ __launch_bounds__(kSmallScanThreads) void k_scan_small(KBatch b, const uint4 *iv_src, const uint32_t *pos_src,
+                                                                  uint4 *snap_iv, uint32_t *snap_pos, uint64_t *bstart,
+                                                                  uint64_t *total_out) {
+    __shared__ uint64_t sh[kSmallScanThreads];
+    const int t = threadIdx.x;
+    const uint64_t per = (b.count + kSmallScanThreads - 1) / kSmallScanThreads;  // <= kSmallScanItems
+    const uint64_t lo = (uint64_t)t * per;
+    uint64_t v[kSmallScanItems], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kSmallScanItems; k++) {
+        const uint64_t s = lo + k;
+        v[k] = 0;
+        if ((uint64_t)k < per && s < b.count) {
+            const uint32_t len = b.len ? b.len[s] : b.uniform_len;
+            uint32_t pos = 0;
+            if (STREAM) {
+                pos = pos_src[s];
+                snap_pos[s] = pos;
+                snap_iv[s] = iv_src[s];
+            }
+            v[k] = seg_blocks(len, pos);
+        }
+        sum += v[k];
+    }
+    sh[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < kSmallScanThreads; off <<= 1) {
+        const uint64_t add = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += add;
+        __syncthreads();
+    }
+    uint64_t run = sh[t] - sum;
+#pragma unroll
+    for (int k = 0; k < kSmallScanItems; k++) {
+        const uint64_t s = lo + k;
+        if ((uint64_t)k < per && s < b.count) bstart[s] = run;
+        run += v[k];
+    }
+    if (t == kSmallScanThreads - 1) {
+        bstart[b.count] = sh[t];
+        *total_out = sh[t];
+    }
+}
+
+hipError_t launch_block_map_small(const KBatch &b, bool stream, const uint8_t *iv_state, const uint32_t *pos_state,
+                                  uint4 *snap_iv, uint32_t *snap_pos, uint64_t *bstart, uint64_t *total,
+                                  hipStream_t st) {
+    if (stream)
+        hipLaunchKernelGGL((k_scan_small<true>), dim3(1), dim3(kSmallScanThreads), 0, st, b,
+                           reinterpret_cast<const uint4 *>(iv_state), pos_state, snap_iv, snap_pos, bstart, total);
+    else
+        hipLaunchKernelGGL((k_scan_small<false>), dim3(1), dim3(kSmallScanThreads), 0, st, b, nullptr, nullptr,
+                           nullptr, nullptr, bstart, total);
+    return hipGetLastError();
+}
+
+uint64_t block_map_small_max() { return kSmallScanMax; }
+
 // ---------------------------------------------------------------------------
 // Length ordering for ragged encrypt batches: counting sort into 128 descending
 // quarter-octave buckets of the block count (order inside a bucket is arbitrary; it

@@ -132,6 +132,12 @@ hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchun
 // device); wg_sums scratch of ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
+// The same for count <= block_map_small_max() in one workgroup; stream batches also
+// copy (iv_state, pos_state) into the snapshot (snap_iv / snap_pos) on the way.
+hipError_t launch_block_map_small(const KBatch &b, bool stream, const uint8_t *iv_state, const uint32_t *pos_state,
+                                  uint4 *snap_iv, uint32_t *snap_pos, uint64_t *bstart, uint64_t *total,
+                                  hipStream_t st);
+uint64_t block_map_small_max();
 // The rest of rijndael.h (k_modes.hip): ECB / CBC / OFB over one host call's buffers.
 enum : int { MODE_ECB_ENC = 0, MODE_ECB_DEC = 1, MODE_CBC_ENC = 2, MODE_CBC_DEC = 3, MODE_OFB = 4 };
 struct ModeArgs {
