@@ -71,3 +71,17 @@ def queue_engine():
     yield eng
     eng.sync()
     eng.close()
+
+
+@pytest.fixture(params=["lane", "wave"])
+def scan_mode(request):
+    """Run a receive test through both device frame walks (framing.hip: one lane per
+    segment, or one wavefront per segment with length-guessing header reads); by default
+    the engine picks by segment count."""
+    old = os.environ.get("FPNN_AES_SCAN")
+    os.environ["FPNN_AES_SCAN"] = request.param
+    yield request.param
+    if old is None:
+        del os.environ["FPNN_AES_SCAN"]
+    else:
+        os.environ["FPNN_AES_SCAN"] = old

@@ -37,7 +37,7 @@ def _layout(cases, lead):
 
 
 @pytest.mark.parametrize("inplace", [False, True])
-def test_package_recv_matches_reference_receiver(engine, inplace):
+def test_package_recv_matches_reference_receiver(engine, inplace, scan_mode):
     import fpnn_amd
     for (max_len, keylen), cases in _groups("package"):
         n = len(cases)
@@ -63,7 +63,7 @@ def test_package_recv_matches_reference_receiver(engine, inplace):
                     assert res[offs[i] + o:offs[i] + o + ln].tobytes() == raw, (c["name"], j)
 
 
-def test_stream_recv_matches_reference_receiver(engine, oracle):
+def test_stream_recv_matches_reference_receiver(engine, oracle, scan_mode):
     import fpnn_amd
     for (max_len, keylen), cases in _groups("stream"):
         n = len(cases)

@@ -794,7 +794,7 @@ def _package_wire(rng, oracle, key, iv, nframes, max_len, partial, oversize):
 
 
 @pytest.mark.parametrize("inplace", [False, True])
-def test_package_recv_frames(engine, oracle, inplace):
+def test_package_recv_frames(engine, oracle, inplace, scan_mode):
     import fpnn_amd
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as PO
@@ -845,7 +845,7 @@ def _fpnn_message(rng, mtype, ss, psize):
     return hdr + rng.bytes(body)
 
 
-def test_stream_recv_messages(engine, oracle):
+def test_stream_recv_messages(engine, oracle, scan_mode):
     """Two receive calls per stream: the first ends mid-message, its plaintext tail is
     carried in front of the second call's segment; malformed headers stop the scan with
     the reference's verdict."""
@@ -923,6 +923,104 @@ def test_stream_recv_messages(engine, oracle):
         _, iv_end, pos_end = oracle.cfb(keys[s * keylen:(s + 1) * keylen].tobytes(), True, plains[s],
                                         iv0[s].tobytes(), 0)
         assert d_iv[s].cpu().numpy().tobytes() == iv_end and int(d_pos[s]) == pos_end
+
+
+def _runs(rng, total, maxlen):
+    """Frame lengths in runs of equal length (the wave walk's guess holds inside a run)."""
+    out = []
+    while len(out) < total:
+        out += [int(rng.integers(0, maxlen + 1))] * int(rng.choice([1, 2, 5, 63, 64, 65, 130]))
+    return out[:total]
+
+
+def test_recv_runs_of_equal_frames(engine, oracle, scan_mode):
+    """Both receive modes over connections whose frames come in runs of equal length, the
+    runs ending in every way the walk can stop: end of data, a partial frame, an oversize
+    prefix / bad header after a run, and max_frames reached inside a run."""
+    import fpnn_amd
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as PO
+    rng = np.random.default_rng(77)
+    nconn, keylen, max_len, max_frames = 24, 16, 3000, 200
+    keys = rng.integers(0, 256, nconn * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nconn * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, ivs.tobytes())
+    kv = [(keys[c * keylen:(c + 1) * keylen].tobytes(), ivs[c * 16:(c + 1) * 16].tobytes()) for c in range(nconn)]
+
+    def layout(segs):
+        offs = np.cumsum([0] + [len(w) + 3 for w in segs[:-1]]).astype(np.int64)
+        host = np.zeros(int(offs[-1] + len(segs[-1]) + 3), dtype=np.uint8)
+        for o, w in zip(offs, segs):
+            host[o:o + len(w)] = np.frombuffer(w, np.uint8)
+        lens = torch.tensor([len(w) for w in segs], dtype=torch.int32, device=DEV)
+        return offs, host, lens
+
+    # package mode
+    segs, bodies = [], []
+    for c in range(nconn):
+        k, v = kv[c]
+        nfr = 250 if c % 4 == 3 else int(rng.integers(0, 190))
+        bs = [rng.bytes(n) for n in _runs(rng, nfr, 300)]
+        wire = b"".join(len(b).to_bytes(4, "little") + oracle.package(k, v, True, b) for b in bs)
+        if c % 4 == 1:
+            wire += (200).to_bytes(4, "little") + rng.bytes(int(rng.integers(0, 200)))
+        elif c % 4 == 2:
+            wire += (max_len + 1).to_bytes(4, "little") + rng.bytes(64)
+        segs.append(wire)
+        bodies.append(bs)
+    offs, host, lens = layout(segs)
+    inp = torch.from_numpy(host).to(DEV)
+    out = torch.zeros_like(inp)
+    foff, flen, scan = engine.package_recv(inp, out, nconn, ks, max_len, max_frames,
+                                           in_off=torch.from_numpy(offs).to(DEV), lens=lens,
+                                           key_slot=torch.arange(nconn, dtype=torch.int32, device=DEV))
+    torch.cuda.synchronize()
+    frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+    foff, flen, res = foff.cpu().numpy(), flen.cpu().numpy(), out.cpu().numpy()
+    for c in range(nconn):
+        ef, es, ec = PO.scan_package(segs[c], max_len, max_frames)
+        assert (frames[c], status[c], consumed[c]) == (len(ef), es, ec), c
+        assert [tuple(x) for x in zip(foff[c * max_frames:c * max_frames + len(ef)],
+                                      flen[c * max_frames:c * max_frames + len(ef)])] == ef, c
+        assert (flen[c * max_frames + len(ef):(c + 1) * max_frames] == 0).all(), c
+        for j, (bo, n) in enumerate(ef):
+            assert res[offs[c] + bo:offs[c] + bo + n].tobytes() == bodies[c][j], (c, j)
+    assert set(status.tolist()) == {PO.SCAN_OK, PO.SCAN_TOO_LARGE, PO.SCAN_FULL}
+
+    # stream mode: runs of identical message headers
+    plains = []
+    for c in range(nconn):
+        nmsg = 250 if c % 4 == 3 else int(rng.integers(0, 190))
+        msgs, i = [], 0
+        while i < nmsg:
+            run = min(nmsg - i, int(rng.choice([1, 3, 64, 65, 100])))
+            mt, ss, ps = int(rng.integers(0, 3)), int(rng.integers(0, 8)), int(rng.integers(0, 200))
+            msgs += [_fpnn_message(rng, mt, ss, ps) for _ in range(run)]
+            i += run
+        if c % 4 == 1:
+            msgs.append(_fpnn_message(rng, 2, 0, 100)[:50])  # partial
+        elif c % 4 == 2:
+            msgs.append(b"FPNX" + bytes(20))
+        plains.append(b"".join(msgs))
+    ciphers = [oracle.cfb(kv[c][0], True, plains[c], kv[c][1], 0)[0] for c in range(nconn)]
+    offs, host, lens = layout(ciphers)
+    inp = torch.from_numpy(host).to(DEV)
+    out = torch.zeros_like(inp)
+    d_iv = torch.from_numpy(ivs.copy()).to(DEV)
+    d_pos = torch.zeros(nconn, dtype=torch.int32, device=DEV)
+    foff, flen, scan = engine.stream_recv(inp, out, nconn, ks, d_iv, d_pos, max_len, max_frames,
+                                          in_off=torch.from_numpy(offs).to(DEV), lens=lens,
+                                          key_slot=torch.arange(nconn, dtype=torch.int32, device=DEV))
+    torch.cuda.synchronize()
+    frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+    foff, flen, res = foff.cpu().numpy(), flen.cpu().numpy(), out.cpu().numpy()
+    for c in range(nconn):
+        assert res[offs[c]:offs[c] + len(plains[c])].tobytes() == plains[c], c
+        ef, es, ec = PO.scan_stream(plains[c], max_len, max_frames)
+        assert (frames[c], status[c], consumed[c]) == (len(ef), es, ec), c
+        assert [tuple(x) for x in zip(foff[c * max_frames:c * max_frames + len(ef)],
+                                      flen[c * max_frames:c * max_frames + len(ef)])] == ef, c
+    assert set(status.tolist()) == {PO.SCAN_OK, PO.SCAN_BAD_MAGIC, PO.SCAN_FULL}
 
 
 def test_udp_datagram_batches(engine, oracle):

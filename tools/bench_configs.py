@@ -387,6 +387,89 @@ def main():
         del a, wire, plain
         print(json.dumps({"R1": out["R1"]}), flush=True)
 
+    if "R1R" in todo:
+        # R1 with realistic body lengths: CFB does not pad, so FPNN package bodies have any
+        # length -- here uniform 1 .. 2047 bytes (mean ~1 KiB), 64 frames per connection
+        NC, F = 16384, 64
+        key, iv = W.single_key(W.C2)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        P = NC * F
+        rng = np.random.default_rng(1717)
+        blen = rng.integers(1, 2048, P).astype(np.int64)
+        in_off = np.concatenate([[0], np.cumsum(blen[:-1])]).astype(np.int64)
+        out_off = in_off + 4 * np.arange(P, dtype=np.int64)
+        total = int(blen.sum())
+        a = torch.empty(total, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, 8)
+        wire = torch.empty(total + 4 * P, dtype=torch.uint8, device="cuda")
+        eng.package_encrypt(a, wire, P, ks, in_off=torch.from_numpy(in_off).cuda(),
+                            out_off=torch.from_numpy(out_off).cuda(),
+                            lens=torch.from_numpy(blen.astype(np.int32)).cuda(), wire_prefix=True)
+        per_conn = (blen + 4).reshape(NC, F).sum(axis=1)
+        conn_off = torch.from_numpy(np.concatenate([[0], np.cumsum(per_conn[:-1])]).astype(np.int64)).cuda()
+        conn_len = torch.from_numpy(per_conn.astype(np.int32)).cuda()
+        plain = torch.empty_like(wire)
+
+        def recv():
+            return eng.package_recv(wire, plain, NC, ks, 8 << 20, F, in_off=conn_off, lens=conn_len)
+
+        wr, kr, _ = timed(eng, D, recv, args.reps)
+        recv()
+        torch.cuda.synchronize()
+        body_mask = torch.ones(total + 4 * P, dtype=torch.bool, device="cuda")
+        pre = torch.from_numpy(out_off).cuda()
+        for k in range(4):
+            body_mask[pre + k] = False
+        assert torch.equal(plain[body_mask], a), "R1R receive-path plaintext differs"
+        out["R1R"] = {"frames": P, "body_bytes": total, "recv_wall_GiBs": gib(total, wr),
+                      "decrypt_kernel_GiBs": gib(total, kr),
+                      "note": "R1 with body lengths uniform in 1..2047 B (not 16-aligned): frame scan + K1r"}
+        del a, wire, plain, body_mask
+        print(json.dumps({"R1R": out["R1R"]}), flush=True)
+
+    if "R2" in todo:
+        # The stream-mode receive path: 4096 streams (C3's connections, AES-128), each call's
+        # segment = 256 KiB of ciphertext holding 256 FPNN answers of 1 KiB (12-byte header
+        # + seq + 1008-byte payload); fpnn_aes_stream_recv decrypts it (state carried) and
+        # splits it into messages with the reference's BodyLen checks.
+        NS, M, L = 4096, 256, 1024
+        keys, ivs = W.many_keys(W.C3)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), 16, np.zeros(NS * 16, np.uint8).tobytes())
+        plain = torch.empty(NS * M * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(plain, 9)
+        msg = plain.view(NS * M, L)
+        hdr = torch.tensor(list(b"FPNN") + [1, 0x80, 2, 0] + list((L - 16).to_bytes(4, "little")), dtype=torch.uint8,
+                           device="cuda")
+        msg[:, :12] = hdr
+        wire = torch.empty_like(plain)
+        iv0 = torch.from_numpy(ivs.copy()).cuda()
+        pos0 = torch.zeros(NS, dtype=torch.int32, device="cuda")
+        iv_e, pos_e = iv0.clone(), pos0.clone()
+        eng.stream_encrypt(plain, wire, NS, ks, iv_e, pos_e, stride=M * L, uniform_len=M * L)
+        out_buf = torch.empty_like(wire)
+        seg_len = torch.full((NS,), M * L, dtype=torch.int32, device="cuda")
+        seg_off = torch.arange(NS, dtype=torch.int64, device="cuda") * (M * L)
+        state = {}
+
+        def recv():
+            state["iv"], state["pos"] = iv0.clone(), pos0.clone()
+            return eng.stream_recv(wire, out_buf, NS, ks, state["iv"], state["pos"], 8 << 20, M, in_off=seg_off,
+                                   lens=seg_len)
+
+        wr, kr, _ = timed(eng, D, recv, args.reps)
+        foff, flen, scan = recv()
+        torch.cuda.synchronize()
+        frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+        assert (frames == M).all() and (status == 0).all() and (consumed == M * L).all(), "R2 framing"
+        assert torch.equal(out_buf, plain), "R2 plaintext differs"
+        assert torch.equal(state["iv"], iv_e) and torch.equal(state["pos"], pos_e), "R2 stream state"
+        out["R2"] = {"streams": NS, "messages": NS * M, "bytes": NS * M * L, "recv_wall_GiBs": gib(NS * M * L, wr),
+                     "decrypt_kernel_GiBs": gib(NS * M * L, kr),
+                     "note": "fpnn_aes_stream_recv over 4096 AES-128 streams x 256 KiB (256 FPNN messages of 1 KiB "
+                             "each): decrypt with carried state + device message scan; no host sync"}
+        del plain, wire, out_buf
+        print(json.dumps({"R2": out["R2"]}), flush=True)
+
     print(json.dumps({"configs": out}))
 
 
