@@ -33,6 +33,7 @@ SCAN_OK, SCAN_FULL, SCAN_TOO_LARGE, SCAN_BAD_MAGIC, SCAN_BAD_MTYPE, SCAN_BAD_LEN
 MAX_RECV_PACKAGE_LENGTH = 8 * 1024 * 1024  # FPNN_DEFAULT_MAX_PACKAGE_LEN, core/Config.h:14
 K_DECRYPT = 0
 K_ENCRYPT = 1
+K_HOST = 2  # last_kernel only: "host_mapped" / "host_staged"
 
 
 class FpnnAesError(RuntimeError):
@@ -111,6 +112,9 @@ SIGNATURES = {
                                               C.c_uint32]),
     "fpnn_aes_stream_host_multi": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.POINTER(HostFrame), C.c_uint32, _vp,
                                              _vp]),
+    "fpnn_aes_host_register": (C.c_int, [_vp, C.c_size_t]),
+    "fpnn_aes_host_unregister": (C.c_int, [_vp]),
+    "fpnn_aes_host_is_mapped": (C.c_int, [_vp, C.c_size_t]),
     "fpnn_aes_package_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), C.c_uint32, C.c_uint32, _vp, _vp, _vp]),
     "fpnn_aes_stream_recv": (C.c_int, [_vp, C.POINTER(BatchDesc), _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
                                        _vp]),

@@ -11,6 +11,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <climits>
+#include <cstdint>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -65,8 +68,9 @@ struct HostSlot {
     uint8_t *h = nullptr, *d = nullptr;
     uint64_t cap = 0;
     hipStream_t st = nullptr;
-    hipEvent_t done = nullptr;   // chunk's D2H finished
-    hipEvent_t kdone = nullptr;  // chunk's kernel finished (stream mode chains chunks on it)
+    hipEvent_t done = nullptr;    // chunk's D2H finished
+    hipEvent_t staged = nullptr;  // chunk's H2D finished (the engine stream may cipher it)
+    hipEvent_t kdone = nullptr;   // chunk's kernel finished (the slot stream may copy it back)
     bool busy = false;
     std::vector<CopyJob> scatter;  // staged output -> callers' buffers, run after `done`
     uint64_t scatter_bytes = 0;
@@ -76,6 +80,21 @@ struct HostSlot {
     uint32_t first = 0, count = 0;
     uint64_t pre = 0, out_at = 0;
     const uint64_t *out_off = nullptr;  // pinned, inside h
+};
+
+// One slot of the host-mapped frame pipeline (frames in memory registered with
+// fpnn_aes_host_register): device staging for one chunk (input | output | descriptors),
+// the pinned descriptor block the host fills, and the events that hand the chunk from
+// the move stream to the engine stream and back.
+struct MapSlot {
+    uint8_t *d = nullptr;  // device: in | out | desc
+    uint64_t dcap = 0;
+    uint8_t *h = nullptr;  // pinned: desc
+    uint64_t hcap = 0;
+    hipEvent_t gathered = nullptr;  // chunk staged in HBM (the engine stream may cipher it)
+    hipEvent_t ciphered = nullptr;  // cipher done (the move stream may scatter)
+    hipEvent_t done = nullptr;      // the slot's descriptors went H2D (its pinned block is free)
+    bool busy = false;
 };
 
 // Persistent host workers for the host-frame path.  Gathering 1M separate 1 KiB frames
@@ -205,6 +224,9 @@ struct fpnn_aes_engine {
     uint64_t cap_stage = 0;
     // host-frame pipeline
     HostSlot hs[3];  // chunk i on slot i % 3: gather(i) runs beside scatter(i - 2)
+    MapSlot ms[4];   // host-mapped chunks: gather(t) + scatter(t - 2) || cipher(t - 1), upload(t + 1)
+    hipStream_t map_stream = nullptr;  // host-mapped moves (both PCIe directions in one launch)
+    const char *host_path = "";  // "host_staged" / "host_mapped": the last host-frame call's path
     std::unique_ptr<HostPool> pool;  // created on first use
     // instrumentation
     bool timing = false;
@@ -612,9 +634,19 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         if (h.h) (void)hipHostFree(h.h);
         if (h.d) (void)hipFree(h.d);
         if (h.done) (void)hipEventDestroy(h.done);
+        if (h.staged) (void)hipEventDestroy(h.staged);
         if (h.kdone) (void)hipEventDestroy(h.kdone);
         if (h.st) (void)hipStreamDestroy(h.st);
     }
+    if (e->map_stream) (void)hipStreamSynchronize(e->map_stream);
+    for (auto &m : e->ms) {
+        if (m.h) (void)hipHostFree(m.h);
+        if (m.d) (void)hipFree(m.d);
+        if (m.gathered) (void)hipEventDestroy(m.gathered);
+        if (m.ciphered) (void)hipEventDestroy(m.ciphered);
+        if (m.done) (void)hipEventDestroy(m.done);
+    }
+    if (e->map_stream) (void)hipStreamDestroy(e->map_stream);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return FPNN_AES_OK;
@@ -1101,6 +1133,7 @@ int slot_reserve(HostSlot &s, int device, uint64_t need) {
     if (!s.st) {
         HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming));
     }
     if (need <= s.cap) return FPNN_AES_OK;
@@ -1177,9 +1210,10 @@ struct Piece {
 //            successive calls, base/rijndael.c:1171-1201 carries ivec/num), whose
 //            state lives in iv_state/pos_state[slot] on the host.
 // Chunks of <= kChunk input bytes are gathered into pinned staging by the copy pool,
-// then H2D, kernel, D2H run on the slot's stream while the host gathers the next chunk.
-// In stream mode a stream may be split across chunks; the chunks' kernels are then
-// chained with events so each continues from the state the previous one left.
+// then H2D and D2H run on the slot's stream and the kernel on the engine stream (events
+// hand the chunk over) while the host gathers the next chunk.  Kernels of successive
+// chunks are therefore ordered: they share the engine's scratch, and in stream mode a
+// stream split across chunks continues from the state the previous chunk left.
 int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_host_frame *frames, uint32_t n,
                   const fpnn_aes_keyset *keys, uint32_t flags, uint8_t *iv_state, uint32_t *pos_state) {
     const uint64_t pre = (!stream && (flags & FPNN_AES_F_WIRE_PREFIX)) ? 4 : 0;
@@ -1216,6 +1250,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         }
     }
     if (stream && segs.empty()) return FPNN_AES_OK;
+    e->host_path = "host_staged";
     const uint64_t nseg = stream ? segs.size() : n;
     HostStats hst;
     const double t_call = hst.on ? HostStats::now() : 0;
@@ -1423,7 +1458,12 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         }
         nchunks++;
         HIP_TRY(hipMemcpyAsync(s.d, s.h, in_pad + arr, hipMemcpyHostToDevice, s.st));
-        if (stream && prev) HIP_TRY(hipStreamWaitEvent(s.st, prev->kdone, 0));
+        // The cipher runs on the engine stream: chunks share the engine's scratch (block
+        // map, plan, length order, queue counter), so their kernels must not overlap --
+        // and stream chunks continue from the state the previous chunk left.  The copies
+        // of the slots still overlap each other and the kernels.
+        HIP_TRY(hipEventRecord(s.staged, s.st));
+        HIP_TRY(hipStreamWaitEvent(main_stream, s.staged, 0));
         fpnn_aes_batch b;
         memset(&b, 0, sizeof b);
         b.in = s.d;
@@ -1437,11 +1477,10 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         b.flags = pre ? FPNN_AES_F_WIRE_PREFIX : 0;
         uint8_t *ivp = stream ? d_state + 16 * state0 : nullptr;
         uint32_t *posp = stream ? reinterpret_cast<uint32_t *>(d_state + 16 * nseg) + state0 : nullptr;
-        e->stream = s.st;  // queue this chunk's kernels on the slot stream
         rc = encrypt ? run_encrypt(e, &b, ivp, posp, stream) : run_decrypt(e, &b, ivp, posp, stream);
-        e->stream = main_stream;
         if (rc) break;
-        HIP_TRY(hipEventRecord(s.kdone, s.st));
+        HIP_TRY(hipEventRecord(s.kdone, main_stream));
+        HIP_TRY(hipStreamWaitEvent(s.st, s.kdone, 0));
         HIP_TRY(hipMemcpyAsync(s.h + out_at, s.d + out_at, out_pad, hipMemcpyDeviceToHost, s.st));
         HIP_TRY(hipEventRecord(s.done, s.st));
         s.busy = true;
@@ -1486,6 +1525,342 @@ int check_host_frames(const fpnn_aes_engine *e, const fpnn_aes_host_frame *frame
     return FPNN_AES_OK;
 }
 
+// ---- host-mapped frames ------------------------------------------------------------------
+// Host ranges registered with fpnn_aes_host_register (process-wide, portable: every GPU may
+// access them).  A range's device-visible address is looked up per device on first use.
+constexpr int kMapDevices = 64;
+struct MappedRange {
+    uintptr_t lo, hi;
+    intptr_t delta[kMapDevices];  // device address - host address per device (INTPTR_MIN: not looked up)
+};
+std::mutex g_map_mu;
+std::vector<MappedRange> g_mapped;  // sorted by lo, disjoint
+
+// One call's view of the registry: the ranges and this device's address deltas.
+struct MapView {
+    std::vector<uintptr_t> lo, hi;
+    std::vector<intptr_t> delta;
+    // the range holding [p, p + n), or -1
+    long find(const void *ptr, uint64_t n) const {
+        const uintptr_t p = (uintptr_t)ptr;
+        auto it = std::upper_bound(lo.begin(), lo.end(), p);
+        if (it == lo.begin()) return -1;
+        const size_t i = (size_t)(it - lo.begin()) - 1;
+        return p + n <= hi[i] && p + n >= p ? (long)i : -1;
+    }
+};
+
+int map_view(int device, MapView &v) {
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    v.lo.clear();
+    v.hi.clear();
+    v.delta.clear();
+    if (device < 0 || device >= kMapDevices) return FPNN_AES_OK;  // (no mapped path there)
+    for (auto &r : g_mapped) {
+        if (r.delta[device] == INTPTR_MIN) {
+            DeviceGuard g(device);
+            void *dp = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&dp, reinterpret_cast<void *>(r.lo), 0));
+            r.delta[device] = (intptr_t)dp - (intptr_t)r.lo;
+        }
+        v.lo.push_back(r.lo);
+        v.hi.push_back(r.hi);
+        v.delta.push_back(r.delta[device]);
+    }
+    return FPNN_AES_OK;
+}
+
+int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
+    if (!m.gathered) {
+        HIP_TRY(hipEventCreateWithFlags(&m.gathered, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&m.ciphered, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&m.done, hipEventDisableTiming));
+    }
+    if (dneed > m.dcap) {
+        uint64_t c = m.dcap ? m.dcap : (16u << 20);
+        while (c < dneed) c *= 2;
+        if (m.d) (void)hipFree(m.d);
+        m.d = nullptr;
+        m.dcap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&m.d), c));
+        m.dcap = c;
+    }
+    if (hneed > m.hcap) {
+        uint64_t c = m.hcap ? m.hcap : (1u << 20);
+        while (c < hneed) c *= 2;
+        if (m.h) (void)hipHostFree(m.h);
+        m.h = nullptr;
+        m.hcap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&m.h), c, 0));
+        m.hcap = c;
+    }
+    return FPNN_AES_OK;
+}
+
+// Package-mode host frames that all lie in registered memory.  The call is cut into
+// chunks of whole frames; chunk t lives in slot t % 4 (HBM staging in | out | descriptors,
+// pinned descriptor block).  Step t: on the move stream ONE launch gathers chunk t from
+// host memory into its staging AND scatters chunk t - 2's results to the frames'
+// destinations (k_move_segments: both PCIe directions busy in one kernel); meanwhile the
+// engine stream ciphers chunk t - 1 as an ordinary device batch (uniform lengths keep the
+// dense K2 / K1d paths) and then uploads chunk t + 1's descriptors (40 B per frame,
+// written by the host threads during step t), so the move stream never waits for a copy.
+// Events hand each chunk between the two streams.  The host threads only write
+// descriptors.
+int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                    const fpnn_aes_keyset *keys, uint32_t flags, const MapView &v, uint32_t *done) {
+    const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
+    static const uint64_t kChunk = [] {     // input bytes per full chunk (FPNN_AES_MAP_CHUNK_MB)
+        const char *x = getenv("FPNN_AES_MAP_CHUNK_MB");
+        return (x && atoi(x) > 0 ? (uint64_t)atoi(x) : 32ull) << 20;
+    }();
+    const uint32_t kMaxFrames = 1u << 20;   // frames per chunk (descriptor block <= 40 MiB)
+    constexpr int kSlots = (int)(sizeof(e->ms) / sizeof(e->ms[0]));
+    static_assert(kSlots >= 4, "a chunk's staging is live for three steps, plus the upload ahead");
+    HostStats hst;
+    const double t_call = hst.on ? HostStats::now() : 0;
+    DeviceGuard g(e->device);
+    for (auto &m : e->ms)
+        if (int rc = mslot_reserve(m, 0, 0)) return rc;
+    if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
+    hipStream_t ms = e->map_stream;
+    // the move stream starts after work already queued on the engine stream
+    HIP_TRY(hipEventRecord(e->ms[0].ciphered, e->stream));
+    HIP_TRY(hipStreamWaitEvent(ms, e->ms[0].ciphered, 0));
+    struct Chunk {
+        uint32_t first = 0, cnt = 0;  // cnt = 0: no chunk in the slot
+        bool uniform = false;
+        uint64_t out_at = 0, desc_at = 0, desc_b = 0;
+    } ch[kSlots];
+    auto jobs_of = [&](int slot, MoveJob &gather, MoveJob &scatter) {
+        const Chunk &c = ch[slot];
+        MapSlot &m = e->ms[slot];
+        const uint64_t *d_src = reinterpret_cast<const uint64_t *>(m.d + c.desc_at);
+        const uint64_t *d_so = d_src + c.cnt, *d_dst = d_so + c.cnt, *d_oo = d_dst + c.cnt;
+        const uint32_t *d_len = reinterpret_cast<const uint32_t *>(d_oo + c.cnt);
+        gather = MoveJob{0, d_src, (uint64_t)(uintptr_t)m.d, d_so, d_len, 0, c.cnt};
+        scatter = MoveJob{(uint64_t)(uintptr_t)(m.d + c.out_at), d_oo, 0, d_dst, d_len, (uint32_t)pre, c.cnt};
+    };
+    uint32_t si = 0;
+    bool stop = false;  // a frame outside registered memory ended the mapped chunks
+    // host: the descriptors of chunk t into its slot's pinned block (false: no chunk t)
+    auto prepare = [&](uint64_t t, int &rc) -> bool {
+        const int k = (int)(t % kSlots);
+        Chunk &c = ch[k];
+        c.cnt = 0;
+        if (si >= n || stop) return false;
+        MapSlot &m = e->ms[k];
+        if (m.busy) {  // the slot's previous pinned block went H2D
+            const double tw = hst.on ? HostStats::now() : 0;
+            if (hipError_t err = hipEventSynchronize(m.done)) {
+                rc = hip_fail(err, "hipEventSynchronize");
+                return false;
+            }
+            if (hst.on) hst.wait += HostStats::now() - tw;
+            m.busy = false;
+        }
+        const double tf = hst.on ? HostStats::now() : 0;
+        uint64_t in_b = 0;
+        uint32_t j = si;
+        while (j < n && (j == si || (in_b + frames[j].len <= kChunk && j - si < kMaxFrames))) in_b += frames[j++].len;
+        uint32_t cnt = j - si;
+        const fpnn_aes_host_frame *fr = frames + si;
+        // every frame of the chunk inside registered memory?  The chunk ends before the
+        // first one that is not (the caller takes the rest through the staged path).
+        {
+            const unsigned parts = cnt >= 16384 ? pool_of(e)->parts() : 1u;
+            std::atomic<uint32_t> bad{cnt};
+            pool_of(e)->run(parts, [&](unsigned p) {
+                const uint32_t a0 = (uint32_t)((uint64_t)cnt * p / parts), b0 = (uint32_t)((uint64_t)cnt * (p + 1) / parts);
+                long rs = -1, rd = -1;
+                for (uint32_t q = a0; q < b0; q++) {
+                    const fpnn_aes_host_frame &f = fr[q];
+                    const uintptr_t xs = (uintptr_t)f.src, xd = (uintptr_t)f.dst;
+                    bool ok = true;
+                    if (f.len && (rs < 0 || xs < v.lo[rs] || xs + f.len > v.hi[rs])) ok = (rs = v.find(f.src, f.len)) >= 0;
+                    if (ok && f.len + pre && (rd < 0 || xd < v.lo[rd] || xd + f.len + pre > v.hi[rd]))
+                        ok = (rd = v.find(f.dst, f.len + pre)) >= 0;
+                    if (!ok) {
+                        uint32_t cur = bad.load();
+                        while (q < cur && !bad.compare_exchange_weak(cur, q)) {
+                        }
+                        return;
+                    }
+                }
+            });
+            if (bad.load() < cnt) {
+                cnt = bad.load();
+                j = si + cnt;
+                in_b = 0;
+                for (uint32_t q = 0; q < cnt; q++) in_b += fr[q].len;
+                stop = true;  // no chunk after this one
+                if (!cnt) return false;
+            }
+        }
+        const uint64_t out_b = in_b + pre * cnt;
+        const uint64_t in_pad = (in_b + 255) & ~255ull, out_pad = (out_b + 255) & ~255ull;
+        c.first = si;
+        c.out_at = in_pad;
+        c.desc_at = in_pad + out_pad;
+        c.desc_b = (uint64_t)cnt * 40;
+        if (c.desc_at + c.desc_b + 64 > m.dcap || c.desc_b + 64 > m.hcap) {
+            // growing frees the slot's buffers: let every queued use of them finish
+            hipError_t err = hipStreamSynchronize(ms);
+            if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+            if (err != hipSuccess) {
+                rc = hip_fail(err, "hipStreamSynchronize");
+                return false;
+            }
+            if ((rc = mslot_reserve(m, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
+        }
+        // descriptor block (same layout in h and at d + desc_at):
+        //   src u64 | so u64 | dst u64 | oo u64 | len u32 | slot u32   (cnt entries each)
+        uint64_t *h_src = reinterpret_cast<uint64_t *>(m.h);
+        uint64_t *h_so = h_src + cnt, *h_dst = h_so + cnt, *h_oo = h_dst + cnt;
+        uint32_t *h_len = reinterpret_cast<uint32_t *>(h_oo + cnt), *h_slot = h_len + cnt;
+        const unsigned parts = cnt >= 16384 ? pool_of(e)->parts() : 1u;
+        uint64_t psum[64 + 1] = {0};
+        uint8_t same[64];
+        auto range = [&](unsigned p, uint32_t &a0, uint32_t &b0) {
+            a0 = (uint32_t)((uint64_t)cnt * p / parts);
+            b0 = (uint32_t)((uint64_t)cnt * (p + 1) / parts);
+        };
+        pool_of(e)->run(parts, [&](unsigned p) {
+            uint32_t a0, b0;
+            range(p, a0, b0);
+            uint64_t sum = 0;
+            bool eq = true;
+            for (uint32_t q = a0; q < b0; q++) {
+                sum += fr[q].len;
+                eq = eq && fr[q].len == fr[0].len;
+            }
+            psum[p + 1] = sum;
+            same[p] = eq;
+        });
+        c.uniform = true;
+        for (unsigned p = 0; p < parts; p++) {
+            psum[p + 1] += psum[p];
+            c.uniform = c.uniform && same[p];
+        }
+        pool_of(e)->run(parts, [&](unsigned p) {
+            uint32_t a0, b0;
+            range(p, a0, b0);
+            uint64_t io = psum[p], oo = psum[p] + pre * a0;
+            long rs = -1, rd = -1;  // last range hit (frames of one arena: one search each)
+            for (uint32_t q = a0; q < b0; q++) {
+                const fpnn_aes_host_frame &f = fr[q];
+                uint64_t sa = 0, da = 0;
+                if (f.len) {
+                    const uintptr_t x = (uintptr_t)f.src;
+                    if (rs < 0 || x < v.lo[rs] || x + f.len > v.hi[rs]) rs = v.find(f.src, f.len);
+                    sa = (uint64_t)((intptr_t)x + v.delta[rs]);
+                }
+                if (f.len + pre) {
+                    const uintptr_t x = (uintptr_t)f.dst;
+                    if (rd < 0 || x < v.lo[rd] || x + f.len + pre > v.hi[rd]) rd = v.find(f.dst, f.len + pre);
+                    da = (uint64_t)((intptr_t)x + v.delta[rd]);
+                }
+                h_src[q] = sa;
+                h_so[q] = io;
+                h_dst[q] = da;
+                h_oo[q] = oo;
+                h_len[q] = f.len;
+                h_slot[q] = f.key_slot;
+                io += f.len;
+                oo += f.len + pre;
+            }
+        });
+        c.cnt = cnt;
+        si = j;
+        if (hst.on) hst.gather += HostStats::now() - tf;  // (descriptor fill)
+        return true;
+    };
+    // engine stream: chunk t's descriptors H2D; `done` doubles as "descriptors on the device"
+    auto upload = [&](uint64_t t) -> int {
+        const int k = (int)(t % kSlots);
+        MapSlot &m = e->ms[k];
+        HIP_TRY(hipMemcpyAsync(m.d + ch[k].desc_at, m.h, ch[k].desc_b, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipEventRecord(m.done, e->stream));
+        m.busy = true;
+        return FPNN_AES_OK;
+    };
+    int rc = FPNN_AES_OK;
+    if (prepare(0, rc)) rc = upload(0);
+    const MoveJob none{0, nullptr, 0, nullptr, nullptr, 0, 0};
+    for (uint64_t t = 0; rc == FPNN_AES_OK; t++) {
+        const int kt = (int)(t % kSlots), k1 = (int)((t + kSlots - 1) % kSlots), k2 = (int)((t + kSlots - 2) % kSlots);
+        const bool gather_t = ch[kt].cnt != 0;
+        const bool cipher_t1 = t >= 1 && ch[k1].cnt != 0;
+        const bool scatter_t2 = t >= 2 && ch[k2].cnt != 0;
+        if (!gather_t && !cipher_t1 && !scatter_t2) break;
+        // move stream: gather t || scatter t - 2
+        MoveJob gj = none, sj = none, tmp;
+        if (gather_t) {
+            HIP_TRY(hipStreamWaitEvent(ms, e->ms[kt].done, 0));
+            jobs_of(kt, gj, tmp);
+        }
+        if (scatter_t2) {
+            HIP_TRY(hipStreamWaitEvent(ms, e->ms[k2].ciphered, 0));
+            jobs_of(k2, tmp, sj);
+        }
+        HIP_TRY(launch_move_segments(gj, sj, ms));
+        if (gather_t) HIP_TRY(hipEventRecord(e->ms[kt].gathered, ms));
+        // host: chunk t + 1's descriptors while the GPU moves
+        const bool next = prepare(t + 1, rc);
+        if (rc) break;
+        // engine stream: cipher t - 1, then upload chunk t + 1 (its slot's previous chunk,
+        // t - 3, was scattered by step t - 1's launch, which the cipher waited for)
+        if (cipher_t1) {
+            const Chunk &c = ch[k1];
+            MapSlot &m = e->ms[k1];
+            HIP_TRY(hipStreamWaitEvent(e->stream, m.gathered, 0));
+            MoveJob gq, sq;
+            jobs_of(k1, gq, sq);
+            fpnn_aes_batch bt;
+            memset(&bt, 0, sizeof bt);
+            bt.in = m.d;
+            bt.out = m.d + c.out_at;
+            bt.count = c.cnt;
+            bt.keys = keys;
+            bt.flags = pre ? FPNN_AES_F_WIRE_PREFIX : 0u;
+            if (c.uniform && !pre) {  // dense uniform staging: the K2 / K1d fast paths
+                bt.stride = frames[c.first].len;
+                bt.uniform_len = frames[c.first].len;
+            } else {
+                bt.in_off = gq.doff;
+                bt.out_off = sq.soff;
+                bt.len = gq.len;
+            }
+            if (keys->count > 1) bt.key_slot = gq.len + c.cnt;
+            rc = encrypt ? run_encrypt(e, &bt, nullptr, nullptr, false) : run_decrypt(e, &bt, nullptr, nullptr, false);
+            if (rc) break;
+            HIP_TRY(hipEventRecord(m.ciphered, e->stream));
+        }
+        // (chunk t + 1 exists only if chunk t - 1 does, for t >= 1: the upload always
+        // follows a cipher; at t = 0 the slot is unused)
+        if (next && (rc = upload(t + 1))) break;
+        if (scatter_t2) ch[k2].cnt = 0;  // (its slot's next chunk is prepared at step t + 1)
+    }
+    const double td = hst.on ? HostStats::now() : 0;
+    HIP_TRY(hipStreamSynchronize(ms));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (auto &m : e->ms) m.busy = false;
+    for (auto &c : ch) c.cnt = 0;
+    *done = si;
+    e->host_path = "host_mapped";
+    if (hst.on)
+        fprintf(stderr, "[fpnn_aes host] mapped %s: %u frames, %.2f ms total, descriptors %.2f, slot waits %.2f, "
+                "final drain %.2f ms, chunk %llu MiB\n", encrypt ? "encrypt" : "decrypt", n,
+                1e3 * (HostStats::now() - t_call), 1e3 * hst.gather, 1e3 * hst.wait, 1e3 * (HostStats::now() - td),
+                (unsigned long long)(kChunk >> 20));
+    return rc;
+}
+
+bool mapped_enabled() {
+    const char *v = getenv("FPNN_AES_HOST_MAPPED");
+    return !v || atoi(v) != 0;
+}
+
 }  // namespace
 
 int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
@@ -1496,7 +1871,62 @@ int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_f
         for (uint32_t i = 0; i < n; i++)
             if (!frames[i].dst) return FPNN_AES_ERR_ARG;
     if (!n) return FPNN_AES_OK;
+    if (mapped_enabled()) {  // every frame in registered host memory: the GPU moves the bytes
+        MapView v;
+        if (int rc = map_view(e->device, v)) return rc;
+        const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
+        if (!v.lo.empty() && (!frames[0].len || v.find(frames[0].src, frames[0].len) >= 0) &&
+            (!(frames[0].len + pre) || v.find(frames[0].dst, frames[0].len + pre) >= 0)) {
+            // frames in registered memory from the first on: mapped until the first frame
+            // that is not, the rest (if any) staged -- package frames are independent
+            uint32_t done = 0;
+            if (int rc = mapped_pipeline(e, encrypt != 0, frames, n, keys, flags, v, &done)) return rc;
+            if (done == n) return FPNN_AES_OK;
+            frames += done;
+            n -= done;
+            const int rc = host_pipeline(e, encrypt != 0, false, frames, n, keys, flags, nullptr, nullptr);
+            if (done) e->host_path = "host_mapped+staged";
+            return rc;
+        }
+    }
     return host_pipeline(e, encrypt != 0, false, frames, n, keys, flags, nullptr, nullptr);
+}
+
+int fpnn_aes_host_register(void *ptr, size_t len) {
+    if (!ptr || !len) return FPNN_AES_ERR_ARG;
+    const uintptr_t lo = (uintptr_t)ptr, hi = lo + len;
+    if (hi < lo) return FPNN_AES_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    auto it = std::lower_bound(g_mapped.begin(), g_mapped.end(), lo,
+                               [](const MappedRange &r, uintptr_t x) { return r.lo < x; });
+    if ((it != g_mapped.end() && it->lo < hi) || (it != g_mapped.begin() && std::prev(it)->hi > lo)) {
+        g_last_error = "fpnn_aes_host_register: range overlaps a registered range";
+        return FPNN_AES_ERR_ARG;
+    }
+    HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterPortable | hipHostRegisterMapped));
+    MappedRange r;
+    r.lo = lo;
+    r.hi = hi;
+    for (auto &d : r.delta) d = INTPTR_MIN;
+    g_mapped.insert(it, r);
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_host_unregister(void *ptr) {
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    auto it = std::find_if(g_mapped.begin(), g_mapped.end(), [ptr](const MappedRange &r) { return r.lo == (uintptr_t)ptr; });
+    if (it == g_mapped.end()) return FPNN_AES_ERR_ARG;
+    g_mapped.erase(it);
+    HIP_TRY(hipHostUnregister(ptr));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_host_is_mapped(const void *ptr, size_t len) {
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    const uintptr_t p = (uintptr_t)ptr;
+    for (const auto &r : g_mapped)
+        if (p >= r.lo && p + len <= r.hi && p + len >= p) return 1;
+    return 0;
 }
 
 int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
@@ -1617,7 +2047,8 @@ int fpnn_aes_engine_kernel_stats(fpnn_aes_engine *e, int which, uint64_t *launch
 }
 
 const char *fpnn_aes_engine_last_kernel(fpnn_aes_engine *e, int which) {
-    if (!e || which < 0 || which > 1) return "";
+    if (!e || which < 0 || which > 2) return "";
+    if (which == FPNN_AES_K_HOST) return e->host_path;
     return e->last_kernel[which];
 }
 

@@ -325,4 +325,75 @@ hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, u
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Host-mapped frame moves (fpnn_aes_package_host over registered host memory, §8f row 1).
+// A MoveJob copies n segments, segment i from address sbase + soff[i] to dbase + doff[i],
+// len[i] + extra bytes: the gather of frames from host socket buffers into contiguous HBM
+// staging (sbase = 0, soff = device-visible host addresses) or the scatter of results back
+// (dbase = 0).  The GPU moves the bytes over PCIe itself: no CPU copy, no pinned bounce
+// buffer.  One launch runs TWO jobs -- the gather of chunk t and the scatter of chunk
+// t - 2 -- with their segment groups interleaved over the waves, so both link directions
+// are busy inside one kernel (separate gather and scatter launches on two streams, many
+// per call, overlapped only partially on MI355X: tools/probe/hostmap_bw.hip).
+// A wave moves a group of F segments per step in 1 KiB pieces, lane l taking bytes
+// [16l, 16l + 16) of a piece (unaligned dwordx4; byte copies for the lane that straddles
+// a segment's end); all F pieces' loads go out before their stores.
+template <int F>
+__device__ __forceinline__ void move_group(const MoveJob &J, uint64_t g, uint32_t lane) {
+    const uint8_t *src[F];
+    uint8_t *dst[F];
+    uint32_t L[F];
+    uint32_t maxl = 0;
+#pragma unroll
+    for (int k = 0; k < F; k++) {
+        const uint64_t i = g * F + k;
+        L[k] = i < J.n ? J.len[i] + J.extra : 0u;
+        src[k] = reinterpret_cast<const uint8_t *>(i < J.n ? J.sbase + J.soff[i] : J.sbase);
+        dst[k] = reinterpret_cast<uint8_t *>(i < J.n ? J.dbase + J.doff[i] : J.dbase);
+        maxl = L[k] > maxl ? L[k] : maxl;
+    }
+    for (uint32_t p = 0; p < maxl; p += 1024) {
+        const uint32_t b = p + 16 * lane;
+        uint4 v[F];
+#pragma unroll
+        for (int k = 0; k < F; k++) v[k] = b + 16 <= L[k] ? load16(src[k] + b) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < F; k++) {
+            if (b + 16 <= L[k]) {
+                store16(dst[k] + b, v[k]);
+            } else if (b < L[k]) {
+                for (uint32_t j = b; j < L[k]; j++) dst[k][j] = src[k][j];
+            }
+        }
+    }
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void k_move_segments(MoveJob a, MoveJob b) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+    const uint64_t ga = (a.n + F - 1) / F, gb = (b.n + F - 1) / F;
+    const uint64_t both = 2 * (ga < gb ? ga : gb);  // virtual groups [0, both) alternate a, b
+    for (uint64_t v = w; v < ga + gb; v += nw) {
+        if (v < both) {
+            if (v & 1) move_group<F>(b, v >> 1, lane); else move_group<F>(a, v >> 1, lane);
+        } else if (ga > gb) {
+            move_group<F>(a, v - both / 2, lane);
+        } else {
+            move_group<F>(b, v - both / 2, lane);
+        }
+    }
+}
+
+hipError_t launch_move_segments(const MoveJob &a, const MoveJob &b, hipStream_t st) {
+    const uint64_t groups = (a.n + 3) / 4 + (b.n + 3) / 4;
+    if (!groups) return hipSuccess;
+    // 256 x 256 threads: 1024 waves x 4 KiB in flight saturate the link (more waves only
+    // slow the opposite direction)
+    const int grid = grid_for(groups, 4, 256);
+    hipLaunchKernelGGL((k_move_segments<4>), dim3(grid), dim3(256), 0, st, a, b);
+    return hipGetLastError();
+}
+
 }  // namespace fpnn_aes

@@ -154,6 +154,20 @@ struct ModeArgs {
 hipError_t launch_block_modes(const ModeArgs &a, int nrounds, int mode, int num_cus, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
+// Host-mapped frame moves: a job copies n segments, segment i from address sbase + soff[i]
+// to dbase + doff[i], len[i] + extra bytes (soff/doff/len device arrays; either side may be
+// mapped host memory; a base of 0 makes the offsets absolute device-visible addresses).
+// One launch runs two jobs concurrently (n = 0: none).
+struct MoveJob {
+    uint64_t sbase;
+    const uint64_t *soff;
+    uint64_t dbase;
+    const uint64_t *doff;
+    const uint32_t *len;
+    uint32_t extra;
+    uint32_t n;
+};
+hipError_t launch_move_segments(const MoveJob &a, const MoveJob &b, hipStream_t st);
 hipError_t launch_fill_synthetic(uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset, int grid,
                                  hipStream_t st);
 

@@ -357,6 +357,21 @@ class Engine:
         check(lib.fpnn_aes_stream_decrypt(self._h, C.byref(d), _ptr(iv_state), _ptr(pos_state)), "stream_decrypt")
 
 
+def host_register(buf: np.ndarray):
+    """fpnn_aes_host_register over a numpy buffer's memory (e.g. a socket-buffer arena):
+    package_host calls whose frames all lie in registered memory are then moved by the GPU
+    over PCIe (no host gather/scatter).  Keep `buf` alive until host_unregister(buf)."""
+    check(lib.fpnn_aes_host_register(C.c_void_p(buf.ctypes.data), buf.nbytes), "host_register")
+
+
+def host_unregister(buf: np.ndarray):
+    check(lib.fpnn_aes_host_unregister(C.c_void_p(buf.ctypes.data)), "host_unregister")
+
+
+def host_is_mapped(addr: int, nbytes: int) -> bool:
+    return bool(lib.fpnn_aes_host_is_mapped(C.c_void_p(addr), nbytes))
+
+
 def package_host_multi(engines, keysets, encrypt: bool, frames_np, wire_prefix: bool = False):
     """fpnn_aes_package_host_multi: one host-frame batch split byte-balanced over engines
     (keysets[k] on engines[k])."""

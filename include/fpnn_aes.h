@@ -212,6 +212,21 @@ int fpnn_aes_stream_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_k
                                int encrypt, const fpnn_aes_host_frame *frames, uint32_t n, uint8_t *iv_state,
                                uint32_t *pos_state);
 
+/* ---- host-mapped frames (zero-copy host-frame path) --------------------------------- */
+/* Register [ptr, ptr + len) of host memory -- e.g. the arena a server allocates its
+ * connections' socket buffers from -- with every GPU (hipHostRegister, portable + mapped;
+ * the pages are locked).  fpnn_aes_package_host / _multi calls whose frames all lie in
+ * registered memory (src: len bytes, dst: len (+4 with the wire prefix) bytes) are then
+ * moved by the GPU itself over PCIe: no host gather/scatter and no pinned bounce copy;
+ * the host threads only write 40 bytes of descriptor per frame.  A call whose frames
+ * leave registered memory from frame k on runs frames [k, n) through the staged path;
+ * calls that start outside it are staged entirely.  Ranges must not overlap; registration is process-wide.
+ * Unregister only while no call uses the range. */
+int fpnn_aes_host_register(void *ptr, size_t len);
+int fpnn_aes_host_unregister(void *ptr);
+/* 1 if [ptr, ptr + len) lies inside one registered range, else 0. */
+int fpnn_aes_host_is_mapped(const void *ptr, size_t len);
+
 /* ---- receive side: wire framing on the device (§8f row 3) --------------------------- */
 /* Per received segment (the bytes one connection delivered), the outcome of walking its
  * frames: `frames` complete frames cover the first `consumed` bytes; the rest is an
@@ -269,6 +284,8 @@ int fpnn_aes_engine_reset_stats(fpnn_aes_engine *e);
 const char *fpnn_aes_engine_last_kernel(fpnn_aes_engine *e, int which);
 #define FPNN_AES_K_DECRYPT 0
 #define FPNN_AES_K_ENCRYPT 1
+#define FPNN_AES_K_HOST 2 /* last_kernel only: the last host-frame call's path, "host_mapped",
+                           "host_staged" or "host_mapped+staged" */
 
 /* Version string of the built library (kernel variant + build flags). */
 const char *fpnn_aes_version(void);
