@@ -395,6 +395,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     while (threads < kThreads && (uint64_t)threads * slots < b->count) threads *= 2;
     const uint64_t want = (b->count + threads - 1) / threads;
     const int grid = (int)(want < slots ? (want ? want : 1) : slots);
+    if (e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
     HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, threads, e->stream));
@@ -573,6 +574,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
+    if (const char *v = getenv("FPNN_AES_ENC_ALIGN")) e->variant.enc_align = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;

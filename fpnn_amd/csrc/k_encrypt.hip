@@ -69,7 +69,22 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         uint32_t i = 0;
         // Per-lane AES-256 round keys (60 VGPRs) leave room for 4-block chunks only.
         constexpr int C = (KM == KEY_LANE && NR == 14 && CH > 4) ? 4 : CH;
-        if (C > 1 && nfull >= C) {
+        if (C > 1 && (b.flags & F_ALIGN_CHUNKS)) {
+            // a 16-B aligned segment that starts inside a 128-B line (1472-B datagrams:
+            // every other one) runs its first blocks singly, so every chunk below reads
+            // and writes whole lines (a chunk straddling two lines leaves half of each
+            // to a later chunk, by which time L2 has often dropped it: re-read from HBM)
+            const uint32_t mis = (uint32_t)(uintptr_t)p & 127u;
+            uint32_t h = (mis & 15u) ? 0u : ((128u - mis) & 127u) >> 4;
+            h = h < nfull ? h : nfull;
+            for (; i < h; i++) {
+                iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ load16(p);
+                store16(q, iv);
+                p += 16;
+                q += 16;
+            }
+        }
+        if (C > 1 && i + C <= nfull) {
             // C-block chunks (C*16 = 64 or 128 bytes): a chunk's loads and its stores
             // each go out back to back, so every cache line is read and written whole
             // while it is in L2; the next chunk's loads are in flight during this

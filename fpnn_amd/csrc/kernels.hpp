@@ -10,6 +10,7 @@
 namespace fpnn_aes {
 
 constexpr uint32_t F_WIRE_PREFIX = 0x1u;
+constexpr uint32_t F_ALIGN_CHUNKS = 0x100u;  // internal (engine -> K2): line-align the chunks of each chain
 
 // Kernel-side view of one batch (passed by value as the kernel argument).
 struct KBatch {
@@ -57,6 +58,7 @@ enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 struct Variant {
     int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
     int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
+    int enc_align = 1;     // K2: run a chain's blocks before its first 128-B line boundary singly
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
     int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
