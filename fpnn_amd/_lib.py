@@ -18,7 +18,8 @@ import subprocess
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libfpnn_aes.so")
+# FPNN_AES_LIB: another build of the library (A/B of two builds in one session; tools only)
+LIB_PATH = os.environ.get("FPNN_AES_LIB") or os.path.join(PKG_DIR, "libfpnn_aes.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 OK = 0

@@ -311,10 +311,67 @@ __device__ __forceinline__ uint4 load_bytes(const uint8_t *base, int lo, int hi)
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Byte shifts of a 16-byte block by a per-lane count n in [0, 16]: shr_bytes gives
+// byte j = v byte (j + n), shl_bytes byte j = v byte (j - n); zeros shifted in.
+__device__ __forceinline__ uint4 shr_bytes(const uint4 &v, int n) {
+    uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    if (n >= 8) {
+        lo = n >= 16 ? 0ull : hi >> (8 * (n - 8));
+        hi = 0;
+    } else if (n > 0) {
+        lo = (lo >> (8 * n)) | (hi << (64 - 8 * n));
+        hi >>= 8 * n;
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+__device__ __forceinline__ uint4 shl_bytes(const uint4 &v, int n) {
+    uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    if (n >= 8) {
+        hi = n >= 16 ? 0ull : lo << (8 * (n - 8));
+        lo = 0;
+    } else if (n > 0) {
+        hi = (hi << (8 * n)) | (lo >> (64 - 8 * n));
+        lo <<= 8 * n;
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+typedef uint2 __attribute__((aligned(1))) uint2_ua;
+typedef uint32_t __attribute__((aligned(1))) uint32_ua;
+typedef uint16_t __attribute__((aligned(1))) uint16_ua;
+
+// Bytes [lo, hi) of v to base + lo .. base + hi - 1, nothing else written: the range goes
+// out as 8-, 4-, 2- and 1-byte stores (at most four instead of up to sixteen byte stores;
+// gfx950 global stores tolerate any alignment).
 __device__ __forceinline__ void store_bytes(uint8_t *base, const uint4 &v, int lo, int hi) {
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (j >= lo && j < hi) base[j] = (uint8_t)byte_of(v, j);
+    if (lo >= hi) return;
+    uint4 s = shr_bytes(v, lo);  // byte 0 = v byte lo
+    uint8_t *p = base + lo;
+    const int n = hi - lo;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Walign-mismatch"
+    if (n == 16) {
+        store16(p, s);
+        return;
+    }
+    if (n & 8) {
+        *reinterpret_cast<uint2_ua *>(p) = make_uint2(s.x, s.y);
+        p += 8;
+        s = make_uint4(s.z, s.w, 0u, 0u);
+    }
+    if (n & 4) {
+        *reinterpret_cast<uint32_ua *>(p) = s.x;
+        p += 4;
+        s = make_uint4(s.y, s.z, s.w, 0u);
+    }
+    if (n & 2) {
+        *reinterpret_cast<uint16_ua *>(p) = (uint16_t)s.x;
+        p += 2;
+        s.x >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)s.x;
+#pragma clang diagnostic pop
 }
 
 // Lane l receives lane (l-1)'s value (lane 0 receives `fill`): DPP wave_shr:1.

@@ -268,7 +268,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         }
         const int64_t lo = 16 * (int64_t)X.bi - X.n0;  // the block's first byte in the segment
         X.full = lo >= 0 && lo + 16 <= (int64_t)X.len;
-        X.x = load16(X.full ? X.in + lo : dummy);  // edge blocks are built in process()
+        // Edge blocks of segments of 16+ bytes load the 16 segment bytes nearest to them
+        // (the first 16 for a head block, the last 16 for a tail block) and process()
+        // shifts them into place; edge blocks of shorter segments are built bytewise there.
+        const int64_t at = X.full ? lo : lo < 0 ? 0 : (int64_t)X.len - 16;
+        X.x = load16(X.full || X.len >= 16 ? X.in + at : dummy);
         return X;
     };
 
@@ -285,10 +289,21 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
             }
         }
         if (__builtin_amdgcn_ballot_w64(X.valid && !X.full) != 0) {  // segment edges: byte-exact block
-            if (X.valid && !X.full) X.x = load_cx(Seg{X.in, X.out, X.len, X.slot}, X.n0, X.bi, ivs);
-            // drain here, inside the rare branch: the merge below then carries no pending
-            // load, and the common path keeps its prefetches in flight
-            __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+            if (X.valid && !X.full && X.len >= 16) {
+                // head block (bi 0 at position n0 > 0): segment bytes [0, 16 - n0) at n0..15,
+                // the carried ivec below them; tail block: the last hi bytes at 0..hi-1
+                const int hi = (int)((int64_t)X.n0 + X.len - 16 * (int64_t)X.bi);
+                if (X.bi == 0 && X.n0 != 0)
+                    X.x = select_bytes(byte_mask(0, (int)X.n0), ivs, shl_bytes(X.x, (int)X.n0));
+                else
+                    X.x = shr_bytes(X.x, 16 - hi);
+            }
+            if (__builtin_amdgcn_ballot_w64(X.valid && !X.full && X.len < 16) != 0) {
+                if (X.valid && !X.full && X.len < 16) X.x = load_cx(Seg{X.in, X.out, X.len, X.slot}, X.n0, X.bi, ivs);
+                // drain here, inside the rare branch: the merge below then carries no pending
+                // load, and the common path keeps its prefetches in flight
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+            }
         }
         uint4 kin = make_uint4(wave_shr1(X.x.x, f.x), wave_shr1(X.x.y, f.y), wave_shr1(X.x.z, f.z),
                                wave_shr1(X.x.w, f.w));

@@ -56,7 +56,16 @@ __device__ __forceinline__ uint4 load_cx(const Seg &g, uint32_t n0, uint32_t bi,
     const int hi = hi64 > 16 ? 16 : (int)hi64;
     const uint8_t *base = g.in + (vlo - (int64_t)n0);
     if (lo == 0 && hi == 16) return load16(base);
-    uint4 d = load_bytes(base, lo, hi);
+    uint4 d;
+    if (g.len >= 16) {
+        // An edge block of a segment of 16+ bytes: one 16-byte load that stays inside the
+        // segment, shifted into place -- the head block (lo = n0 > 0, hi = 16) holds
+        // segment bytes [0, 16 - lo) at positions lo.., the tail block (lo = 0) the
+        // segment's last hi bytes at 0..hi-1 -- instead of up to sixteen byte loads.
+        d = lo != 0 ? shl_bytes(load16(g.in), lo) : shr_bytes(load16(g.in + g.len - 16), 16 - hi);
+    } else {
+        d = load_bytes(base, lo, hi);
+    }
     if (lo != 0) d = select_bytes(byte_mask(0, lo), ivs, d);
     return d;
 }
