@@ -1,0 +1,628 @@
+// PROBE (not built into the product): K2q with the next chain prefetched one dependent link per chunk
+// step and wave-batched tickets.  Parity green, measured slower on C4 (630 vs 700 GiB/s).
+// k_encrypt.hip -- CFB-128 encryption kernels for gfx950 (see segments.hpp for the
+// segment semantics and aes_device.hpp for the LDS T-table round function).
+//   K2  k_cfb_encrypt_chains : one lane per packet / stream chain.
+//        C_i = P_i ^ E(C_{i-1}) is serial inside a chain (base/rijndael.c:1176-1185),
+//        so parallelism is across packets (package mode) or streams (stream mode).
+//   K2c k_cfb_encrypt_coop   : one lane quad per chain (few / long chains).
+//   K2q k_cfb_encrypt_queue  : K2c with a work queue (many ragged chains).
+//   All are persistent: workgroups walk the chains with a grid stride or the queue.
+#include "segments.hpp"
+
+namespace fpnn_aes {
+
+// ---------------------------------------------------------------------------
+// K2: encryption, one lane per chain.
+
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT, int CH>
+__global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_encrypt_chains(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+
+    RoundKeys<NR> rku;
+    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        RoundKeys<NR> rk;
+        if (KM == KEY_UNIFORM)
+            rk = rku;
+        else
+            rk = load_round_keys<NR>(key);
+
+        uint4 iv;
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = ld_state_iv(b.iv_state + 16 * s);
+            n = b.pos_state[s];
+        } else {
+            iv = *reinterpret_cast<const uint4 *>(key->iv);
+        }
+        const uint8_t *p = g.in;
+        uint8_t *q = g.out;
+        uint32_t rem = g.len;
+
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
+            q[0] = (uint8_t)rem;
+            q[1] = (uint8_t)(rem >> 8);
+            q[2] = (uint8_t)(rem >> 16);
+            q[3] = (uint8_t)(rem >> 24);
+            q += 4;
+        }
+
+        if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = (int)n, hi = (int)(n + take);
+            const uint4 o = load_bytes(p - n, lo, hi) ^ iv;
+            store_bytes(q - n, o, lo, hi);
+            iv = select_bytes(byte_mask(lo, hi), o, iv);
+            p += take;
+            q += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+
+        const uint32_t nfull = rem >> 4;
+        uint32_t i = 0;
+        // Per-lane AES-256 round keys (60 VGPRs) leave room for 4-block chunks only.
+        constexpr int C = (KM == KEY_LANE && NR == 14 && CH > 4) ? 4 : CH;
+        if (C > 1 && (b.flags & F_ALIGN_CHUNKS)) {
+            // a 16-B aligned segment that starts inside a 128-B line (1472-B datagrams:
+            // every other one) runs its first blocks singly, so every chunk below reads
+            // and writes whole lines (a chunk straddling two lines leaves half of each
+            // to a later chunk, by which time L2 has often dropped it: re-read from HBM)
+            const uint32_t mis = (uint32_t)(uintptr_t)p & 127u;
+            uint32_t h = (mis & 15u) ? 0u : ((128u - mis) & 127u) >> 4;
+            h = h < nfull ? h : nfull;
+            for (; i < h; i++) {
+                iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ load16(p);
+                store16(q, iv);
+                p += 16;
+                q += 16;
+            }
+        }
+        if (C > 1 && i + C <= nfull) {
+            // C-block chunks (C*16 = 64 or 128 bytes): a chunk's loads and its stores
+            // each go out back to back, so every cache line is read and written whole
+            // while it is in L2; the next chunk's loads are in flight during this
+            // chunk's rounds.  Ciphertext overwrites the chunk's plaintext registers.
+            // (Two alternating buffers with unconditional loads, which avoid the copy
+            // and the conservative waits below, measured 1.3 % slower.)
+            uint4 a[C];
+#pragma unroll
+            for (int j = 0; j < C; j++) a[j] = load16(p + 16 * j);
+            for (; i + C <= nfull; i += C) {
+                const bool more = i + 2 * C <= nfull;
+                uint4 nx[C];
+#pragma unroll
+                for (int j = 0; j < C; j++) nx[j] = more ? load16(p + 16 * (C + j)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < C; j++) {
+                    iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ a[j];
+                    a[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < C; j++) store16(q + 16 * j, a[j]);
+#pragma unroll
+                for (int j = 0; j < C; j++) a[j] = nx[j];
+                p += 16 * C;
+                q += 16 * C;
+            }
+        }
+        uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
+        for (; i < nfull; i++) {
+            const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
+            iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            store16(q, iv);
+            pt = pn;
+            p += 16;
+            q += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
+            const uint4 ks = aes_encrypt_block<NR, NT>(iv, rk, T);
+            const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
+            store_bytes(q, o, 0, (int)rem);
+            iv = select_bytes(byte_mask(0, (int)rem), o, ks);
+            n = rem;
+        }
+        if (STREAM) {
+            *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = iv;
+            b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2c: encryption, one lane QUAD per chain.  Lane q of the quad owns state column q:
+// per round it does the 4 T-table lookups of its own 4 bytes and the quad sums the
+// contributions with DPP quad_perm (VALU only; aes_encrypt_column below).  A chain
+// therefore issues 4 LDS reads per lane and round instead of 16 -- 4x the lanes per
+// chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
+// lane instead of 60.  Used when chains are few (streams) or long/ragged.
+
+// value held by lane (q + SHIFT) & 3 of this lane's quad.  bound_ctrl: every lane has a
+// source under quad_perm, so no "old" value is needed (update_dpp with old = 0 costs a
+// v_mov per call to materialise it -- 3 of the 12 VALU of a K2c round).
+template <int SHIFT>
+__device__ __forceinline__ uint32_t quad_from(uint32_t v) {
+    constexpr int ctl = ((0 + SHIFT) & 3) | (((1 + SHIFT) & 3) << 2) | (((2 + SHIFT) & 3) << 4) | (((3 + SHIFT) & 3) << 6);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctl, 0xf, 0xf, true);
+}
+
+// XOR of a and the value b holds in lane (q + SHIFT) & 3: one v_xor_b32 with a DPP
+// quad_perm source (the mov_dpp folds into the xor).
+template <int SHIFT>
+__device__ __forceinline__ uint32_t xor_quad_from(uint32_t a, uint32_t b) {
+    return a ^ quad_from<SHIFT>(b);
+}
+
+// Round structure: lane q looks up ITS OWN four bytes -- T0[b0] feeds output column q,
+// T1[b1] column q-1, T2[b2] column q-2, T3[b3] column q-3 -- and the quad then sums
+// the contributions with DPP-sourced XORs.  Per lane and round: 4 v_perm + 4 ds_read
+// + 3 DPP ops + 1 v_bitop3 = 8 VALU, and every DPP operand is an LDS result or a round
+// key, never a fresh VALU result, so no hazard wait states (moving the state words to
+// the neighbours first costs 9 VALU plus an s_nop per round).
+template <int NR, int NT>
+__device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32_t *rkq, const Tables4<NT> &T) {
+    uint32_t s0 = sq ^ rkq[0];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t t0 = T.template t<0>(s0), t1 = T.template t<1>(s0), t2 = T.template t<2>(s0),
+                       t3 = T.template t<3>(s0);
+        // three independent DPP ops whose other operand is an LDS result or a round key
+        // (a chain of DPP xors would need 2 wait states between them), then one xor3
+        s0 = xor3(xor_quad_from<1>(t0, t1), xor_quad_from<2>(rkq[r], t2), quad_from<3>(t3));
+    }
+    // final round: S(byte j) of the own word, masked to byte j, summed the same way
+    const uint32_t m0 = T.template sraw<0>(s0) & 0x000000ffu, m1 = T.template sraw<1>(s0) & 0x0000ff00u,
+                   m2 = T.template sraw<2>(s0) & 0x00ff0000u, m3 = T.template sraw<3>(s0) & 0xff000000u;
+    return xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(rkq[NR], m2), quad_from<3>(m3));
+}
+
+typedef uint32_t __attribute__((aligned(1))) uint32_u;
+
+// bytes [lo, hi) of this lane's word (word covers block bytes [4q, 4q+4))
+__device__ __forceinline__ uint32_t load_word_bytes(const uint8_t *p, int lo, int hi) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) w |= (uint32_t)p[j] << (8 * j);
+    return w;
+}
+
+__device__ __forceinline__ void store_word_bytes(uint8_t *p, uint32_t w, int lo, int hi) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (j >= lo && j < hi) p[j] = (uint8_t)(w >> (8 * j));
+}
+
+__device__ __forceinline__ uint32_t word_mask(int lo, int hi) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) m |= (j >= lo && j < hi) ? (0xffu << (8 * j)) : 0u;
+    return m;
+}
+
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const int q = (int)(threadIdx.x & 3u);
+    constexpr int CH = 8;
+
+    const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; t < b.count; t += nquads) {
+        const uint64_t s = b.perm ? b.perm[t] : t;  // longest chains first (ragged batches)
+        const Seg g = get_seg<LAYOUT>(b, s);
+        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        uint32_t rkq[NR + 1];
+#pragma unroll
+        for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+
+        uint32_t iv;  // this lane's word of the 16-byte feedback register
+        uint32_t n = 0;
+        if (STREAM) {
+            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            n = b.pos_state[s];
+        } else {
+            iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
+        }
+        const uint8_t *p = g.in;
+        uint8_t *o = g.out;
+        uint32_t rem = g.len;
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
+            if (q == 0) store_word_bytes(o, rem, 0, 4);
+            o += 4;
+        }
+        const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+        if (STREAM && n != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - n ? rem : 16 - n;
+            const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
+            if (lo < hi) {
+                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
+                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (iv & ~m);
+            }
+            p += take;
+            o += take;
+            rem -= take;
+            n = (n + take) & 15u;
+        }
+        const uint32_t nfull = rem >> 4;
+        uint32_t i = 0;
+        if (nfull >= CH) {
+            uint32_t a[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo);
+            for (; i + CH <= nfull; i += CH) {
+                const bool more = i + 2 * CH <= nfull;
+                uint32_t nx[CH], c[CH];
+#pragma unroll
+                for (int j = 0; j < CH; j++) nx[j] = more ? *reinterpret_cast<const uint32_u *>(p + 16 * (CH + j) + wlo) : 0u;
+#pragma unroll
+                for (int j = 0; j < CH; j++) {
+                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
+                    c[j] = iv;
+                }
+#pragma unroll
+                for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
+#pragma unroll
+                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                p += 16 * CH;
+                o += 16 * CH;
+            }
+        }
+        for (; i < nfull; i++) {
+            const uint32_t pt = *reinterpret_cast<const uint32_u *>(p + wlo);
+            iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ pt;
+            *reinterpret_cast<uint32_u *>(o + wlo) = iv;
+            p += 16;
+            o += 16;
+        }
+        rem &= 15u;
+        if (rem) {  // partial final block
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const int lo = 0, hi = min((int)rem, wlo + 4) - wlo;
+            if (hi > lo) {
+                const uint32_t c = load_word_bytes(p + wlo, lo, hi) ^ ks;
+                store_word_bytes(o + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                iv = (c & m) | (ks & ~m);
+            } else {
+                iv = ks;
+            }
+            n = rem;
+        }
+        if (STREAM) {
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
+            if (q == 0) b.pos_state[s] = n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2q: K2c's quad-per-chain cipher with a work queue instead of a grid stride.
+// Chains are visited longest first (perm[]); a quad that finishes a chain takes the
+// next one from a global counter at once, so lanes of a wave never wait for the
+// longest chain of their wave (greedy longest-processing-time scheduling).  The loop
+// body is one step of up to CH blocks; a block past the chain's end is computed but not
+// committed (a select, not a branch).  The wave leaves the loop when no quad of it has
+// work.  Used for ragged batches with more chains than quads (C4), where a static
+// chain-to-lane assignment leaves most lanes idle.  (Two chains per quad, round-
+// interleaved, measured 35 % slower on C4: the longest chains, which set the end of the
+// launch, then advance at half speed -- the schedule's critical path is its longest job.)
+//
+// Chain switches are prefetched.  A switch is a chain of dependent loads (ticket ->
+// perm[] -> segment descriptor -> IV / stream state), and while any quad of a wave waits
+// for them the whole wave waits.  So a quad fetches its NEXT chain's descriptor while
+// the current chain runs, one link of that chain per chunk step (the loads of step i are
+// consumed in step i + 1, after the chunk loads of step i have been waited for): at the
+// switch the data is in registers.  A chain shorter than the three steps the fetch takes
+// finishes the fetch synchronously.
+template <int NR, int KM, bool STREAM, int NT, bool FIRST_PRIO = true>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uint32_t *next) {
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const int q = (int)(threadIdx.x & 3u);
+    const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+    constexpr int CH = 8;
+    const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
+
+    uint32_t rkq[NR + 1];
+    uint32_t iv_u = 0;  // package mode, one key: the IV word of this lane
+    if (KM == KEY_UNIFORM) {
+#pragma unroll
+        for (int r = 0; r <= NR; r++) rkq[r] = b.keys[0].rk[4 * r + q];
+        iv_u = reinterpret_cast<const uint32_t *>(b.keys[0].iv)[q];
+    }
+    // current chain
+    uint64_t sid = 0;
+    const uint8_t *p = nullptr;
+    uint8_t *o = nullptr;
+    uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
+    bool active = false;
+    // next chain, fetched ahead: stage 0 = take a ticket, 1 = ticket pending, 2 = chain
+    // index pending, 3 = descriptor pending / ready, 4 = queue exhausted
+    // (every load of a link goes straight into its register -- no same-step use, not even
+    // a copy or a widening -- so nothing waits for it before the next step; the host
+    // guarantees in_off, out_off, len and perm are device arrays)
+    int stage = 0;
+    uint32_t tk = 0, ns = 0;  // tk: quad leader's rank in its wave's ticket batch
+    uint32_t base_v = 0;      // the batch's first ticket, in the issuing lane
+    int issuer = 0;           // (wave-uniform) lane that took the wave's last ticket batch
+    uint64_t n_in = 0, n_out = 0;
+    uint32_t n_len = 0, n_slot = 0, n_word = 0, n_pos = 0;
+
+    auto fetch_step = [&]() {  // advance the prefetch by one link (loads issued, not waited for)
+        if (stage == 2) {      // chain index arrived: its segment descriptor
+            n_in = b.in_off[ns];
+            n_out = b.out_off[ns];
+            n_len = b.len[ns];
+            if (KM != KEY_UNIFORM) n_slot = b.key_slot[ns];
+            if (STREAM) {
+                n_word = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * (uint64_t)ns)[q];
+                n_pos = b.pos_state[ns];
+            }
+            stage = 3;
+        }
+        if (stage == 1) {  // ticket batch arrived: this quad's ticket, its chain index
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)base_v, issuer);
+            const uint64_t nt =
+                (uint64_t)(base + (uint32_t)__builtin_amdgcn_mov_dpp((int)tk, 0x00, 0xf, 0xf, true)) + nquads;
+            if (nt < b.count) {
+                ns = b.perm[nt];
+                stage = 2;
+            } else {
+                stage = 4;
+            }
+        }
+        // stage 0: the quads of the wave that need a ticket take one batch of them with ONE
+        // atomic (the counter is shared by every wave of the launch), each quad its rank
+        // in the batch; the batch's base is read a step later.  (Done by hand: the
+        // compiler's atomic optimizer makes the same single atomic but waits for it at
+        // once; k_encrypt.hip is built with it off.)
+        const uint64_t want = __builtin_amdgcn_ballot_w64(stage == 0 && q == 0);
+        if (want) {
+            const int first = __builtin_ctzll(want);
+            if ((int)(threadIdx.x & 63u) == first) base_v = atomicAdd(next, (uint32_t)__builtin_popcountll(want));
+            issuer = first;
+            if (stage == 0) {
+                tk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+                stage = 1;
+            }
+        }
+    };
+    auto begin = [&](uint64_t s, uint64_t io, uint64_t oo, uint32_t len, uint32_t slot, uint32_t word,
+                     uint32_t pos) {  // start chain s: its head
+        sid = s;
+        if (KM != KEY_UNIFORM) {
+            const DevKey *key = b.keys + slot;
+#pragma unroll
+            for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
+            if (!STREAM) word = reinterpret_cast<const uint32_t *>(key->iv)[q];
+        } else if (!STREAM) {
+            word = iv_u;
+        }
+        uint32_t v = word;
+        const uint8_t *pp = b.in + io;
+        uint8_t *oo8 = b.out + oo;
+        uint32_t rem = len;
+        if (!STREAM) pos = 0;
+        if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
+            if (q == 0) store_word_bytes(oo8, rem, 0, 4);
+            oo8 += 4;
+        }
+        if (STREAM && pos != 0 && rem != 0) {  // rest of the partially used keystream block
+            const uint32_t take = rem < 16 - pos ? rem : 16 - pos;
+            const int lo = max((int)pos, wlo) - wlo, hi = min((int)(pos + take), wlo + 4) - wlo;
+            if (lo < hi) {
+                const uint32_t c = load_word_bytes(pp - pos + wlo, lo, hi) ^ v;
+                store_word_bytes(oo8 - pos + wlo, c, lo, hi);
+                const uint32_t m = word_mask(lo, hi);
+                v = (c & m) | (v & ~m);
+            }
+            pp += take;
+            oo8 += take;
+            rem -= take;
+            pos = (pos + take) & 15u;
+        }
+        iv = v;
+        n = pos;
+        p = pp;
+        o = oo8;
+        nfull = rem >> 4;
+        tail = rem & 15u;
+        active = true;
+    };
+    auto begin_index = [&](uint64_t s) {  // start chain s, descriptor loaded here
+        const uint32_t slot = KM != KEY_UNIFORM ? b.key_slot[s] : 0u;
+        uint32_t word = 0, pos = 0;
+        if (STREAM) {
+            word = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
+            pos = b.pos_state[s];
+        }
+        begin(s, b.in_off[s], b.out_off[s], b.len[s], slot, word, pos);
+    };
+    auto finish = [&]() {  // partial final block and the stream state
+        if (tail) {
+            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const int hi = min((int)tail, wlo + 4) - wlo;
+            if (hi > 0) {
+                const uint32_t c = load_word_bytes(p + wlo, 0, hi) ^ ks;
+                store_word_bytes(o + wlo, c, 0, hi);
+                const uint32_t m = word_mask(0, hi);
+                iv = (c & m) | (ks & ~m);
+            } else {
+                iv = ks;
+            }
+            n = tail;
+        }
+        if (STREAM) {
+            reinterpret_cast<uint32_t *>(b.iv_state + 16 * sid)[q] = iv;
+            if (q == 0) b.pos_state[sid] = n;
+        }
+    };
+    // First chains: the longest (perm[] order) are dealt round-robin over the
+    // workgroups -- quad j of workgroup w takes chain j * gridDim.x + w -- so the few
+    // longest chains, which set the end of the launch, sit on different CUs and in the
+    // first wave of each; that wave runs at raised priority so its chain's rounds are
+    // not queued behind the 15 other waves' (the critical path of a greedy schedule
+    // is its longest job).  Later chains come from the counter (from nquads on).
+    const uint64_t t0 = (uint64_t)(threadIdx.x >> 2) * gridDim.x + blockIdx.x;
+    if (FIRST_PRIO && threadIdx.x < 64) __builtin_amdgcn_s_setprio(2);
+    if (t0 < b.count) begin_index(b.perm[t0]);
+    else stage = 4;
+    while (true) {
+        // a chain with no whole block left: finish it; a quad without a chain starts the
+        // prefetched one if it is in registers (else it idles this step while the fetch
+        // advances: a chain shorter than the fetch)
+        if (active && nfull == 0) {
+            finish();
+            active = false;
+        }
+        if (!active && stage == 3) {
+            begin(ns, n_in, n_out, n_len, n_slot, n_word, n_pos);
+            stage = 0;
+        }
+        if (__builtin_amdgcn_ballot_w64(active || stage != 4) == 0) break;
+        fetch_step();  // (uniform control flow: the ticket batch is a wave-wide ballot)
+        const uint32_t kk = active ? (nfull < CH ? nfull : CH) : 0u;
+        uint32_t a[CH];
+#pragma unroll
+        for (int j = 0; j < CH; j++) a[j] = j < (int)kk ? *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo) : 0u;
+        // (a quad with no work still runs the rounds: its results are dropped like those
+        // of blocks past a chain's end)
+#pragma unroll
+        for (int j = 0; j < CH; j++) {
+            const uint32_t c = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+            iv = j < (int)kk ? c : iv;
+            a[j] = c;
+        }
+#pragma unroll
+        for (int j = 0; j < CH; j++)
+            if (j < (int)kk) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = a[j];
+        p += 16 * kk;
+        o += 16 * kk;
+        nfull -= kk;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (runtime -> template dispatch)
+
+// Variant selection.  Per-packet keys need ~100 VGPRs of round keys, so they always
+// use the 4-table layout (one workgroup per CU); uniform-key variants take the
+// layout the engine asks for.
+template <int NR, int NT, int CH>
+static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads,
+                       hipStream_t st) {
+#define FPNN_ENC(L, K, S, NTX) \
+    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
+    } else {
+        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true, 4); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false, 4);
+    }
+#undef FPNN_ENC
+}
+
+template <int NR>
+static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid, int threads,
+                   hipStream_t st) {
+    if (v.tables == 2) {
+        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, threads, st);
+    } else {
+        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, threads, st);
+        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, threads, st);
+        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, threads, st);
+    }
+}
+
+template <int NR>
+static void coop_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads, hipStream_t st) {
+#define FPNN_COOP(L, K, S) \
+    hipLaunchKernelGGL((k_cfb_encrypt_coop<NR, L, K, S, 4>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_UNIFORM, KEY_UNIFORM, false);
+    } else if (km == KEY_UNIFORM) {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_COOP(LAYOUT_GENERAL, KEY_LANE, false);
+    }
+#undef FPNN_COOP
+}
+
+template <int NR>
+static void queue_nr(const KBatch &b, KeyMode km, bool stream, int grid, int threads, uint32_t *next,
+                     hipStream_t st) {
+#define FPNN_QUEUE(K, STR) \
+    hipLaunchKernelGGL((k_cfb_encrypt_queue<NR, K, STR, 4>), dim3(grid), dim3(threads), 0, st, b, next)
+    if (km == KEY_UNIFORM) {
+        if (stream) FPNN_QUEUE(KEY_UNIFORM, true); else FPNN_QUEUE(KEY_UNIFORM, false);
+    } else {
+        if (stream) FPNN_QUEUE(KEY_LANE, true); else FPNN_QUEUE(KEY_LANE, false);
+    }
+#undef FPNN_QUEUE
+}
+
+hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool stream, int grid, int threads,
+                                uint32_t *next, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(next, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess) return err;
+    set_launched("cfb_encrypt_queue");
+    switch (nrounds) {
+        case 10: queue_nr<10>(b, km, stream, grid, threads, next, st); break;
+        case 12: queue_nr<12>(b, km, stream, grid, threads, next, st); break;
+        case 14: queue_nr<14>(b, km, stream, grid, threads, next, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                               int threads, hipStream_t st) {
+    set_launched("cfb_encrypt_coop");
+    switch (nrounds) {
+        case 10: coop_nr<10>(b, layout, km, stream, grid, threads, st); break;
+        case 12: coop_nr<12>(b, layout, km, stream, grid, threads, st); break;
+        case 14: coop_nr<14>(b, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+int blocks_per_cu(const Variant &v, KeyMode km) { return (km == KEY_UNIFORM && v.tables == 2) ? 2 : 1; }
+
+namespace {
+thread_local const char *g_launched = "";
+}
+const char *last_launched() { return g_launched; }
+void set_launched(const char *name) { g_launched = name; }
+
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
+                                 bool stream, int grid, int threads, hipStream_t st) {
+    set_launched("cfb_encrypt_chains");
+    switch (nrounds) {
+        case 10: enc_nr<10>(b, v, layout, km, stream, grid, threads, st); break;
+        case 12: enc_nr<12>(b, v, layout, km, stream, grid, threads, st); break;
+        case 14: enc_nr<14>(b, v, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace fpnn_aes
