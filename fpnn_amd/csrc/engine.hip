@@ -379,6 +379,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // chains every quad holds at most one and the grid stride is cheaper)
         const bool queue = b->len && (e->variant.queue == 2 || (e->variant.queue == 1 && lanes > full_chip));
         if (queue && (rc = grow(e->d_next, e->cap_next, 1))) return rc;
+        if (queue && e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
         if (queue)
             HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));

@@ -475,7 +475,19 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
         uint32_t a[S][CH];
 #pragma unroll
         for (int k = 0; k < S; k++) {
-            kk[k] = active[k] ? (nfull[k] < CH ? nfull[k] : CH) : 0u;
+            uint32_t lim = CH;
+            if (b.flags & F_ALIGN_CHUNKS) {
+                // line-aligned steps (as K2): a chain whose input and output sit at the
+                // same 16-B multiple inside a 128-B line takes a short first step to the
+                // line boundary, so every later step reads and writes whole lines back to
+                // back instead of leaving half of each line to the next step (C4: 64-B
+                // packet offsets; write bytes 1.17x -> 1.00x of algorithmic).  Aligning
+                // the output alone when the two differ (wire frames: 4-byte prefix)
+                // measured 2.4x slower, so those chains keep the unaligned steps.
+                const uint32_t xo = (uint32_t)(uintptr_t)o[k] & 127u, xi = (uint32_t)(uintptr_t)p[k] & 127u;
+                if (xo == xi && !(xo & 15u)) lim = CH - (xo >> 4);
+            }
+            kk[k] = active[k] ? (nfull[k] < lim ? nfull[k] : lim) : 0u;
 #pragma unroll
             for (int j = 0; j < CH; j++)
                 a[k][j] = j < (int)kk[k] ? *reinterpret_cast<const uint32_u *>(p[k] + 16 * j + wlo) : 0u;

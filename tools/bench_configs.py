@@ -402,7 +402,10 @@ def main():
         in_off = torch.arange(P, dtype=torch.int64, device="cuda") * L
         out_off = torch.arange(P, dtype=torch.int64, device="cuda") * (L + 4)
         lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
-        eng.package_encrypt(a, wire, P, ks, in_off=in_off, out_off=out_off, lens=lens, wire_prefix=True)
+        def wire_encrypt():  # the send side: bodies -> htole32(len) || ciphertext (K2q)
+            eng.package_encrypt(a, wire, P, ks, in_off=in_off, out_off=out_off, lens=lens, wire_prefix=True)
+
+        we, ke, _ = timed(eng, E, wire_encrypt, args.reps)
         conn_off = torch.arange(NC, dtype=torch.int64, device="cuda") * (F * (L + 4))
         conn_len = torch.full((NC,), F * (L + 4), dtype=torch.int32, device="cuda")
         plain = torch.empty_like(wire)
@@ -416,6 +419,7 @@ def main():
         body = plain.view(P, L + 4)[:, 4:]
         assert torch.equal(body.reshape(-1), a), "R1 receive-path plaintext differs"
         out["R1"] = {"frames": P, "body_bytes": P * L, "recv_wall_GiBs": gib(P * L, wr),
+                     "wire_encrypt_kernel_GiBs": gib(P * L, ke), "wire_encrypt_wall_GiBs": gib(P * L, we),
                      "decrypt_kernel_GiBs": gib(P * L, kr),
                      "note": "fpnn_aes_package_recv over 16384 connections x 64 wire frames (4-byte LE length + 1 KiB): "
                              "device frame scan + decrypt of the bodies at their frame offsets (wall includes the scan, "
