@@ -65,6 +65,10 @@ __device__ __forceinline__ void mac_s(uint64_t &lo, uint32_t &hi, uint32_t x, ui
 // t = L + H*(2^32 + 977) (mod p) folded twice and one conditional subtraction.  The host
 // passes R = 1 (r1 = r2 = 1) for this form, so the Montgomery-form conversions around the
 // ladder become identities and every field value is the same residue as micro-ecc's.
+// Field kinds: Montgomery form with the generic product (any curve), or normal form with
+// a special-prime reduction of the full 512-bit product (R = 1 on the host side).
+enum : int { FK_MONT = 0, FK_K1 = 1, FK_P256 = 2 };
+
 // t (512 bits) mod p: t = L + H*(2^32 + 977) folded twice, every column sum < 2^43,
 // then U + top*(2^32 + 977) < 2^256 + 2^67 < 2p and one conditional subtraction
 template <int NW>
@@ -92,37 +96,85 @@ __device__ __forceinline__ Fe<NW> k1_fold(const uint32_t (&t)[16], const EccCons
     return reduce_once<NW>(u, (uint32_t)x, c);
 }
 
+// secp256r1 (p = 2^256 - 2^224 + 2^192 + 2^96 - 1): the NIST word-sum reduction (FIPS
+// 186-4 D.2.3) t = s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9 as signed column sums,
+// the signed carry k (|k| <= 6) folded back as k * (2^224 - 2^192 - 2^96 + 1), and the
+// final carry c2 in {-1, 0, 1} settled by one add or subtract of p (all selects).
 template <int NW>
-__device__ __forceinline__ Fe<NW> fmul_k1(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
-    static_assert(NW == 8, "secp256k1 has 8 limbs");
-    uint32_t t[16];
+__device__ __forceinline__ Fe<NW> p256_fold(const uint32_t (&t)[16], const EccConst &c) {
+    const int64_t c0 = t[0], c1 = t[1], c2 = t[2], c3 = t[3], c4 = t[4], c5 = t[5], c6 = t[6], c7 = t[7];
+    const int64_t c8 = t[8], c9 = t[9], c10 = t[10], c11 = t[11], c12 = t[12], c13 = t[13], c14 = t[14],
+                  c15 = t[15];
+    int64_t a[8];
+    a[0] = c0 + c8 + c9 - c11 - c12 - c13 - c14;
+    a[1] = c1 + c9 + c10 - c12 - c13 - c14 - c15;
+    a[2] = c2 + c10 + c11 - c13 - c14 - c15;
+    a[3] = c3 + 2 * (c11 + c12) + c13 - c15 - c8 - c9;
+    a[4] = c4 + 2 * (c12 + c13) + c14 - c9 - c10;
+    a[5] = c5 + 2 * (c13 + c14) + c15 - c10 - c11;
+    a[6] = c6 + 3 * c14 + 2 * c15 + c13 - c8 - c9;
+    a[7] = c7 + 3 * c15 + c8 - c10 - c11 - c12 - c13;
+    uint32_t u[8];
+    int64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        acc += a[j];
+        u[j] = (uint32_t)acc;
+        acc >>= 32;  // arithmetic
+    }
+    const int64_t k = acc;
+    int64_t b[8] = {(int64_t)u[0] + k, u[1], u[2], (int64_t)u[3] - k, u[4], u[5], (int64_t)u[6] - k,
+                    (int64_t)u[7] + k};
+    acc = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        acc += b[j];
+        u[j] = (uint32_t)acc;
+        acc >>= 32;
+    }
+    const int32_t cr = (int32_t)acc;  // -1, 0 or 1: value = U + cr * 2^256
+    uint32_t d[8], e[8], borrow = 0, carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint64_t sd = (uint64_t)u[j] - c.p[j] - borrow;
+        d[j] = (uint32_t)sd;
+        borrow = (uint32_t)(sd >> 63);
+        const uint64_t se = (uint64_t)u[j] + c.p[j] + carry;
+        e[j] = (uint32_t)se;
+        carry = (uint32_t)(se >> 32);
+    }
+    const bool use_e = cr < 0, use_d = cr > 0 || (cr == 0 && borrow == 0);
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = use_e ? e[j] : (use_d ? d[j] : u[j]);
+    return r;
+}
+
+// 512-bit product of two 8-limb values, product scanning
+__device__ __forceinline__ void prod8(const uint32_t *a, const uint32_t *b, uint32_t (&t)[16]) {
     uint64_t lo = 0;
     uint32_t hi = 0;
 #pragma unroll
     for (int i = 0; i < 15; i++) {
 #pragma unroll
-        for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) mac(lo, hi, a.v[j], b.v[i - j]);
+        for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) mac(lo, hi, a[j], b[i - j]);
         t[i] = (uint32_t)lo;
         lo = (lo >> 32) | ((uint64_t)hi << 32);
         hi = 0;
     }
     t[15] = (uint32_t)lo;
-    return k1_fold<NW>(t, c);
 }
 
 // a^2: the 28 cross products once (product scanning), doubled by a one-bit shift of the
 // 512-bit sum, plus the 8 squares -- 36 partial products instead of 64
-template <int NW>
-__device__ __forceinline__ Fe<NW> fsqr_k1(const Fe<NW> &a, const EccConst &c) {
-    static_assert(NW == 8, "secp256k1 has 8 limbs");
-    uint32_t t[16];
+__device__ __forceinline__ void sqr8(const uint32_t *a, uint32_t (&t)[16]) {
     uint64_t lo = 0;
     uint32_t hi = 0;
     t[0] = 0;
 #pragma unroll
     for (int i = 1; i < 15; i++) {
 #pragma unroll
-        for (int j = (i > 7 ? i - 7 : 0); 2 * j < i; j++) mac(lo, hi, a.v[j], a.v[i - j]);
+        for (int j = (i > 7 ? i - 7 : 0); 2 * j < i; j++) mac(lo, hi, a[j], a[i - j]);
         t[i] = (uint32_t)lo;
         lo = (lo >> 32) | ((uint64_t)hi << 32);
         hi = 0;
@@ -136,18 +188,28 @@ __device__ __forceinline__ Fe<NW> fsqr_k1(const Fe<NW> &a, const EccConst &c) {
     for (int i = 0; i < 8; i++) {
         uint64_t w = (((uint64_t)t[2 * i + 1] << 32) | t[2 * i]) + cin;
         uint32_t h = w < cin;
-        mac(w, h, a.v[i], a.v[i]);
+        mac(w, h, a[i], a[i]);
         t[2 * i] = (uint32_t)w;
         t[2 * i + 1] = (uint32_t)(w >> 32);
         cin = h;
     }
-    return k1_fold<NW>(t, c);
 }
 
-template <int NW, bool K1 = false>
+template <int NW, int FK>
+__device__ __forceinline__ Fe<NW> fold_nf(const uint32_t (&t)[16], const EccConst &c) {
+    static_assert(NW == 8 && (FK == FK_K1 || FK == FK_P256), "normal form: the 256-bit special primes");
+    if constexpr (FK == FK_K1)
+        return k1_fold<NW>(t, c);
+    else
+        return p256_fold<NW>(t, c);
+}
+
+template <int NW, int FK = FK_MONT>
 __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
-    if constexpr (K1) {
-        return fmul_k1<NW>(a, b, c);
+    if constexpr (FK != FK_MONT) {
+        uint32_t t[16];
+        prod8(a.v, b.v, t);
+        return fold_nf<NW, FK>(t, c);
     } else {
         uint32_t m[NW], r[NW];
         uint64_t lo = 0;
@@ -180,12 +242,15 @@ __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const E
     }
 }
 
-template <int NW, bool K1 = false>
+template <int NW, int FK = FK_MONT>
 __device__ __forceinline__ Fe<NW> fsqr(const Fe<NW> &a, const EccConst &c) {
-    if constexpr (K1)
-        return fsqr_k1<NW>(a, c);
-    else
-        return fmul<NW, K1>(a, a, c);
+    if constexpr (FK != FK_MONT) {
+        uint32_t t[16];
+        sqr8(a.v, t);
+        return fold_nf<NW, FK>(t, c);
+    } else {
+        return fmul<NW, FK>(a, a, c);
+    }
 }
 
 template <int NW>
@@ -258,111 +323,111 @@ __device__ __forceinline__ Fe<NW> fconst(const uint32_t *k) {
 }
 
 // a^(p-2) = 1/a (0 -> 0, as uECC_vli_modInv); the exponent is public: uniform branches
-template <int NW, bool K1>
+template <int NW, int FK>
 __device__ Fe<NW> finv(const Fe<NW> &a, const EccConst &c) {
     Fe<NW> r = fconst<NW>(c.r1);
     for (int w = NW - 1; w >= 0; w--) {
         const uint32_t e = c.pm2[w];
         for (int b = 31; b >= 0; b--) {
-            r = fsqr<NW, K1>(r, c);
-            if ((e >> b) & 1u) r = fmul<NW, K1>(r, a, c);
+            r = fsqr<NW, FK>(r, c);
+            if ((e >> b) & 1u) r = fmul<NW, FK>(r, a, c);
         }
     }
     return r;
 }
 
 // double_jacobian (curve-specific.inc:50-95 a = -3; :1110-1141 secp256k1, a = 0), z != 0
-template <int NW, bool AM3, bool K1>
+template <int NW, bool AM3, int FK>
 __device__ __forceinline__ void dbl_jacobian(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &Z1, const EccConst &c) {
     if (AM3) {
-        Fe<NW> t4 = fsqr<NW, K1>(Y1, c);
-        Fe<NW> t5 = fmul<NW, K1>(X1, t4, c);
-        t4 = fsqr<NW, K1>(t4, c);
-        Y1 = fmul<NW, K1>(Y1, Z1, c);
-        Z1 = fsqr<NW, K1>(Z1, c);
+        Fe<NW> t4 = fsqr<NW, FK>(Y1, c);
+        Fe<NW> t5 = fmul<NW, FK>(X1, t4, c);
+        t4 = fsqr<NW, FK>(t4, c);
+        Y1 = fmul<NW, FK>(Y1, Z1, c);
+        Z1 = fsqr<NW, FK>(Z1, c);
         X1 = fadd<NW>(X1, Z1, c);
         Z1 = fadd<NW>(Z1, Z1, c);
         Z1 = fsub<NW>(X1, Z1, c);
-        X1 = fmul<NW, K1>(X1, Z1, c);
+        X1 = fmul<NW, FK>(X1, Z1, c);
         Z1 = fadd<NW>(X1, X1, c);
         X1 = fadd<NW>(X1, Z1, c);
         X1 = fhalf<NW>(X1, c);
-        Z1 = fsqr<NW, K1>(X1, c);
+        Z1 = fsqr<NW, FK>(X1, c);
         Z1 = fsub<NW>(Z1, t5, c);
         Z1 = fsub<NW>(Z1, t5, c);
         t5 = fsub<NW>(t5, Z1, c);
-        X1 = fmul<NW, K1>(X1, t5, c);
+        X1 = fmul<NW, FK>(X1, t5, c);
         t4 = fsub<NW>(X1, t4, c);
         X1 = Z1;
         Z1 = Y1;
         Y1 = t4;
     } else {
-        Fe<NW> t5 = fsqr<NW, K1>(Y1, c);
-        Fe<NW> t4 = fmul<NW, K1>(X1, t5, c);
-        X1 = fsqr<NW, K1>(X1, c);
-        t5 = fsqr<NW, K1>(t5, c);
-        Z1 = fmul<NW, K1>(Y1, Z1, c);
+        Fe<NW> t5 = fsqr<NW, FK>(Y1, c);
+        Fe<NW> t4 = fmul<NW, FK>(X1, t5, c);
+        X1 = fsqr<NW, FK>(X1, c);
+        t5 = fsqr<NW, FK>(t5, c);
+        Z1 = fmul<NW, FK>(Y1, Z1, c);
         Y1 = fadd<NW>(X1, X1, c);
         Y1 = fadd<NW>(Y1, X1, c);
         Y1 = fhalf<NW>(Y1, c);
-        X1 = fsqr<NW, K1>(Y1, c);
+        X1 = fsqr<NW, FK>(Y1, c);
         X1 = fsub<NW>(X1, t4, c);
         X1 = fsub<NW>(X1, t4, c);
         t4 = fsub<NW>(t4, X1, c);
-        Y1 = fmul<NW, K1>(Y1, t4, c);
+        Y1 = fmul<NW, FK>(Y1, t4, c);
         Y1 = fsub<NW>(Y1, t5, c);
     }
 }
 
 // (x, y) -> (x z^2, y z^3)  (uECC.c:748-758)
-template <int NW, bool K1>
+template <int NW, int FK>
 __device__ __forceinline__ void apply_z(Fe<NW> &X, Fe<NW> &Y, const Fe<NW> &Z, const EccConst &c) {
-    Fe<NW> t = fsqr<NW, K1>(Z, c);
-    X = fmul<NW, K1>(X, t, c);
-    t = fmul<NW, K1>(t, Z, c);
-    Y = fmul<NW, K1>(Y, t, c);
+    Fe<NW> t = fsqr<NW, FK>(Z, c);
+    X = fmul<NW, FK>(X, t, c);
+    t = fmul<NW, FK>(t, Z, c);
+    Y = fmul<NW, FK>(Y, t, c);
 }
 
 // XYcZ_add (uECC.c:788-813): (P, Q) co-Z -> P into P', Q into P + Q
-template <int NW, bool K1>
+template <int NW, int FK>
 __device__ __forceinline__ void xycz_add(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
     Fe<NW> t5 = fsub<NW>(X2, X1, c);
-    t5 = fsqr<NW, K1>(t5, c);
-    X1 = fmul<NW, K1>(X1, t5, c);
-    X2 = fmul<NW, K1>(X2, t5, c);
+    t5 = fsqr<NW, FK>(t5, c);
+    X1 = fmul<NW, FK>(X1, t5, c);
+    X2 = fmul<NW, FK>(X2, t5, c);
     Y2 = fsub<NW>(Y2, Y1, c);
-    t5 = fsqr<NW, K1>(Y2, c);
+    t5 = fsqr<NW, FK>(Y2, c);
     t5 = fsub<NW>(t5, X1, c);
     t5 = fsub<NW>(t5, X2, c);
     X2 = fsub<NW>(X2, X1, c);
-    Y1 = fmul<NW, K1>(Y1, X2, c);
+    Y1 = fmul<NW, FK>(Y1, X2, c);
     X2 = fsub<NW>(X1, t5, c);
-    Y2 = fmul<NW, K1>(Y2, X2, c);
+    Y2 = fmul<NW, FK>(Y2, X2, c);
     Y2 = fsub<NW>(Y2, Y1, c);
     X2 = t5;
 }
 
 // XYcZ_addC (uECC.c:819-854): (P, Q) co-Z -> P into P - Q, Q into P + Q
-template <int NW, bool K1>
+template <int NW, int FK>
 __device__ __forceinline__ void xycz_addc(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
     Fe<NW> t5 = fsub<NW>(X2, X1, c);
-    t5 = fsqr<NW, K1>(t5, c);
-    X1 = fmul<NW, K1>(X1, t5, c);
-    X2 = fmul<NW, K1>(X2, t5, c);
+    t5 = fsqr<NW, FK>(t5, c);
+    X1 = fmul<NW, FK>(X1, t5, c);
+    X2 = fmul<NW, FK>(X2, t5, c);
     t5 = fadd<NW>(Y2, Y1, c);
     Y2 = fsub<NW>(Y2, Y1, c);
     Fe<NW> t6 = fsub<NW>(X2, X1, c);
-    Y1 = fmul<NW, K1>(Y1, t6, c);
+    Y1 = fmul<NW, FK>(Y1, t6, c);
     t6 = fadd<NW>(X1, X2, c);
-    X2 = fsqr<NW, K1>(Y2, c);
+    X2 = fsqr<NW, FK>(Y2, c);
     X2 = fsub<NW>(X2, t6, c);
     Fe<NW> t7 = fsub<NW>(X1, X2, c);
-    Y2 = fmul<NW, K1>(Y2, t7, c);
+    Y2 = fmul<NW, FK>(Y2, t7, c);
     Y2 = fsub<NW>(Y2, Y1, c);
-    t7 = fsqr<NW, K1>(t5, c);
+    t7 = fsqr<NW, FK>(t5, c);
     t7 = fsub<NW>(t7, t6, c);
     t6 = fsub<NW>(t7, X1, c);
-    t6 = fmul<NW, K1>(t6, t5, c);
+    t6 = fmul<NW, FK>(t6, t5, c);
     Y1 = fsub<NW>(t6, Y1, c);
     X1 = t7;
 }
@@ -381,14 +446,14 @@ __device__ __forceinline__ void cswap(bool s, Fe<NW> &a, Fe<NW> &b) {
 // -> affine result (Montgomery form).  Registers (A, B) hold (R[bit], R[!bit]) of the
 // step; `sw` records whether they currently hold (R0, R1) so that swaps happen only
 // when consecutive bits differ.
-template <int NW, bool AM3, bool K1>
+template <int NW, bool AM3, int FK>
 __device__ void ladder(Fe<NW> &rx, Fe<NW> &ry, const Fe<NW> &xp, const Fe<NW> &yp, const uint32_t *s, int nbits,
                        const EccConst &c) {
     Fe<NW> ax = xp, ay = yp;  // R1
     Fe<NW> bx = xp, by = yp;  // R0
     Fe<NW> z = fconst<NW>(c.r1);
-    dbl_jacobian<NW, AM3, K1>(ax, ay, z, c);  // XYcZ_initial_double: R1 = 2P, R0 = P co-Z
-    apply_z<NW, K1>(bx, by, z, c);
+    dbl_jacobian<NW, AM3, FK>(ax, ay, z, c);  // XYcZ_initial_double: R1 = 2P, R0 = P co-Z
+    apply_z<NW, FK>(bx, by, z, c);
     bool sw = false;  // (A, B) == (R1, R0)
     uint32_t word = 0;
     for (int i = nbits - 2; i >= 0; --i) {
@@ -402,22 +467,22 @@ __device__ void ladder(Fe<NW> &rx, Fe<NW> &ry, const Fe<NW> &xp, const Fe<NW> &y
         cswap<NW>(want != sw, ax, bx);
         cswap<NW>(want != sw, ay, by);
         sw = want;
-        xycz_addc<NW, K1>(ax, ay, bx, by, c);  // R[bit] - R[!bit], R[bit] + R[!bit]
+        xycz_addc<NW, FK>(ax, ay, bx, by, c);  // R[bit] - R[!bit], R[bit] + R[!bit]
         if (i == 0) break;
-        xycz_add<NW, K1>(bx, by, ax, ay, c);
+        xycz_add<NW, FK>(bx, by, ax, ay, c);
     }
     // 1/Z = yP * Xb / (xP * Yb * (X1 - X0)), b = bit 0 (A holds R[b])
     const Fe<NW> x1 = fsel<NW>(sw, bx, ax), x0 = fsel<NW>(sw, ax, bx);
     Fe<NW> zi = fsub<NW>(x1, x0, c);
-    zi = fmul<NW, K1>(zi, ay, c);
-    zi = fmul<NW, K1>(zi, xp, c);
-    zi = finv<NW, K1>(zi, c);
-    zi = fmul<NW, K1>(zi, yp, c);
-    zi = fmul<NW, K1>(zi, ax, c);
-    xycz_add<NW, K1>(bx, by, ax, ay, c);
+    zi = fmul<NW, FK>(zi, ay, c);
+    zi = fmul<NW, FK>(zi, xp, c);
+    zi = finv<NW, FK>(zi, c);
+    zi = fmul<NW, FK>(zi, yp, c);
+    zi = fmul<NW, FK>(zi, ax, c);
+    xycz_add<NW, FK>(bx, by, ax, ay, c);
     rx = fsel<NW>(sw, ax, bx);  // R0
     ry = fsel<NW>(sw, ay, by);
-    apply_z<NW, K1>(rx, ry, zi, c);
+    apply_z<NW, FK>(rx, ry, zi, c);
 }
 
 // big-endian bytes (4-byte aligned, nbytes = 4*NW) -> limbs
@@ -544,7 +609,7 @@ __device__ void sha256_short(const uint32_t *mem, int nw32, uint32_t out[8]) {
     out[7] = h[7] + hh;  // big-endian words of the digest
 }
 
-template <int NW, bool AM3, bool K1>
+template <int NW, bool AM3, int FK>
 __global__ __launch_bounds__(256) void k_ecdh(EccConst c, EcdhJob j) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= j.count) return;  // lanes never exchange data: an early exit is safe
@@ -560,7 +625,7 @@ __global__ __launch_bounds__(256) void k_ecdh(EccConst c, EcdhJob j) {
     x = reduce_once<NW>(x.v, 0, c);
     y = reduce_once<NW>(y.v, 0, c);
     const Fe<NW> r2 = fconst<NW>(c.r2);
-    const Fe<NW> xp = fmul<NW, K1>(x, r2, c), yp = fmul<NW, K1>(y, r2, c);
+    const Fe<NW> xp = fmul<NW, FK>(x, r2, c), yp = fmul<NW, FK>(y, r2, c);
     // the scalar: regularize_k (uECC.c:902-913) -> k + n if that reaches 2^num_n_bits, else k + 2n
     uint32_t s[NW + 1];
     if (j.priv) {
@@ -588,12 +653,12 @@ __global__ __launch_bounds__(256) void k_ecdh(EccConst c, EcdhJob j) {
         for (int w = 0; w <= NW; w++) s[w] = c.k[w];
     }
     Fe<NW> rx, ry;
-    ladder<NW, AM3, K1>(rx, ry, xp, yp, s, c.num_n_bits + 1, c);
+    ladder<NW, AM3, FK>(rx, ry, xp, yp, s, c.num_n_bits + 1, c);
     Fe<NW> one;
 #pragma unroll
     for (int w = 0; w < NW; w++) one.v[w] = w == 0;
-    rx = fmul<NW, K1>(rx, one, c);  // out of Montgomery form
-    ry = fmul<NW, K1>(ry, one, c);
+    rx = fmul<NW, FK>(rx, one, c);  // out of Montgomery form
+    ry = fmul<NW, FK>(ry, one, c);
     uint32_t nz = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) nz |= rx.v[w] | ry.v[w];
@@ -685,19 +750,19 @@ void be_to_limbs(const uint8_t *be, int nbytes, uint32_t *out, int nlimbs) {
     for (int i = 0; i < nbytes; i++) out[i / 4] |= (uint32_t)be[nbytes - 1 - i] << (8 * (i % 4));
 }
 
-template <int NW, bool AM3, bool K1 = false>
+template <int NW, bool AM3, int FK = FK_MONT>
 void launch_nw(const EccConst &c, const EcdhJob &j, hipStream_t st) {
-    hipLaunchKernelGGL((k_ecdh<NW, AM3, K1>), dim3((j.count + 255) / 256), dim3(256), 0, st, c, j);
+    hipLaunchKernelGGL((k_ecdh<NW, AM3, FK>), dim3((j.count + 255) / 256), dim3(256), 0, st, c, j);
 }
 
-// secp256k1 in normal form with its special reduction (fmul_k1); FPNN_ECDH_K1_MONT=1
-// selects the generic Montgomery kernel instead (A/B)
-bool k1_special() {
-    static const bool on = [] {
-        const char *v = getenv("FPNN_ECDH_K1_MONT");
-        return !(v && atoi(v) != 0);
+// secp256k1 / secp256r1 in normal form with their special-prime reductions;
+// FPNN_ECDH_MONT=1 selects the generic Montgomery kernel for every curve (A/B)
+bool special_form(int curve) {
+    static const bool mont = [] {
+        const char *v = getenv("FPNN_ECDH_MONT");
+        return v && atoi(v) != 0;
     }();
-    return on;
+    return !mont && (curve == ECC_SECP256K1 || curve == ECC_SECP256R1);
 }
 
 }  // namespace
@@ -732,7 +797,7 @@ bool ecc_fill_const(int curve, EccConst &c) {
     memcpy(c.r1, r, sizeof r);
     for (int i = 0; i < 32 * nw; i++) dbl_mod(r, c.p, nw);  // R^2 mod p
     memcpy(c.r2, r, sizeof r);
-    if (curve == ECC_SECP256K1 && k1_special()) {  // normal form: R = 1
+    if (special_form(curve)) {  // normal form: R = 1
         memset(c.r1, 0, sizeof c.r1);
         memset(c.r2, 0, sizeof c.r2);
         c.r1[0] = c.r2[0] = 1;
@@ -768,12 +833,17 @@ hipError_t launch_ecdh(const EccConst &c, const EcdhJob &j, int curve, hipStream
     if (j.count == 0) return hipSuccess;
     switch (curve) {
         case ECC_SECP256K1:
-            if (k1_special())
-                launch_nw<8, false, true>(c, j, st);
+            if (special_form(curve))
+                launch_nw<8, false, FK_K1>(c, j, st);
             else
                 launch_nw<8, false>(c, j, st);
             break;
-        case ECC_SECP256R1: launch_nw<8, true>(c, j, st); break;
+        case ECC_SECP256R1:
+            if (special_form(curve))
+                launch_nw<8, true, FK_P256>(c, j, st);
+            else
+                launch_nw<8, true>(c, j, st);
+            break;
         case ECC_SECP224R1: launch_nw<7, true>(c, j, st); break;
         case ECC_SECP192R1: launch_nw<6, true>(c, j, st); break;
         default: return hipErrorInvalidValue;
