@@ -1158,3 +1158,52 @@ def test_host_frames_over_two_engines(engine, oracle):
         got = b"".join(dst[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes() for i in idx)
         assert got == exp, s
         assert (iv_state[16 * s:16 * s + 16].tobytes(), int(pos_state[s])) == (iv_end, pos_end), s
+
+
+@pytest.mark.parametrize("layout", ["same_offsets", "inplace", "shifted_out", "stream"])
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_queue_line_aligned_steps(queue_engine, oracle, layout, keylen):
+    """K2q's line-aligned steps (k_encrypt.hip): a chain whose input and output sit at the
+    same 16-B multiple inside a 128-B line takes a short first step to the line boundary.
+    Ragged batches with 16-B multiple offsets at every line position and lengths from one
+    block to many 8-block steps (some with a partial last block); 'shifted_out' (output
+    16 B off the input) keeps the unaligned steps; 'stream' starts at random CFB
+    positions, so the aligned step begins after the head bytes."""
+    engine = queue_engine
+    rng = np.random.default_rng(77 + 3 * keylen + ["same_offsets", "inplace", "shifted_out", "stream"].index(layout))
+    n = 1200
+    lens = (rng.integers(0, 200, n) * 16 + rng.choice([0, 0, 0, 5, 11], n)).astype(np.int64)
+    lens[:8] = (16, 32, 112, 128, 144, 1, 0, 4096)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + 16 + rng.integers(0, 8, n - 1) * 16)]).astype(np.int64)
+    offs = (offs + 15) // 16 * 16  # 16-B multiples (a partial last block shifts the next one)
+    total = int(offs[-1] + lens[-1] + 256)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    keys = rng.integers(0, 256, n * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    slots = rng.permutation(n).astype(np.int32)
+    ks = keyset(engine, keys, keylen, ivs)
+    out_offs = offs + 16 if layout == "shifted_out" else offs
+    exp = inp.copy()
+    if layout == "stream":
+        iv_h = rng.integers(0, 256, n * 16, dtype=np.uint8)
+        pos_h = rng.integers(0, 16, n).astype(np.uint32)
+        iv_d, pos_d = to_dev(iv_h), to_dev(pos_h.astype(np.int32))
+        oracle.stream_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                            lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys, keylen=keylen,
+                            iv_state=iv_h, pos_state=pos_h, threads=8)
+        src, dst = to_dev(inp), to_dev(inp)
+        engine.stream_encrypt(src, dst, n, ks, iv_d, pos_d, in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)),
+                              key_slot=to_dev(slots))
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(dst), exp)
+        assert np.array_equal(to_host(iv_d), iv_h) and np.array_equal(to_host(pos_d).astype(np.uint32), pos_h)
+        return
+    oracle.package_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), out_off=out_offs.astype(np.uint64),
+                         lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys, keylen=keylen,
+                         ivs=ivs, threads=8)
+    src = to_dev(inp)
+    dst = src if layout == "inplace" else to_dev(inp)
+    engine.package_encrypt(src, dst, n, ks, in_off=to_dev(offs), out_off=to_dev(out_offs),
+                           lens=to_dev(lens.astype(np.int32)), key_slot=to_dev(slots))
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(dst), exp)
