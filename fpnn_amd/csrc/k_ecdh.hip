@@ -67,7 +67,7 @@ __device__ __forceinline__ void mac_s(uint64_t &lo, uint32_t &hi, uint32_t x, ui
 // ladder become identities and every field value is the same residue as micro-ecc's.
 // Field kinds: Montgomery form with the generic product (any curve), or normal form with
 // a special-prime reduction of the full 512-bit product (R = 1 on the host side).
-enum : int { FK_MONT = 0, FK_K1 = 1, FK_P256 = 2 };
+enum : int { FK_MONT = 0, FK_K1 = 1, FK_P256 = 2, FK_P224 = 3, FK_P192 = 4 };
 
 // t (512 bits) mod p: t = L + H*(2^32 + 977) folded twice, every column sum < 2^43,
 // then U + top*(2^32 + 977) < 2^256 + 2^67 < 2p and one conditional subtraction
@@ -150,42 +150,44 @@ __device__ __forceinline__ Fe<NW> p256_fold(const uint32_t (&t)[16], const EccCo
     return r;
 }
 
-// 512-bit product of two 8-limb values, product scanning
-__device__ __forceinline__ void prod8(const uint32_t *a, const uint32_t *b, uint32_t (&t)[16]) {
+// 2*NW-limb product of two NW-limb values, product scanning
+template <int NW>
+__device__ __forceinline__ void prodN(const uint32_t *a, const uint32_t *b, uint32_t (&t)[2 * NW]) {
     uint64_t lo = 0;
     uint32_t hi = 0;
 #pragma unroll
-    for (int i = 0; i < 15; i++) {
+    for (int i = 0; i < 2 * NW - 1; i++) {
 #pragma unroll
-        for (int j = (i > 7 ? i - 7 : 0); j <= (i < 7 ? i : 7); j++) mac(lo, hi, a[j], b[i - j]);
+        for (int j = (i > NW - 1 ? i - (NW - 1) : 0); j <= (i < NW - 1 ? i : NW - 1); j++) mac(lo, hi, a[j], b[i - j]);
         t[i] = (uint32_t)lo;
         lo = (lo >> 32) | ((uint64_t)hi << 32);
         hi = 0;
     }
-    t[15] = (uint32_t)lo;
+    t[2 * NW - 1] = (uint32_t)lo;
 }
 
-// a^2: the 28 cross products once (product scanning), doubled by a one-bit shift of the
-// 512-bit sum, plus the 8 squares -- 36 partial products instead of 64
-__device__ __forceinline__ void sqr8(const uint32_t *a, uint32_t (&t)[16]) {
+// a^2: the NW(NW-1)/2 cross products once (product scanning), doubled by a one-bit shift
+// of the 2*NW-limb sum, plus the NW squares (36 partial products instead of 64 at NW = 8)
+template <int NW>
+__device__ __forceinline__ void sqrN(const uint32_t *a, uint32_t (&t)[2 * NW]) {
     uint64_t lo = 0;
     uint32_t hi = 0;
     t[0] = 0;
 #pragma unroll
-    for (int i = 1; i < 15; i++) {
+    for (int i = 1; i < 2 * NW - 1; i++) {
 #pragma unroll
-        for (int j = (i > 7 ? i - 7 : 0); 2 * j < i; j++) mac(lo, hi, a[j], a[i - j]);
+        for (int j = (i > NW - 1 ? i - (NW - 1) : 0); 2 * j < i; j++) mac(lo, hi, a[j], a[i - j]);
         t[i] = (uint32_t)lo;
         lo = (lo >> 32) | ((uint64_t)hi << 32);
         hi = 0;
     }
-    t[15] = (uint32_t)lo;
+    t[2 * NW - 1] = (uint32_t)lo;
 #pragma unroll
-    for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+    for (int i = 2 * NW - 1; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
     t[0] = 0;  // (the cross sum has no limb-0 term)
     uint32_t cin = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < NW; i++) {
         uint64_t w = (((uint64_t)t[2 * i + 1] << 32) | t[2 * i]) + cin;
         uint32_t h = w < cin;
         mac(w, h, a[i], a[i]);
@@ -195,20 +197,99 @@ __device__ __forceinline__ void sqr8(const uint32_t *a, uint32_t (&t)[16]) {
     }
 }
 
+// secp192r1 (p = 2^192 - 2^64 - 1): t = L + H*(2^64 + 1), all terms positive; the top
+// (< 2^66, weight 2^192) folds once more the same way; the result is < 2^192 + 2^131 < 2p
+template <int NW>
+__device__ __forceinline__ Fe<NW> p192_fold(const uint32_t (&t)[12], const EccConst &c) {
+    uint32_t u[6];
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        acc += (uint64_t)t[j] + t[6 + j] + (j >= 2 ? t[4 + j] : 0u);
+        u[j] = (uint32_t)acc;
+        acc >>= 32;
+    }
+    const uint64_t top = acc + t[10] + ((uint64_t)t[11] << 32);  // < 2^66
+    const uint64_t tl[2] = {(uint32_t)top, top >> 32};
+    acc = 0;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        acc += (uint64_t)u[j] + (j < 2 ? tl[j] : 0u) + (j >= 2 && j < 4 ? tl[j - 2] : 0u);
+        u[j] = (uint32_t)acc;
+        acc >>= 32;
+    }
+    return reduce_once<NW>(u, (uint32_t)acc, c);
+}
+
+// secp224r1 (p = 2^224 - 2^96 + 1): t = L + H*(2^96 - 1) as signed column sums, the
+// signed top (weight 2^224, < 2^97) folded once more, the last carry (-1, 0 or 1)
+// settled by one add or subtract of p (selects)
+template <int NW>
+__device__ __forceinline__ Fe<NW> p224_fold(const uint32_t (&t)[14], const EccConst &c) {
+    uint32_t u[7];
+    int64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        acc += (int64_t)t[j] - (int64_t)t[7 + j] + (j >= 3 ? (int64_t)t[4 + j] : 0);
+        u[j] = (uint32_t)acc;
+        acc >>= 32;  // arithmetic
+    }
+    int64_t tl[4];  // the top in limbs: tl[0..2] unsigned 32-bit, tl[3] the signed rest
+    acc += t[11];
+    tl[0] = (uint32_t)acc;
+    acc = (acc >> 32) + t[12];
+    tl[1] = (uint32_t)acc;
+    acc = (acc >> 32) + t[13];
+    tl[2] = (uint32_t)acc;
+    tl[3] = acc >> 32;
+    acc = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        acc += (int64_t)u[j] - (j < 4 ? tl[j] : 0) + (j >= 3 ? tl[j - 3] : 0);
+        u[j] = (uint32_t)acc;
+        acc >>= 32;
+    }
+    const int32_t cr = (int32_t)acc;
+    uint32_t d[7], e[7], borrow = 0, carry = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const uint64_t sd = (uint64_t)u[j] - c.p[j] - borrow;
+        d[j] = (uint32_t)sd;
+        borrow = (uint32_t)(sd >> 63);
+        const uint64_t se = (uint64_t)u[j] + c.p[j] + carry;
+        e[j] = (uint32_t)se;
+        carry = (uint32_t)(se >> 32);
+    }
+    const bool use_e = cr < 0, use_d = cr > 0 || (cr == 0 && borrow == 0);
+    Fe<NW> r;
+#pragma unroll
+    for (int j = 0; j < 7; j++) r.v[j] = use_e ? e[j] : (use_d ? d[j] : u[j]);
+    return r;
+}
+
 template <int NW, int FK>
-__device__ __forceinline__ Fe<NW> fold_nf(const uint32_t (&t)[16], const EccConst &c) {
-    static_assert(NW == 8 && (FK == FK_K1 || FK == FK_P256), "normal form: the 256-bit special primes");
-    if constexpr (FK == FK_K1)
+__device__ __forceinline__ Fe<NW> fold_nf(const uint32_t (&t)[2 * NW], const EccConst &c) {
+    static_assert(FK != FK_MONT, "normal form only");
+    if constexpr (FK == FK_K1) {
+        static_assert(NW == 8, "secp256k1 has 8 limbs");
         return k1_fold<NW>(t, c);
-    else
+    } else if constexpr (FK == FK_P256) {
+        static_assert(NW == 8, "secp256r1 has 8 limbs");
         return p256_fold<NW>(t, c);
+    } else if constexpr (FK == FK_P224) {
+        static_assert(NW == 7, "secp224r1 has 7 limbs");
+        return p224_fold<NW>(t, c);
+    } else {
+        static_assert(NW == 6 && FK == FK_P192, "secp192r1 has 6 limbs");
+        return p192_fold<NW>(t, c);
+    }
 }
 
 template <int NW, int FK = FK_MONT>
 __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
     if constexpr (FK != FK_MONT) {
-        uint32_t t[16];
-        prod8(a.v, b.v, t);
+        uint32_t t[2 * NW];
+        prodN<NW>(a.v, b.v, t);
         return fold_nf<NW, FK>(t, c);
     } else {
         uint32_t m[NW], r[NW];
@@ -245,8 +326,8 @@ __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const E
 template <int NW, int FK = FK_MONT>
 __device__ __forceinline__ Fe<NW> fsqr(const Fe<NW> &a, const EccConst &c) {
     if constexpr (FK != FK_MONT) {
-        uint32_t t[16];
-        sqr8(a.v, t);
+        uint32_t t[2 * NW];
+        sqrN<NW>(a.v, t);
         return fold_nf<NW, FK>(t, c);
     } else {
         return fmul<NW, FK>(a, a, c);
@@ -331,9 +412,9 @@ __device__ __forceinline__ Fe<NW> fsqr_n(Fe<NW> x, int n, const EccConst &c) {
 }
 
 // a^(p-2) = 1/a (0 -> 0, as uECC_vli_modInv); the exponent is public: uniform branches.
-// secp256k1 / secp256r1: addition chains for p - 2 (blocks of ones x_k = a^(2^k - 1)) --
-// the same power with far fewer products, so the same result (chains checked in Python
-// against pow(a, p - 2, p)).  secp256k1: 255 squarings and 15 products instead of ~248.
+// Special forms: addition chains for p - 2 (blocks of ones x_k = a^(2^k - 1)) -- the same
+// power with far fewer products, so the same result (chains checked in Python against
+// pow(a, p - 2, p)).  secp256k1: 255 squarings and 15 products instead of ~248.
 template <int NW, int FK>
 __device__ Fe<NW> finv(const Fe<NW> &a, const EccConst &c) {
     if constexpr (FK == FK_K1) {
@@ -367,6 +448,25 @@ __device__ Fe<NW> finv(const Fe<NW> &a, const EccConst &c) {
         t = fmul<NW, FK>(fsqr_n<NW, FK>(t, 32, c), x32, c);
         t = fmul<NW, FK>(fsqr_n<NW, FK>(t, 30, c), x30, c);
         return fmul<NW, FK>(fsqr_n<NW, FK>(t, 2, c), a, c);
+    } else if constexpr (FK == FK_P224 || FK == FK_P192) {
+        // common head: x127 (126 squarings, 10 products)
+        const Fe<NW> x2 = fmul<NW, FK>(fsqr<NW, FK>(a, c), a, c);
+        const Fe<NW> x3 = fmul<NW, FK>(fsqr<NW, FK>(x2, c), a, c);
+        const Fe<NW> x6 = fmul<NW, FK>(fsqr_n<NW, FK>(x3, 3, c), x3, c);
+        const Fe<NW> x12 = fmul<NW, FK>(fsqr_n<NW, FK>(x6, 6, c), x6, c);
+        const Fe<NW> x24 = fmul<NW, FK>(fsqr_n<NW, FK>(x12, 12, c), x12, c);
+        const Fe<NW> x48 = fmul<NW, FK>(fsqr_n<NW, FK>(x24, 24, c), x24, c);
+        const Fe<NW> x96 = fmul<NW, FK>(fsqr_n<NW, FK>(x48, 48, c), x48, c);
+        const Fe<NW> x120 = fmul<NW, FK>(fsqr_n<NW, FK>(x96, 24, c), x24, c);
+        const Fe<NW> x126 = fmul<NW, FK>(fsqr_n<NW, FK>(x120, 6, c), x6, c);
+        const Fe<NW> x127 = fmul<NW, FK>(fsqr<NW, FK>(x126, c), a, c);
+        if constexpr (FK == FK_P224) {  // p - 2 = 1^127 0 1^96: 223 squarings, 11 products
+            return fmul<NW, FK>(fsqr_n<NW, FK>(x127, 97, c), x96, c);
+        } else {  // p - 2 = 1^127 0 1^62 0 1: 205 squarings, 14 products (Fermat ~189)
+            const Fe<NW> x62 = fmul<NW, FK>(fsqr_n<NW, FK>(fmul<NW, FK>(fsqr_n<NW, FK>(x48, 12, c), x12, c), 2, c), x2, c);
+            const Fe<NW> t = fmul<NW, FK>(fsqr_n<NW, FK>(x127, 63, c), x62, c);
+            return fmul<NW, FK>(fsqr_n<NW, FK>(t, 2, c), a, c);
+        }
     }
     Fe<NW> r = fconst<NW>(c.r1);
     for (int w = NW - 1; w >= 0; w--) {
@@ -798,14 +898,14 @@ void launch_nw(const EccConst &c, const EcdhJob &j, hipStream_t st) {
     hipLaunchKernelGGL((k_ecdh<NW, AM3, FK>), dim3((j.count + 255) / 256), dim3(256), 0, st, c, j);
 }
 
-// secp256k1 / secp256r1 in normal form with their special-prime reductions;
-// FPNN_ECDH_MONT=1 selects the generic Montgomery kernel for every curve (A/B)
+// Every curve in normal form with its special-prime reduction (secp256k1, secp256r1,
+// secp224r1, secp192r1); FPNN_ECDH_MONT=1 selects the generic Montgomery kernels (A/B)
 bool special_form(int curve) {
     static const bool mont = [] {
         const char *v = getenv("FPNN_ECDH_MONT");
         return v && atoi(v) != 0;
     }();
-    return !mont && (curve == ECC_SECP256K1 || curve == ECC_SECP256R1);
+    return !mont;  // every supported curve has a special-form kernel
 }
 
 }  // namespace
@@ -887,8 +987,18 @@ hipError_t launch_ecdh(const EccConst &c, const EcdhJob &j, int curve, hipStream
             else
                 launch_nw<8, true>(c, j, st);
             break;
-        case ECC_SECP224R1: launch_nw<7, true>(c, j, st); break;
-        case ECC_SECP192R1: launch_nw<6, true>(c, j, st); break;
+        case ECC_SECP224R1:
+            if (special_form(curve))
+                launch_nw<7, true, FK_P224>(c, j, st);
+            else
+                launch_nw<7, true>(c, j, st);
+            break;
+        case ECC_SECP192R1:
+            if (special_form(curve))
+                launch_nw<6, true, FK_P192>(c, j, st);
+            else
+                launch_nw<6, true>(c, j, st);
+            break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

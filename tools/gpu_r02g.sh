@@ -8,7 +8,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/g_tests.log
 for v in 1 0 1 0; do
   echo "== FPNN_ECDH_MONT=$v"
-  FPNN_ECDH_MONT=$v timeout -k 10 120 python tools/bench_ecdh.py --curves secp256k1,secp256r1 --no-cpu --reps 5 \
+  FPNN_ECDH_MONT=$v timeout -k 10 120 python tools/bench_ecdh.py --curves secp256k1,secp256r1,secp224r1,secp192r1 --no-cpu --reps 5 \
     > gpurun_out/g_ecdh_$v.log 2>&1 || { tail -5 gpurun_out/g_ecdh_$v.log; exit 1; }
   grep -E '^\{' gpurun_out/g_ecdh_$v.log | tail -1 | cut -c1-600
 done
