@@ -1,0 +1,211 @@
+"""The special-prime reductions and inversion chains of k_ecdh.hip (field kinds FK_K1,
+FK_P256, FK_P224, FK_P192), restated limb for limb in Python and checked against plain
+modular arithmetic -- including the carry-range assumptions the device code relies on
+(column sums < 2^64, final carries in {-1, 0, 1} or {0, 1}, values < 2p before the last
+conditional subtraction).  The GPU tests check the kernels themselves against the
+reference's fixtures and the oracle (tests/test_gpu_ecdh.py); this pins the arithmetic
+design on CPU."""
+import random
+
+import pytest
+
+M = 1 << 32
+P = {
+    "secp256k1": (1 << 256) - (1 << 32) - 977,
+    "secp256r1": (1 << 256) - (1 << 224) + (1 << 192) + (1 << 96) - 1,
+    "secp224r1": (1 << 224) - (1 << 96) + 1,
+    "secp192r1": (1 << 192) - (1 << 64) - 1,
+}
+NW = {"secp256k1": 8, "secp256r1": 8, "secp224r1": 7, "secp192r1": 6}
+
+
+def limbs(x, n):
+    return [(x >> (32 * i)) & (M - 1) for i in range(n)]
+
+
+def value(u):
+    return sum(w << (32 * i) for i, w in enumerate(u))
+
+
+def settle(u, cr, p, nw):
+    """value = U + cr * 2^(32 nw), cr in {-1, 0, 1} -> [0, p) (p256_fold / p224_fold tail)."""
+    assert cr in (-1, 0, 1)
+    U, top = value(u), 1 << (32 * nw)
+    if cr < 0:
+        return (U + p) % top
+    if cr > 0 or U >= p:
+        return (U - p) % top
+    return U
+
+
+def k1_fold(t):  # k_ecdh.hip k1_fold
+    p = P["secp256k1"]
+    u, acc = [0] * 8, 0
+    for i in range(8):
+        acc = t[8 + i] * 977 + acc + t[i] + (t[7 + i] if i else 0)
+        assert acc < 1 << 64
+        u[i], acc = acc & (M - 1), acc >> 32
+    top = acc + t[15]
+    assert top < 1 << 34
+    x = u[0] + top * 977
+    u[0], x = x & (M - 1), (x >> 32) + u[1] + top
+    u[1], x = x & (M - 1), x >> 32
+    for i in range(2, 8):
+        x += u[i]
+        u[i], x = x & (M - 1), x >> 32
+    v = value(u) + (x << 256)
+    assert v < 2 * p
+    return v - p if v >= p else v
+
+
+def p256_fold(t):  # k_ecdh.hip p256_fold
+    c = t
+    a = [c[0] + c[8] + c[9] - c[11] - c[12] - c[13] - c[14],
+         c[1] + c[9] + c[10] - c[12] - c[13] - c[14] - c[15],
+         c[2] + c[10] + c[11] - c[13] - c[14] - c[15],
+         c[3] + 2 * (c[11] + c[12]) + c[13] - c[15] - c[8] - c[9],
+         c[4] + 2 * (c[12] + c[13]) + c[14] - c[9] - c[10],
+         c[5] + 2 * (c[13] + c[14]) + c[15] - c[10] - c[11],
+         c[6] + 3 * c[14] + 2 * c[15] + c[13] - c[8] - c[9],
+         c[7] + 3 * c[15] + c[8] - c[10] - c[11] - c[12] - c[13]]
+    u, acc = [0] * 8, 0
+    for j in range(8):
+        acc += a[j]
+        u[j], acc = acc & (M - 1), acc >> 32
+    k = acc
+    assert -6 <= k <= 6
+    b = [u[0] + k, u[1], u[2], u[3] - k, u[4], u[5], u[6] - k, u[7] + k]
+    acc = 0
+    for j in range(8):
+        acc += b[j]
+        u[j], acc = acc & (M - 1), acc >> 32
+    return settle(u, acc, P["secp256r1"], 8)
+
+
+def p224_fold(t):  # k_ecdh.hip p224_fold
+    u, acc = [0] * 7, 0
+    for j in range(7):
+        acc += t[j] - t[7 + j] + (t[4 + j] if j >= 3 else 0)
+        u[j], acc = acc & (M - 1), acc >> 32
+    acc += t[11]
+    tl = [acc & (M - 1)]
+    acc = (acc >> 32) + t[12]
+    tl.append(acc & (M - 1))
+    acc = (acc >> 32) + t[13]
+    tl += [acc & (M - 1), acc >> 32]
+    assert -2 <= tl[3] <= 1
+    acc = 0
+    for j in range(7):
+        acc += u[j] - (tl[j] if j < 4 else 0) + (tl[j - 3] if j >= 3 else 0)
+        u[j], acc = acc & (M - 1), acc >> 32
+    return settle(u, acc, P["secp224r1"], 7)
+
+
+def p192_fold(t):  # k_ecdh.hip p192_fold
+    p = P["secp192r1"]
+    u, acc = [0] * 6, 0
+    for j in range(6):
+        acc += t[j] + t[6 + j] + (t[4 + j] if j >= 2 else 0)
+        u[j], acc = acc & (M - 1), acc >> 32
+    top = acc + t[10] + (t[11] << 32)
+    assert top < 1 << 66
+    tl = [top & (M - 1), top >> 32]
+    acc = 0
+    for j in range(6):
+        acc += u[j] + (tl[j] if j < 2 else 0) + (tl[j - 2] if 2 <= j < 4 else 0)
+        u[j], acc = acc & (M - 1), acc >> 32
+    assert acc in (0, 1)
+    v = value(u) + (acc << 192)
+    assert v < 2 * p
+    return v - p if v >= p else v
+
+
+FOLD = {"secp256k1": k1_fold, "secp256r1": p256_fold, "secp224r1": p224_fold, "secp192r1": p192_fold}
+
+
+def sqr_limbs(a, nw):
+    """sqrN: cross products once, doubled by a one-bit shift, plus the squares."""
+    A, t, acc = limbs(a, nw), [0] * (2 * nw), 0
+    for i in range(1, 2 * nw - 1):
+        j = max(0, i - (nw - 1))
+        while 2 * j < i:
+            acc += A[j] * A[i - j]
+            j += 1
+        t[i], acc = acc & (M - 1), acc >> 32
+    t[2 * nw - 1] = acc
+    assert acc < M
+    for i in range(2 * nw - 1, 0, -1):
+        t[i] = ((t[i] << 1) | (t[i - 1] >> 31)) & (M - 1)
+    t[0], cin = 0, 0
+    for i in range(nw):
+        w = ((t[2 * i + 1] << 32) | t[2 * i]) + cin + A[i] * A[i]
+        t[2 * i], t[2 * i + 1], cin = w & (M - 1), (w >> 32) & (M - 1), w >> 64
+    assert cin == 0
+    return t
+
+
+@pytest.mark.parametrize("curve", sorted(P))
+def test_fold_matches_mod(curve):
+    p, nw, fold = P[curve], NW[curve], FOLD[curve]
+    rng = random.Random(len(curve))
+    edge = [0, 1, 2, p - 1, p - 2, 1 << (32 * nw - 1), (1 << 96) - 1, 1 << 64]
+    vals = edge + [rng.randrange(p) for _ in range(600)]
+    for _ in range(3000):
+        x, y = rng.choice(vals), rng.choice(vals)
+        assert fold(limbs(x * y, 2 * nw)) == x * y % p
+        assert fold(sqr_limbs(x, nw)) == x * x % p
+    for _ in range(1500):  # arbitrary words below p^2, extreme limbs included
+        ws = [rng.choice([0, M - 1, rng.randrange(M)]) for _ in range(2 * nw)]
+        if value(ws) < p * p:
+            assert fold(ws) == value(ws) % p
+
+
+def _sq(x, n, p):
+    for _ in range(n):
+        x = x * x % p
+    return x
+
+
+def inv_chain(curve, a):  # k_ecdh.hip finv, special forms
+    p = P[curve]
+
+    def blk(x, n, y):
+        return _sq(x, n, p) * y % p
+    x2 = blk(a, 1, a)
+    x3 = blk(x2, 1, a)
+    x6 = blk(x3, 3, x3)
+    if curve == "secp256k1":
+        x9 = blk(x6, 3, x3)
+        x11 = blk(x9, 2, x2)
+        x22 = blk(x11, 11, x11)
+        x44 = blk(x22, 22, x22)
+        x88 = blk(x44, 44, x44)
+        x176 = blk(x88, 88, x88)
+        x220 = blk(x176, 44, x44)
+        x223 = blk(x220, 3, x3)
+        t = blk(blk(blk(x223, 23, x22), 5, a), 3, x2)
+        return blk(t, 2, a)
+    x12 = blk(x6, 6, x6)
+    x15 = blk(x12, 3, x3)
+    if curve == "secp256r1":
+        x30 = blk(x15, 15, x15)
+        x32 = blk(x30, 2, x2)
+        t = _sq(blk(x32, 32, a), 96, p)
+        t = blk(blk(blk(t, 32, x32), 32, x32), 30, x30)
+        return blk(t, 2, a)
+    x24 = blk(x12, 12, x12)
+    x48 = blk(x24, 24, x24)
+    x96 = blk(x48, 48, x48)
+    x127 = blk(blk(blk(x96, 24, x24), 6, x6), 1, a)
+    if curve == "secp224r1":
+        return blk(x127, 97, x96)
+    x62 = blk(blk(x48, 12, x12), 2, x2)
+    return blk(blk(x127, 63, x62), 2, a)
+
+
+@pytest.mark.parametrize("curve", sorted(P))
+def test_inversion_chain_is_fermat(curve):
+    p = P[curve]
+    rng = random.Random(7 * len(curve))
+    for a in [0, 1, 2, p - 1] + [rng.randrange(p) for _ in range(20)]:
+        assert inv_chain(curve, a) == pow(a, p - 2, p)
