@@ -153,12 +153,44 @@ __device__ __forceinline__ uint4 aes_encrypt_block(uint4 in, const RoundKeys<NR>
     return o;
 }
 
+// aes_encrypt_block with each round's 16 lookups issued before any of them is folded
+// (a scheduling fence after the loads): where the surrounding kernel holds many live
+// registers the compiler otherwise interleaves loads and XORs two or three at a time,
+// leaving the LDS pipe nearly empty per wave.
+template <int NR, int NT>
+__device__ __forceinline__ uint4 aes_encrypt_block_fenced(uint4 in, const RoundKeys<NR> &rk, const Tables4<NT> &T) {
+    uint32_t s0 = in.x ^ rk.k[0], s1 = in.y ^ rk.k[1], s2 = in.z ^ rk.k[2], s3 = in.w ^ rk.k[3];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t a0 = T.template t<0>(s0), a1 = T.template t<1>(s1), a2 = T.template t<2>(s2), a3 = T.template t<3>(s3);
+        const uint32_t b0 = T.template t<0>(s1), b1 = T.template t<1>(s2), b2 = T.template t<2>(s3), b3 = T.template t<3>(s0);
+        const uint32_t c0 = T.template t<0>(s2), c1 = T.template t<1>(s3), c2 = T.template t<2>(s0), c3 = T.template t<3>(s1);
+        const uint32_t d0 = T.template t<0>(s3), d1 = T.template t<1>(s0), d2 = T.template t<2>(s1), d3 = T.template t<3>(s2);
+        __builtin_amdgcn_sched_barrier(0);
+        s0 = xor3(xor3(a0, a1, a2), a3, rk.k[4 * r + 0]);
+        s1 = xor3(xor3(b0, b1, b2), b3, rk.k[4 * r + 1]);
+        s2 = xor3(xor3(c0, c1, c2), c3, rk.k[4 * r + 2]);
+        s3 = xor3(xor3(d0, d1, d2), d3, rk.k[4 * r + 3]);
+    }
+    uint4 o;
+    o.x = T.last(s0, s1, s2, s3, rk.k[4 * NR + 0]);
+    o.y = T.last(s1, s2, s3, s0, rk.k[4 * NR + 1]);
+    o.z = T.last(s2, s3, s0, s1, rk.k[4 * NR + 2]);
+    o.w = T.last(s3, s0, s1, s2, rk.k[4 * NR + 3]);
+    return o;
+}
+
+template <bool FENCE, int NR, int NT>
+__device__ __forceinline__ uint4 aes_encrypt_block_sel(uint4 in, const RoundKeys<NR> &rk, const Tables4<NT> &T) {
+    return FENCE ? aes_encrypt_block_fenced<NR, NT>(in, rk, T) : aes_encrypt_block<NR, NT>(in, rk, T);
+}
+
 // M independent blocks under one key, round-interleaved: round r of every block is
 // issued before round r+1 of any, in ONE basic block, so a wave has 16*M LDS lookups
 // in flight per round instead of 16 and the LDS pipe is fed while the VALU folds the
 // previous block's lookups.  (Separate aes_encrypt_block calls end up serialized by
 // the compiler when control flow sits between them.)
-template <int NR, int NT, int M>
+template <int NR, int NT, int M, bool FENCE = false>
 __device__ __forceinline__ void aes_encrypt_blocks(uint4 (&st)[M], const RoundKeys<NR> &rk, const Tables4<NT> &T) {
     uint32_t s[M][4];
 #pragma unroll
@@ -171,13 +203,32 @@ __device__ __forceinline__ void aes_encrypt_blocks(uint4 (&st)[M], const RoundKe
 #pragma unroll
     for (int r = 1; r < NR; r++) {
         uint32_t t[M][4];
+        if (FENCE) {  // every lookup of the round issued before any fold (see aes_encrypt_block_fenced)
+            uint32_t l[M][4][4];
 #pragma unroll
-        for (int m = 0; m < M; m++) {
+            for (int m = 0; m < M; m++)
 #pragma unroll
-            for (int c = 0; c < 4; c++)
-                t[m][c] = xor3(xor3(T.template t<0>(s[m][c]), T.template t<1>(s[m][(c + 1) & 3]),
-                                    T.template t<2>(s[m][(c + 2) & 3])),
-                               T.template t<3>(s[m][(c + 3) & 3]), rk.k[4 * r + c]);
+                for (int c = 0; c < 4; c++) {
+                    l[m][c][0] = T.template t<0>(s[m][c]);
+                    l[m][c][1] = T.template t<1>(s[m][(c + 1) & 3]);
+                    l[m][c][2] = T.template t<2>(s[m][(c + 2) & 3]);
+                    l[m][c][3] = T.template t<3>(s[m][(c + 3) & 3]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < M; m++)
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    t[m][c] = xor3(xor3(l[m][c][0], l[m][c][1], l[m][c][2]), l[m][c][3], rk.k[4 * r + c]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                    t[m][c] = xor3(xor3(T.template t<0>(s[m][c]), T.template t<1>(s[m][(c + 1) & 3]),
+                                        T.template t<2>(s[m][(c + 2) & 3])),
+                                   T.template t<3>(s[m][(c + 3) & 3]), rk.k[4 * r + c]);
+            }
         }
 #pragma unroll
         for (int m = 0; m < M; m++)

@@ -5,8 +5,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -188,21 +190,82 @@ void EncryptorBatch::decrypt(Encryptor *enc, uint8_t *dest, uint8_t *src, int le
 // Persistent per-key-length table: slot per Encryptor serial, uploaded once
 // (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
 // like the table, so a flush never touches more than its own connections.
+namespace {
+
+// Serials retired by ~Encryptor / Encryptor::operator=, delivered to every live key
+// table (each drops them from its slot map at its next flush).
+struct RetireInbox {
+    std::vector<uint64_t> serials;
+};
+struct RetireRegistry {
+    std::mutex mu;
+    std::vector<RetireInbox *> inboxes;
+    std::atomic<size_t> n{0};
+};
+RetireRegistry &registry() {
+    static RetireRegistry *r = new RetireRegistry();  // never destroyed: Encryptors may die at exit
+    return *r;
+}
+
+}  // namespace
+
+uint64_t encryptor_serial() {
+    static std::atomic<uint64_t> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
+
+void encryptor_retire(uint64_t serial) {
+    RetireRegistry &r = registry();
+    if (r.n.load(std::memory_order_acquire) == 0) return;  // no EncryptorBatch key table exists
+    std::lock_guard<std::mutex> lk(r.mu);
+    for (RetireInbox *b : r.inboxes) b->serials.push_back(serial);
+}
+
+// Persistent per-key-length table: slot per Encryptor serial, uploaded once
+// (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
+// like the table, so a flush never touches more than its own connections.  The table
+// belongs to one engine, identified by its id (not its address, which a later thread's
+// engine may reuse).
 struct EncryptorBatch::KeyTable {
-    fpnn_aes_engine *e = nullptr;
+    uint64_t engine_id = 0;
     fpnn_aes_keyset *ks = nullptr;
     std::unordered_map<uint64_t, uint32_t> slot;
     uint32_t next = 0;
     std::vector<uint8_t> iv;
     std::vector<uint32_t> pos;
+    RetireInbox inbox;
+    KeyTable() {
+        RetireRegistry &r = registry();
+        std::lock_guard<std::mutex> lk(r.mu);
+        r.inboxes.push_back(&inbox);
+        r.n.fetch_add(1, std::memory_order_release);
+    }
     ~KeyTable() {
+        {
+            RetireRegistry &r = registry();
+            std::lock_guard<std::mutex> lk(r.mu);
+            r.inboxes.erase(std::find(r.inboxes.begin(), r.inboxes.end(), &inbox));
+            r.n.fetch_sub(1, std::memory_order_release);
+        }
         if (ks) fpnn_aes_keyset_destroy(ks);
     }
+    // forget the slots of retired encryptors; true when most slots are dead, so the table
+    // should start over (slots are handed out in order and never reused in place)
+    bool collect() {
+        std::vector<uint64_t> dead;
+        {
+            std::lock_guard<std::mutex> lk(registry().mu);
+            dead.swap(inbox.serials);
+        }
+        for (uint64_t s : dead) slot.erase(s);
+        return next >= kTableMinReset && next > 2 * (uint32_t)slot.size();
+    }
+    static constexpr uint32_t kTableMinReset = 1024;
 };
 
 namespace {
 
-// A table past this many slots starts over (slots of dead connections are not tracked).
+// A table past this many slots starts over whatever is live.
 constexpr uint32_t kTableMaxSlots = 1u << 20;
 
 }  // namespace
@@ -214,18 +277,14 @@ EncryptorBatch::~EncryptorBatch() {
     }
 }
 
-uint64_t encryptor_serial() {
-    static std::atomic<uint64_t> next{1};
-    return next.fetch_add(1, std::memory_order_relaxed);
-}
-
 void EncryptorBatch::flush() {
     std::vector<Op> ops;
     ops.swap(_ops);
     _bytes = 0;
     if (ops.empty()) return;
     int rc;
-    fpnn_aes_engine *e = thread_engine(&rc);
+    uint64_t eid = 0;
+    fpnn_aes_engine *e = thread_engine(&rc, &eid);
     if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
     // group by (mode, direction, wire prefix, rounds); queue order is kept inside a group
     struct Group {
@@ -257,13 +316,13 @@ void EncryptorBatch::flush() {
     for (const Group &gr : groups) {
         // ---- this key length's table: new connections get slots, uploaded in one copy ----
         KeyTable *&tp = _tables[(gr.nrounds - 10) / 2];
-        if (tp && tp->e != e) {  // flushed from another thread (engine): start a table there
+        if (tp && tp->engine_id != eid) {  // flushed from another thread (engine): start a table there
             delete tp;
             tp = nullptr;
         }
         if (!tp) {
             tp = new KeyTable();
-            tp->e = e;
+            tp->engine_id = eid;
             rc = fpnn_aes_keyset_reserve(e, 1024, gr.nrounds, &tp->ks);
             if (rc != FPNN_AES_OK) {
                 delete tp;
@@ -272,6 +331,10 @@ void EncryptorBatch::flush() {
             }
         }
         KeyTable &t = *tp;
+        if (t.collect()) {  // mostly dead connections: start over (live ones re-add below or later)
+            t.slot.clear();
+            t.next = 0;
+        }
         std::vector<const Encryptor *> members;  // first use in this group, in order
         std::vector<uint32_t> slots(gr.idx.size());
         for (int attempt = 0;; attempt++) {

@@ -213,11 +213,17 @@ struct fpnn_aes_engine {
     uint64_t cap_fr_slot = 0;
     RaggedPlan *d_plan = nullptr;  // K1r: one entry per wave of the decrypt grid
     uint64_t cap_plan = 0;
+    uint4 *d_sink = nullptr;  // K1r: 2 x uint4 per wave, stores of lanes with nothing to store
+    uint64_t cap_sink = 0;
     uint64_t *d_desc_off = nullptr;  // K1r: materialized in_off / len of stride / uniform batches
     uint64_t cap_desc_off = 0;
     uint32_t *d_desc_len = nullptr;
     uint64_t cap_desc_len = 0;
     uint64_t *d_total = nullptr;  // ragged block total (bstart[count]), device only
+    uint8_t *d_ecdh = nullptr;  // ECDH host forms / keyset: peers | keys | ivs | ok (grown, kept)
+    uint64_t cap_ecdh = 0;
+    bool pools = false;            // stream-ordered allocation (hipMallocAsync) for grow()
+    std::vector<void *> deferred;  // grown-out scratch awaiting an idle stream (no pools)
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
@@ -270,17 +276,40 @@ struct DeviceGuard {
     }
 };
 
+// Scratch growth on the call path never frees synchronously: hipFree waits for the whole
+// device, so one thread's first large call would stall every other engine's queued work.
+// With stream-ordered pools the old buffer is released by hipFreeAsync behind the work
+// already queued on this engine's stream; without them it is kept until engine_sync /
+// engine_destroy.
 template <class T>
-int grow(T *&ptr, uint64_t &cap, uint64_t need) {
+int grow(fpnn_aes_engine *e, T *&ptr, uint64_t &cap, uint64_t need) {
     if (need <= cap) return FPNN_AES_OK;
     uint64_t n = cap ? cap : 1024;
     while (n < need) n *= 2;
-    if (ptr) HIP_TRY(hipFree(ptr));
-    ptr = nullptr;
-    cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ptr), n * sizeof(T)));
+    T *np = nullptr;
+    if (e->pools)
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&np), n * sizeof(T), e->stream));
+    else
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&np), n * sizeof(T)));
+    if (ptr) {
+        if (e->pools) HIP_TRY(hipFreeAsync(ptr, e->stream));
+        else e->deferred.push_back(ptr);
+    }
+    ptr = np;
     cap = n;
     return FPNN_AES_OK;
+}
+
+// a grow()-managed buffer at engine teardown (the stream is idle)
+void release_scratch(fpnn_aes_engine *e, void *p) {
+    if (!p) return;
+    if (e->pools) (void)hipFreeAsync(p, e->stream);
+    else (void)hipFree(p);
+}
+
+void free_deferred(fpnn_aes_engine *e) {  // the engine's stream is idle
+    for (void *p : e->deferred) (void)hipFree(p);
+    e->deferred.clear();
 }
 
 int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
@@ -366,8 +395,8 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         const uint64_t want = (lanes + threads - 1) / threads;
         const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
         if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
-            if ((rc = grow(e->d_perm, e->cap_perm, b->count))) return rc;
-            if ((rc = grow(e->d_buckets, e->cap_buckets, 256))) return rc;
+            if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
+            if ((rc = grow(e, e->d_buckets, e->cap_buckets, 256))) return rc;
             if (stream) {  // bucket sizes read pos_state (the encrypt kernel reads it later)
                 k.pos_snap = pos_state;
             }
@@ -378,10 +407,18 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // ragged and more chains than quads: a work queue balances them (with fewer
         // chains every quad holds at most one and the grid stride is cheaper)
         const bool queue = b->len && (e->variant.queue == 2 || (e->variant.queue == 1 && lanes > full_chip));
-        if (queue && (rc = grow(e->d_next, e->cap_next, 1))) return rc;
+        if (queue && (rc = grow(e, e->d_next, e->cap_next, 2))) return rc;
         if (queue && e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
+        const bool hybrid = queue && e->variant.hybrid && b->count > 1;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-        if (queue)
+        if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
+            HybridArgs h;
+            h.ctr = e->d_next;
+            h.buckets = e->d_buckets;
+            h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
+            h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
+            HIP_TRY(launch_encrypt_hybrid(k, h, b->keys->nrounds, km, stream, e->variant.fence, e->num_cus, e->stream));
+        } else if (queue)
             HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));
         else
             HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
@@ -414,8 +451,8 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // small ragged batches: block map (+ stream snapshot) in one single-workgroup kernel
     const bool small_map = b->count <= block_map_small_max();
     if (stream) {  // snapshot the incoming (iv, pos) state, see KBatch::iv_snap
-        if ((rc = grow(e->d_snap_iv, e->cap_snap_iv, b->count))) return rc;
-        if ((rc = grow(e->d_snap_pos, e->cap_snap_pos, b->count))) return rc;
+        if ((rc = grow(e, e->d_snap_iv, e->cap_snap_iv, b->count))) return rc;
+        if ((rc = grow(e, e->d_snap_pos, e->cap_snap_pos, b->count))) return rc;
         if (!small_map) {  // (stream batches always take the general layout below)
             HIP_TRY(hipMemcpyAsync(e->d_snap_iv, iv_state, 16ull * b->count, hipMemcpyDeviceToDevice, e->stream));
             HIP_TRY(hipMemcpyAsync(e->d_snap_pos, pos_state, 4ull * b->count, hipMemcpyDeviceToDevice, e->stream));
@@ -459,10 +496,11 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // K1r: block-map scan, per-wave plan and decrypt all on the device; the host
         // never learns the block total, so nothing here waits for the GPU
         const uint64_t nwg = (b->count + 1023) / 1024;
-        if ((rc = grow(e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
-        if ((rc = grow(e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
+        if ((rc = grow(e, e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
+        if ((rc = grow(e, e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
         const int grid = e->num_cus;
-        if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
+        if ((rc = grow(e, e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
+        if ((rc = grow(e, e->d_sink, e->cap_sink, 2ull * grid * (kThreads / 64)))) return rc;
         if (small_map)
             HIP_TRY(launch_block_map_small(k, stream, iv_state, pos_state, e->d_snap_iv, e->d_snap_pos, e->d_bstart,
                                            e->d_total, e->stream));
@@ -470,8 +508,8 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         k.bstart = e->d_bstart;
         if (!k.in_off || !k.len) {  // K1r reads descriptor arrays: materialize the missing ones
-            if (!k.in_off && (rc = grow(e->d_desc_off, e->cap_desc_off, b->count))) return rc;
-            if (!k.len && (rc = grow(e->d_desc_len, e->cap_desc_len, b->count))) return rc;
+            if (!k.in_off && (rc = grow(e, e->d_desc_off, e->cap_desc_off, b->count))) return rc;
+            if (!k.len && (rc = grow(e, e->d_desc_len, e->cap_desc_len, b->count))) return rc;
             HIP_TRY(launch_ragged_desc(b->count, b->stride, b->uniform_len, k.in_off ? nullptr : e->d_desc_off,
                                        k.len ? nullptr : e->d_desc_len, e->stream));
             if (!k.in_off) k.in_off = e->d_desc_off;
@@ -480,13 +518,13 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if (!k.out_off) k.out_off = k.in_off;
         EventPair *ev = nullptr;
         if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, grid, e->stream));
+        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, e->d_sink, e->variant.fence, grid, e->stream));
         return timing_end(e, ev, FPNN_AES_K_DECRYPT);
     }
     EventPair *ev = nullptr;
     const uint64_t nchunks = (k.total_blocks + 63) >> 6;
     if (inplace) {
-        if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks))) return rc;
+        if ((rc = grow(e, e->d_boundary, e->cap_boundary, nchunks))) return rc;
         HIP_TRY(launch_boundary_save(k, e->d_boundary, nchunks, e->stream));
         k.boundary = e->d_boundary;
     }
@@ -572,6 +610,10 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     e->num_cus = prop.multiProcessorCount;
     if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
     if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
+    if (const char *v = getenv("FPNN_AES_HYBRID")) e->variant.hybrid = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_FENCE")) e->variant.fence = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
+    if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
@@ -579,6 +621,19 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
         const int c = atoi(v);
         e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;
+    }
+    {  // stream-ordered scratch allocation; the pool keeps freed memory for reuse
+        int pools = 0;
+        const char *v = getenv("FPNN_AES_POOLS");
+        if ((!v || atoi(v) != 0) &&
+            hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device) == hipSuccess && pools) {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+                uint64_t keep = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+                e->pools = true;
+            }
+        }
     }
     int rc = FPNN_AES_OK;
     do {
@@ -612,19 +667,13 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     DeviceGuard g(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     (void)hipFree(e->d_tables);
-    (void)hipFree(e->d_bstart);
-    (void)hipFree(e->d_wgsums);
-    (void)hipFree(e->d_boundary);
-    (void)hipFree(e->d_snap_iv);
-    (void)hipFree(e->d_snap_pos);
-    (void)hipFree(e->d_perm);
-    (void)hipFree(e->d_next);
-    (void)hipFree(e->d_buckets);
-    (void)hipFree(e->d_fr_off);
-    (void)hipFree(e->d_fr_slot);
-    (void)hipFree(e->d_plan);
-    (void)hipFree(e->d_desc_off);
-    (void)hipFree(e->d_desc_len);
+    for (void *p : {(void *)e->d_bstart, (void *)e->d_wgsums, (void *)e->d_boundary, (void *)e->d_snap_iv,
+                    (void *)e->d_snap_pos, (void *)e->d_perm, (void *)e->d_next, (void *)e->d_buckets,
+                    (void *)e->d_fr_off, (void *)e->d_fr_slot, (void *)e->d_plan, (void *)e->d_sink,
+                    (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh})
+        release_scratch(e, p);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    free_deferred(e);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -659,6 +708,7 @@ int fpnn_aes_engine_sync(fpnn_aes_engine *e) {
     if (!e) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
     HIP_TRY(hipStreamSynchronize(e->stream));
+    free_deferred(e);
     return FPNN_AES_OK;
 }
 
@@ -668,11 +718,11 @@ int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t 
     if (!e) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
     int rc;
-    if ((rc = grow(e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
-    if ((rc = grow(e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
+    if ((rc = grow(e, e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
+    if ((rc = grow(e, e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
     const uint64_t nchunks = (max_blocks + 63) / 64;
-    if ((rc = grow(e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
-    if ((rc = grow(e->d_plan, e->cap_plan, (uint64_t)e->num_cus * (kThreads / 64)))) return rc;
+    if ((rc = grow(e, e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
+    if ((rc = grow(e, e->d_plan, e->cap_plan, (uint64_t)e->num_cus * (kThreads / 64)))) return rc;
     return FPNN_AES_OK;
 }
 
@@ -887,8 +937,8 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
     if (slots > 0xffffffffull) return FPNN_AES_ERR_RANGE;
     DeviceGuard g(e->device);
     const bool per_key = b->key_slot && b->keys->count > 1;
-    if ((rc = grow(e->d_fr_off, e->cap_fr_off, slots))) return rc;
-    if (per_key && (rc = grow(e->d_fr_slot, e->cap_fr_slot, slots))) return rc;
+    if ((rc = grow(e, e->d_fr_off, e->cap_fr_off, slots))) return rc;
+    if (per_key && (rc = grow(e, e->d_fr_slot, e->cap_fr_slot, slots))) return rc;
     KScan s;
     memset(&s, 0, sizeof s);
     s.buf = b->in;
@@ -2167,13 +2217,12 @@ int fpnn_ecdh_keyset(fpnn_aes_engine *e, int curve, const uint8_t *private_key, 
     *out = nullptr;
     if (keylen != 16 && keylen != 32) return FPNN_AES_ERR_KEYLEN;
     DeviceGuard g(e->device);
-    uint8_t *tmp = nullptr;  // keys | ivs | ok
     const size_t kb = (size_t)count * keylen, ib = (size_t)count * 16;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&tmp), kb + ib + count));
-    int rc = fpnn_ecdh_calc_keys(e, curve, private_key, peer_public, count, keylen, tmp, tmp + kb,
-                                 ok ? ok : tmp + kb + ib);
+    int rc = grow(e, e->d_ecdh, e->cap_ecdh, kb + ib + count);  // keys | ivs | ok, engine scratch
+    if (rc) return rc;
+    uint8_t *tmp = e->d_ecdh;
+    rc = fpnn_ecdh_calc_keys(e, curve, private_key, peer_public, count, keylen, tmp, tmp + kb, ok ? ok : tmp + kb + ib);
     if (!rc) rc = fpnn_aes_keyset_create(e, count, (size_t)keylen, tmp, tmp + kb, 0, out);  // synchronizes
-    (void)hipFree(tmp);
     return rc;
 }
 
@@ -2186,9 +2235,9 @@ int fpnn_ecdh_calc_keys_host(fpnn_aes_engine *e, int curve, const uint8_t *priva
     if (count == 0) return FPNN_AES_OK;
     DeviceGuard g(e->device);
     const size_t pb = (size_t)count * 2 * sl, kb = (size_t)count * keylen, ib = (size_t)count * 16;
-    uint8_t *d = nullptr;  // peers | keys | ivs | ok
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), pb + kb + ib + count));
-    int rc = FPNN_AES_OK;
+    int rc = grow(e, e->d_ecdh, e->cap_ecdh, pb + kb + ib + count);  // peers | keys | ivs | ok
+    if (rc) return rc;
+    uint8_t *d = e->d_ecdh;
     do {
         hipError_t err = hipMemcpyAsync(d, peer_public, pb, hipMemcpyHostToDevice, e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
@@ -2201,7 +2250,6 @@ int fpnn_ecdh_calc_keys_host(fpnn_aes_engine *e, int curve, const uint8_t *priva
         if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
-    (void)hipFree(d);
     return rc;
 }
 
@@ -2215,9 +2263,9 @@ int fpnn_ecdh_calc_key_host(fpnn_aes_engine *e, const char *curve, const uint8_t
     if (keylen != 16 && keylen != 32) return 0;
     if (!key || !iv) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
-    uint8_t *d = nullptr;  // peer (<= 64) | key (32) | iv (16) | ok
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), 64 + 32 + 16 + 16));
-    int rc = FPNN_AES_OK;
+    int rc = grow(e, e->d_ecdh, e->cap_ecdh, 64 + 32 + 16 + 16);  // peer (<= 64) | key (32) | iv (16) | ok
+    if (rc) return rc;
+    uint8_t *d = e->d_ecdh;
     uint8_t res[32 + 16 + 1];
     do {
         hipError_t err = hipMemcpyAsync(d, peer_public, peer_len, hipMemcpyHostToDevice, e->stream);
@@ -2227,7 +2275,6 @@ int fpnn_ecdh_calc_key_host(fpnn_aes_engine *e, const char *curve, const uint8_t
         if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
-    (void)hipFree(d);
     if (rc) return rc;
     if (!res[48]) return 0;
     memcpy(key, res, (size_t)keylen);
@@ -2240,9 +2287,9 @@ int fpnn_ecdh_public_key_host(fpnn_aes_engine *e, int curve, const uint8_t *priv
     const int pl = fpnn_ecdh_private_len(curve), sl = fpnn_ecdh_secret_len(curve);
     if (pl < 0) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
-    uint8_t *d = nullptr;  // private (<= 32) | public (<= 64) | ok
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), 32 + 64 + 16));
-    int rc = FPNN_AES_OK;
+    int rc = grow(e, e->d_ecdh, e->cap_ecdh, 32 + 64 + 16);  // private (<= 32) | public (<= 64) | ok
+    if (rc) return rc;
+    uint8_t *d = e->d_ecdh;
     uint8_t res[64 + 1];
     do {
         hipError_t err = hipMemcpyAsync(d, private_key, (size_t)pl, hipMemcpyHostToDevice, e->stream);
@@ -2253,7 +2300,6 @@ int fpnn_ecdh_public_key_host(fpnn_aes_engine *e, int curve, const uint8_t *priv
         if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
-    (void)hipFree(d);
     if (rc) return rc;
     memcpy(public_key, res, (size_t)(2 * sl));
     return res[64] ? 1 : 0;

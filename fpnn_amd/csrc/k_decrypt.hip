@@ -157,7 +157,7 @@ typedef __attribute__((address_space(4))) const uint32_t ConstU32;
 //   KEYED: one key per packet (key_slot[] with the dense layout, chunk-aligned packets:
 //   the C5 shape).  A step's U chunks never straddle two packets (U divides nb/64), so
 //   the step's key is wave-uniform: slot and round keys are scalar loads per step.
-template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED>
+template <int NR, bool INPLACE, int NT, bool ALIGNED, int U, int IL, bool PF, bool KEYED, bool FENCE = false>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_decrypt_dense(KBatch b) {
     static_assert(U % IL == 0, "IL-way interleave of U chunks");
     static_assert(!KEYED || ALIGNED, "per-packet keys need chunk-aligned packets");
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
             uint4 grp[IL];
 #pragma unroll
             for (int m = 0; m < IL; m++) grp[m] = ks[j + m];
-            aes_encrypt_blocks<NR, NT, IL>(grp, rk, T);
+            aes_encrypt_blocks<NR, NT, IL, FENCE>(grp, rk, T);
 #pragma unroll
             for (int m = 0; m < IL; m++) ks[j + m] = grp[m];
         }
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) void k_boundary_save(KBatch b, uint4 *boundary
 constexpr int dec_u(bool stream, int km) { return (!stream && km == KEY_UNIFORM) ? 4 : 1; }
 
 template <int NR, bool INPLACE, int NT>
-static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, int grid, hipStream_t st) {
+static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, bool fence, int grid, hipStream_t st) {
 #define FPNN_DEC(L, NTX) \
     hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, KEY_UNIFORM, false, INPLACE, NTX, 4, 1>), dim3(grid), \
                        dim3(kThreads), 0, st, b)
@@ -389,7 +389,11 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, in
         else if (nbc % 2 == 0) FPNN_DENSE(true, 2, true, true);
         else FPNN_DENSE(true, 1, true, true);
     } else if (layout == LAYOUT_FULL && dense == 2) {
-        if (aligned) FPNN_DENSE(true, 4, true, false); else FPNN_DENSE(false, 4, true, false);
+        if (aligned && fence && NT == 4)  // the C2 decrypt with fenced rounds (Variant::fence)
+            hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, true, 4, 1, true, false, true>), dim3(grid),
+                               dim3(kThreads), 0, st, b);
+        else if (aligned) FPNN_DENSE(true, 4, true, false);
+        else FPNN_DENSE(false, 4, true, false);
     } else if (layout == LAYOUT_FULL && dense) {
         if (aligned) FPNN_DENSE(true, 4, false, false); else FPNN_DENSE(false, 4, false, false);
     } else if (layout == LAYOUT_FULL) {
@@ -406,11 +410,11 @@ static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km,
                    hipStream_t st) {
     const int dense = b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0;
     if (v.tables == 2 && km == KEY_UNIFORM) {
-        if (inplace) dec_launch<NR, true, 2>(b, layout, km, dense, grid, st);
-        else dec_launch<NR, false, 2>(b, layout, km, dense, grid, st);
+        if (inplace) dec_launch<NR, true, 2>(b, layout, km, dense, v.fence, grid, st);
+        else dec_launch<NR, false, 2>(b, layout, km, dense, v.fence, grid, st);
     } else {
-        if (inplace) dec_launch<NR, true, 4>(b, layout, km, dense, grid, st);
-        else dec_launch<NR, false, 4>(b, layout, km, dense, grid, st);
+        if (inplace) dec_launch<NR, true, 4>(b, layout, km, dense, v.fence, grid, st);
+        else dec_launch<NR, false, 4>(b, layout, km, dense, v.fence, grid, st);
     }
 }
 

@@ -6,14 +6,14 @@
 //   K2c k_cfb_encrypt_coop   : one lane quad per chain (few / long chains).
 //   K2q k_cfb_encrypt_queue  : K2c with a work queue (many ragged chains).
 //   All are persistent: workgroups walk the chains with a grid stride or the queue.
-#include "segments.hpp"
+#include "coop.hpp"
 
 namespace fpnn_aes {
 
 // ---------------------------------------------------------------------------
 // K2: encryption, one lane per chain.
 
-template <int NR, int LAYOUT, int KM, bool STREAM, int NT, int CH>
+template <int NR, int LAYOUT, int KM, bool STREAM, int NT, int CH, bool FENCE = false>
 __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_encrypt_chains(KBatch b) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
                 for (int j = 0; j < C; j++) nx[j] = more ? load16(p + 16 * (C + j)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
                 for (int j = 0; j < C; j++) {
-                    iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ a[j];
+                    iv = (FENCE ? aes_encrypt_block_fenced<NR, NT>(iv, rk, T) : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ a[j];
                     a[j] = iv;
                 }
 #pragma unroll
@@ -143,69 +143,6 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 // therefore issues 4 LDS reads per lane and round instead of 16 -- 4x the lanes per
 // chain and ~4x shorter per-chain critical path -- and holds 15 round-key words per
 // lane instead of 60.  Used when chains are few (streams) or long/ragged.
-
-// value held by lane (q + SHIFT) & 3 of this lane's quad.  bound_ctrl: every lane has a
-// source under quad_perm, so no "old" value is needed (update_dpp with old = 0 costs a
-// v_mov per call to materialise it -- 3 of the 12 VALU of a K2c round).
-template <int SHIFT>
-__device__ __forceinline__ uint32_t quad_from(uint32_t v) {
-    constexpr int ctl = ((0 + SHIFT) & 3) | (((1 + SHIFT) & 3) << 2) | (((2 + SHIFT) & 3) << 4) | (((3 + SHIFT) & 3) << 6);
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctl, 0xf, 0xf, true);
-}
-
-// XOR of a and the value b holds in lane (q + SHIFT) & 3: one v_xor_b32 with a DPP
-// quad_perm source (the mov_dpp folds into the xor).
-template <int SHIFT>
-__device__ __forceinline__ uint32_t xor_quad_from(uint32_t a, uint32_t b) {
-    return a ^ quad_from<SHIFT>(b);
-}
-
-// Round structure: lane q looks up ITS OWN four bytes -- T0[b0] feeds output column q,
-// T1[b1] column q-1, T2[b2] column q-2, T3[b3] column q-3 -- and the quad then sums
-// the contributions with DPP-sourced XORs.  Per lane and round: 4 v_perm + 4 ds_read
-// + 3 DPP ops + 1 v_bitop3 = 8 VALU, and every DPP operand is an LDS result or a round
-// key, never a fresh VALU result, so no hazard wait states (moving the state words to
-// the neighbours first costs 9 VALU plus an s_nop per round).
-template <int NR, int NT>
-__device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32_t *rkq, const Tables4<NT> &T) {
-    uint32_t s0 = sq ^ rkq[0];
-#pragma unroll
-    for (int r = 1; r < NR; r++) {
-        const uint32_t t0 = T.template t<0>(s0), t1 = T.template t<1>(s0), t2 = T.template t<2>(s0),
-                       t3 = T.template t<3>(s0);
-        // three independent DPP ops whose other operand is an LDS result or a round key
-        // (a chain of DPP xors would need 2 wait states between them), then one xor3
-        s0 = xor3(xor_quad_from<1>(t0, t1), xor_quad_from<2>(rkq[r], t2), quad_from<3>(t3));
-    }
-    // final round: S(byte j) of the own word, masked to byte j, summed the same way
-    const uint32_t m0 = T.template sraw<0>(s0) & 0x000000ffu, m1 = T.template sraw<1>(s0) & 0x0000ff00u,
-                   m2 = T.template sraw<2>(s0) & 0x00ff0000u, m3 = T.template sraw<3>(s0) & 0xff000000u;
-    return xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(rkq[NR], m2), quad_from<3>(m3));
-}
-
-typedef uint32_t __attribute__((aligned(1))) uint32_u;
-
-// bytes [lo, hi) of this lane's word (word covers block bytes [4q, 4q+4))
-__device__ __forceinline__ uint32_t load_word_bytes(const uint8_t *p, int lo, int hi) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-        if (j >= lo && j < hi) w |= (uint32_t)p[j] << (8 * j);
-    return w;
-}
-
-__device__ __forceinline__ void store_word_bytes(uint8_t *p, uint32_t w, int lo, int hi) {
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-        if (j >= lo && j < hi) p[j] = (uint8_t)(w >> (8 * j));
-}
-
-__device__ __forceinline__ uint32_t word_mask(int lo, int hi) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) m |= (j >= lo && j < hi) ? (0xffu << (8 * j)) : 0u;
-    return m;
-}
 
 template <int NR, int LAYOUT, int KM, bool STREAM, int NT>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
@@ -526,11 +463,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_queue(KBatch b, uin
 // use the 4-table layout (one workgroup per CU); uniform-key variants take the
 // layout the engine asks for.
 template <int NR, int NT, int CH>
-static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads,
+static void enc_launch(const KBatch &b, Layout layout, KeyMode km, bool stream, bool fence, int grid, int threads,
                        hipStream_t st) {
 #define FPNN_ENC(L, K, S, NTX) \
     hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, NTX, CH>), dim3(grid), dim3(threads), 0, st, b)
-    if (layout == LAYOUT_UNIFORM) {
+    if (layout == LAYOUT_UNIFORM && !stream && fence && NT == 4 && CH == 8) {  // C2 with fenced rounds
+        hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_UNIFORM, KEY_UNIFORM, false, 4, 8, true>), dim3(grid),
+                           dim3(threads), 0, st, b);
+    } else if (layout == LAYOUT_UNIFORM) {
         if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, NT);
     } else if (km == KEY_UNIFORM) {
         if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true, NT); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false, NT);
@@ -544,12 +484,12 @@ template <int NR>
 static void enc_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool stream, int grid, int threads,
                    hipStream_t st) {
     if (v.tables == 2) {
-        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, grid, threads, st);
-        else enc_launch<NR, 2, 1>(b, layout, km, stream, grid, threads, st);
+        if (v.enc_chunk == 4) enc_launch<NR, 2, 4>(b, layout, km, stream, v.fence, grid, threads, st);
+        else enc_launch<NR, 2, 1>(b, layout, km, stream, v.fence, grid, threads, st);
     } else {
-        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, grid, threads, st);
-        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, grid, threads, st);
-        else enc_launch<NR, 4, 1>(b, layout, km, stream, grid, threads, st);
+        if (v.enc_chunk == 8) enc_launch<NR, 4, 8>(b, layout, km, stream, v.fence, grid, threads, st);
+        else if (v.enc_chunk == 4) enc_launch<NR, 4, 4>(b, layout, km, stream, v.fence, grid, threads, st);
+        else enc_launch<NR, 4, 1>(b, layout, km, stream, v.fence, grid, threads, st);
     }
 }
 

@@ -138,8 +138,9 @@ __device__ __forceinline__ void set_keys(RoundKeys<NR> &rk, ConstDevKeyR *kp) {
     }
 }
 
-template <int NR, bool STREAM, int KM>
-__global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, const RaggedPlan *__restrict__ plan) {
+template <int NR, bool STREAM, int KM, bool FENCE>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, const RaggedPlan *__restrict__ plan,
+                                                                     uint4 *sink) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
     lds_fill_tables<4>(lds4, b.t0le);
     __syncthreads();
@@ -164,8 +165,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         ivu = make_uint4(ivp[0], ivp[1], ivp[2], ivp[3]);
     }
     const uint8_t *dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 16 readable bytes
-    // 32 writable bytes that nobody reads after the first lines below: this wave's plan entry
-    uint8_t *scratch = reinterpret_cast<uint8_t *>(const_cast<RaggedPlan *>(plan) + w);
+    // 32 writable bytes that nobody reads: this wave's sink entry (not its plan entry,
+    // which is read through constant-address loads the compiler may repeat anywhere)
+    uint8_t *scratch = reinterpret_cast<uint8_t *>(sink + 2 * w);
 
     // window: wv = bstart[wb + lane] (all-ones past bstart[count])
     uint64_t wb = ((ConstU64R *)&plan[w].s0)[0];
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         if (X.bi == 0) kin = ivs;
         uint4 ks;
         if (KM == KEY_UNIFORM) {
-            ks = aes_encrypt_block<NR, 4>(kin, rku, T);
+            ks = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
         } else {
             // one pass per distinct key slot in the chunk, each with wave-uniform (SGPR)
             // round keys; a lane keeps the pass of its own slot.  Chunks inside one segment
@@ -332,11 +334,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                         set_keys(rku, (ConstDevKeyR *)b.keys + slotk);
                         key_slot = slotk;
                     }
-                    e = aes_encrypt_block<NR, 4>(kin, rku, T);
+                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
                 } else {
                     RoundKeys<NR> rk;
                     set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
-                    e = aes_encrypt_block<NR, 4>(kin, rk, T);
+                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rk, T);
                 }
                 if (mine) ks = e;
             } while (todo);
@@ -411,10 +413,11 @@ hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_
     return hipGetLastError();
 }
 
-template <int NR>
-static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, int grid, hipStream_t st) {
+template <int NR, bool F>
+static void ragged_nrf(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, int grid,
+                       hipStream_t st) {
 #define FPNN_RAGGED(S, K) \
-    hipLaunchKernelGGL((k_cfb_decrypt_ragged<NR, S, K>), dim3(grid), dim3(kThreads), 0, st, b, plan)
+    hipLaunchKernelGGL((k_cfb_decrypt_ragged<NR, S, K, F>), dim3(grid), dim3(kThreads), 0, st, b, plan, sink)
     if (stream) {
         if (km == KEY_LANE) FPNN_RAGGED(true, KEY_LANE); else FPNN_RAGGED(true, KEY_UNIFORM);
     } else {
@@ -423,8 +426,15 @@ static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan
 #undef FPNN_RAGGED
 }
 
-hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, int grid,
-                                 hipStream_t st) {
+template <int NR>
+static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, bool fence,
+                      int grid, hipStream_t st) {
+    if (fence) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
+    else ragged_nrf<NR, false>(b, km, stream, plan, sink, grid, st);
+}
+
+hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
+                                 bool fence, int grid, hipStream_t st) {
     const uint64_t nwaves = (uint64_t)grid * (kThreads / 64);
     const unsigned pgrid = (unsigned)((nwaves * 64 + 255) / 256);
     if (stream)
@@ -433,9 +443,9 @@ hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool 
         hipLaunchKernelGGL((k_ragged_plan<false>), dim3(pgrid), dim3(256), 0, st, b, nwaves, plan);
     set_launched("cfb_decrypt_ragged");
     switch (nrounds) {
-        case 10: ragged_nr<10>(b, km, stream, plan, grid, st); break;
-        case 12: ragged_nr<12>(b, km, stream, plan, grid, st); break;
-        case 14: ragged_nr<14>(b, km, stream, plan, grid, st); break;
+        case 10: ragged_nr<10>(b, km, stream, plan, sink, fence, grid, st); break;
+        case 12: ragged_nr<12>(b, km, stream, plan, sink, fence, grid, st); break;
+        case 14: ragged_nr<14>(b, km, stream, plan, sink, fence, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

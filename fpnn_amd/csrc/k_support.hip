@@ -163,6 +163,14 @@ __device__ __forceinline__ uint32_t length_bucket(const KBatch &b, uint64_t s) {
     return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);  // descending length
 }
 
+uint32_t length_bucket_of(uint64_t nblocks) {
+    const uint64_t nb = nblocks + 1;
+    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
+    const int lz = 31 - __builtin_clz(x);
+    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
+    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);
+}
+
 template <bool STREAM>
 __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts) {
     __shared__ uint32_t h[kBuckets];

@@ -61,8 +61,12 @@ struct Variant {
     int enc_align = 1;     // K2: run a chain's blocks before its first 128-B line boundary singly
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
     int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
+    int hybrid = 1;        // ragged batches that take the queue: K2h (lanes + quads) instead of K2q
+    int hyb_long = 512;    // K2h: chains of at least this many blocks (bucket-rounded) go to quads
+    int hyb_quad_waves = 8;  // K2h: waves per workgroup that start on the long chains
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
+    int fence = 1;         // K2 / K1d (C2 shape), K1r, K2h: issue each round's 16 lookups before folding
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
@@ -108,6 +112,20 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
 // next = one device word of scratch (zeroed here, on the stream).
 hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool stream, int grid, int threads,
                                 uint32_t *next, hipStream_t st);
+// K2h (k_hybrid.hip): ragged batches with more chains than quads.  Chains of perm[]
+// in length buckets <= long_bucket run on quads (K2c's cipher), the rest one per lane
+// (K2's); quad_waves waves per workgroup start on the long ones.  ctr: 2 device words
+// (zeroed here, on the stream); buckets: launch_length_order's counts.
+struct HybridArgs {
+    uint32_t *ctr;
+    const uint32_t *buckets;
+    uint32_t long_bucket;
+    uint32_t quad_waves;
+};
+hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, bool fence,
+                                 int grid, hipStream_t st);
+// length bucket of a block count (descending: bucket 0 = longest), as launch_length_order
+uint32_t length_bucket_of(uint64_t nblocks);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
 // (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
@@ -124,8 +142,9 @@ struct RaggedPlan {
 };
 // b.in_off, b.out_off and b.len must be device arrays (launch_ragged_desc writes the missing
 // ones from stride / uniform_len; out_off may be in_off).
-hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, int grid,
-                                 hipStream_t st);
+// sink: 2 x uint4 per wave of the grid, written by lanes with nothing to store, never read.
+hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
+                                 bool fence, int grid, hipStream_t st);
 hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len, uint64_t *in_off, uint32_t *len,
                               hipStream_t st);
 // In-place K1 / K1d: save the ciphertext block before every 64-block chunk.

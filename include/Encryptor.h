@@ -31,8 +31,11 @@ class EncryptorBatch;  // EncryptorBatch.h: runs queued calls of many encryptors
 
 /* libfpnn_aes.so: a process-unique number per constructed Encryptor -- the key of its
    slot in an EncryptorBatch's persistent device key table (an address can be reused by
-   a later Encryptor, a serial cannot). */
+   a later Encryptor, a serial cannot).  A copy gets a serial of its own (its state then
+   evolves apart from the original's); a destroyed or overwritten Encryptor retires its
+   serial, which frees its slot in every key table at that table's next flush. */
 uint64_t encryptor_serial();
+void encryptor_retire(uint64_t serial);
 
 class EncryptorError : public std::runtime_error {
 public:
@@ -55,7 +58,21 @@ public:
         _keyLen = key_len;
         _serial = encryptor_serial();
     }
-    virtual ~Encryptor() {}
+    Encryptor(const Encryptor &o) : _keyLen(o._keyLen), _serial(encryptor_serial()) {
+        memcpy(_iv, o._iv, 16);
+        memcpy(_key, o._key, sizeof _key);
+    }
+    Encryptor &operator=(const Encryptor &o) {
+        if (this != &o) {
+            memcpy(_iv, o._iv, 16);
+            memcpy(_key, o._key, sizeof _key);
+            _keyLen = o._keyLen;
+            encryptor_retire(_serial);
+            _serial = encryptor_serial();
+        }
+        return *this;
+    }
+    virtual ~Encryptor() { encryptor_retire(_serial); }
 
     virtual void decrypt(uint8_t *dest, uint8_t *src, int len) = 0;
     virtual void encrypt(uint8_t *dest, uint8_t *src, int len) = 0;

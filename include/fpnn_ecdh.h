@@ -64,9 +64,12 @@ int fpnn_ecdh_public_keys(fpnn_aes_engine *e, int curve, const uint8_t *private_
                           uint8_t *public_keys, uint8_t *ok);
 
 /* Server side straight into a key set: derive (key, iv) for every peer and expand the
- * keys on the device (fpnn_aes_keyset_create).  Slot i is connection i; where ok[i] == 0
- * the slot holds the zero-derived key and must not be used (the reference refuses the
- * connection).  ok may be NULL.  Synchronous (returns a usable key set). */
+ * keys on the device (fpnn_aes_keyset_create).  private_key: host; peer_public: DEVICE,
+ * count * 2*secret_len bytes (as fpnn_ecdh_calc_keys); ok: DEVICE, count bytes, or NULL
+ * (the kernel writes it; a host pointer here is a GPU memory fault).  Slot i is
+ * connection i; where ok[i] == 0 the slot holds the zero-derived key and must not be
+ * used (the reference refuses the connection).  Synchronous (returns a usable key set);
+ * the derived keys pass through the engine's own scratch, which is kept between calls. */
 int fpnn_ecdh_keyset(fpnn_aes_engine *e, int curve, const uint8_t *private_key, const uint8_t *peer_public,
                      uint32_t count, int keylen, uint8_t *ok, fpnn_aes_keyset **out);
 

@@ -51,23 +51,71 @@ def engine():
     eng.close()
 
 
-@pytest.fixture(scope="session")
-def queue_engine():
-    """An engine that always uses the K2q work-queue encrypt for ragged batches
-    (by default it only does so when chains outnumber the chip's lane quads)."""
+def _env_engine(env):
+    """An engine created under extra FPNN_AES_* settings (read once, at creation)."""
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU test collected on a machine without a HIP device")
     import fpnn_amd
-    old = os.environ.get("FPNN_AES_QUEUE")
-    os.environ["FPNN_AES_QUEUE"] = "2"
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        eng = fpnn_amd.Engine(0)
+        return fpnn_amd.Engine(0)
     finally:
-        if old is None:
-            del os.environ["FPNN_AES_QUEUE"]
-        else:
-            os.environ["FPNN_AES_QUEUE"] = old
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="session")
+def queue_engine():
+    """An engine that always uses the K2q work-queue encrypt for ragged batches
+    (by default ragged batches with more chains than lane quads take K2h)."""
+    eng = _env_engine({"FPNN_AES_QUEUE": "2", "FPNN_AES_HYBRID": "0"})
+    yield eng
+    eng.sync()
+    eng.close()
+
+
+# K2h (k_hybrid.hip) on every ragged batch, with the long-chain threshold and the number
+# of waves that start on quads set so that small test batches exercise each session:
+#   hybrid_engine       chains of >= 64 blocks on quads, 3 quad waves per workgroup
+#   hybrid_lane_engine  every chain one lane (no quad queue)
+#   hybrid_quad_engine  every chain on quads, no quad waves at start (lane waves join)
+HYBRID_ENGINES = {
+    "hybrid_engine": {"FPNN_AES_HYB_LONG": "64", "FPNN_AES_HYB_QW": "3"},
+    "hybrid_lane_engine": {"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2"},
+    "hybrid_quad_engine": {"FPNN_AES_HYB_LONG": "1", "FPNN_AES_HYB_QW": "0"},
+}
+
+
+def _hybrid(name):
+    env = {"FPNN_AES_QUEUE": "2", "FPNN_AES_HYBRID": "1"}
+    env.update(HYBRID_ENGINES[name])
+    return _env_engine(env)
+
+
+@pytest.fixture(scope="session")
+def hybrid_engine():
+    eng = _hybrid("hybrid_engine")
+    yield eng
+    eng.sync()
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def hybrid_lane_engine():
+    eng = _hybrid("hybrid_lane_engine")
+    yield eng
+    eng.sync()
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def hybrid_quad_engine():
+    eng = _hybrid("hybrid_quad_engine")
     yield eng
     eng.sync()
     eng.close()

@@ -1,6 +1,6 @@
 """Randomized package-mode batches over every layout the engine dispatches on, against
 the oracle, bit-exact.  Each case draws a shape that steers run_encrypt / run_decrypt
-into one kernel family -- K2 / K2c / K2q for encryption; K1d (plain, keyed, ragged),
+into one kernel family -- K2 / K2c / K2q / K2h (three threshold settings) for encryption; K1d (plain, keyed, ragged),
 K1k and K1 for decryption -- plus key lengths, key counts, in-place or not, and
 lengths including 0 and non-multiples of 16.  The decrypt input is the encrypt output
 of the same case, so each case also checks the round trip.  Seeds are fixed."""
@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 
+ENGINES = ["engine", "engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine", "hybrid_quad_engine"]
 SHAPES = ["uniform", "dense", "dense_partial", "keyed_dense", "keyed_lane", "contiguous", "gapped", "ragged_keys"]
 
 
@@ -60,7 +61,7 @@ def test_fuzz_package_batches(request, oracle, seed):
     import fpnn_amd
     rng = np.random.default_rng(4242 + seed)
     shape = SHAPES[seed % len(SHAPES)]
-    engine = request.getfixturevalue("queue_engine" if seed % 3 == 2 else "engine")
+    engine = request.getfixturevalue(ENGINES[(seed + seed // len(SHAPES)) % len(ENGINES)])
     keylen = int(rng.choice([16, 24, 32]))
     n, size, kw, nkeys = _case(rng, shape)
     keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)

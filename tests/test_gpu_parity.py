@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import workloads as W
+from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -125,7 +126,8 @@ def test_golden_cfb_cases_stream_batch(engine, golden):
                 assert int(poso[i]) == c["pos_out"]
 
 
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+                                      "hybrid_quad_engine"])
 def test_golden_package_cases(request, golden, eng_kind):
     engine = request.getfixturevalue(eng_kind)
     import fpnn_amd
@@ -207,7 +209,8 @@ def make_ragged(rng, n, max_len, align_gap=True):
 @pytest.mark.parametrize("keylen", [16, 24, 32])
 @pytest.mark.parametrize("nkeys", [1, 7])
 @pytest.mark.parametrize("inplace", [False, True])
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+                                      "hybrid_quad_engine"])
 def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind):
     engine = request.getfixturevalue(eng_kind)
     rng = np.random.default_rng(1000 * keylen + 10 * nkeys + inplace)
@@ -395,7 +398,8 @@ def test_dense_keyed_layout(engine, oracle, length, inplace):
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine"])
+@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+                                      "hybrid_quad_engine"])
 def test_random_stream_batches(request, oracle, keylen, eng_kind):
     """Many streams, several successive calls each with random lengths; outputs and the
     carried (iv, pos) state must follow the reference byte loop exactly."""
@@ -627,8 +631,13 @@ def test_c4_zipf_vs_oracle(engine, oracle):
     oracle.package_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), lens=sizes.astype(np.uint32),
                          keys=np.frombuffer(key, np.uint8).copy(), keylen=len(key),
                          ivs=np.frombuffer(iv, np.uint8).copy(), threads=min(16, os.cpu_count() or 1))
-    assert np.array_equal(to_host(cipher), exp)
+    got = to_host(cipher)
+    assert np.array_equal(got, exp)
     assert torch.equal(back, plain)
+    # and against the reference itself: digests.json "shards" C4/w1/r0 is the whole batch
+    # encrypted by base/rijndael.c + core/Encryptor.cpp (oracle/_ref, oracle/gen_golden.py)
+    gold = load_golden("digests.json")["shards"]["C4/w1/r0"]
+    assert hashlib.sha256(got.tobytes()).hexdigest() == gold
 
 
 # --------------------------------------------------------------------------------------

@@ -26,20 +26,26 @@ import workloads as W  # noqa: E402
 
 
 def timed(eng, which, fn, reps):
-    import fpnn_amd
-    for _ in range(3):  # warm (clocks ramp; the first calls grow scratch buffers)
+    """Median over `reps` individually timed calls, after two warm-up calls (clocks ramp;
+    the first calls grow scratch buffers): (wall s per call, kernel s per launch of the
+    main kernel `which`, launches per call)."""
+    import statistics
+    for _ in range(2):
         fn()
     torch.cuda.synchronize()
-    eng.reset_stats()
-    eng.set_timing(True)
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    walls, kern, launches = [], [], 0
+    for _ in range(max(1, reps)):
+        eng.reset_stats()
+        eng.set_timing(True)
+        t0 = time.perf_counter()
         fn()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    eng.set_timing(False)
-    n, ms = eng.kernel_stats(which)
-    return wall / reps, ms / max(1, n) / 1e3, n // reps
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        eng.set_timing(False)
+        n, ms = eng.kernel_stats(which)
+        kern.append(ms / max(1, n) / 1e3)
+        launches = n
+    return statistics.median(walls), statistics.median(kern), launches
 
 
 def gib(nbytes, sec):
@@ -48,7 +54,7 @@ def gib(nbytes, sec):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5, help="timed calls per measurement (the median is reported)")
     ap.add_argument("--configs", default="C2,C3,C4,C5,U1,R1")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory / PCIe legs (profiling runs)")
     args = ap.parse_args()
@@ -321,8 +327,8 @@ def main():
             fn(src, dst, S, ks, st_iv, st_pos, stride=L, uniform_len=L, key_slot=slots,
                in_off=torch.arange(S, dtype=torch.int64, device="cuda") * L)
 
-        we, ke, _ = timed(eng, E, lambda: whole(eng.stream_encrypt, a, b), max(1, args.reps // 2))
-        wd, kd, _ = timed(eng, D, lambda: whole(eng.stream_decrypt, b, r), max(1, args.reps // 2))
+        we, ke, _ = timed(eng, E, lambda: whole(eng.stream_encrypt, a, b), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: whole(eng.stream_decrypt, b, r), args.reps)
         assert torch.equal(r, a)
         # framed: one call per frame round (every stream's next frame)
         splits = [W.stream_splits(c, s) for s in range(S)]
@@ -341,8 +347,8 @@ def main():
             for f in range(nmax):
                 fn(src, dst, S, ks, st_iv, st_pos, in_off=d_offs[f], lens=d_lens[f], key_slot=slots)
 
-        wfe, kfe, nfe = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), 1)
-        wfd, kfd, nfd = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), 1)
+        wfe, kfe, nfe = timed(eng, E, lambda: framed(eng.stream_encrypt, a, b), args.reps)
+        wfd, kfd, nfd = timed(eng, D, lambda: framed(eng.stream_decrypt, b, r), args.reps)
         assert torch.equal(r, a)
         if args.no_host:
             out["C3"] = {"whole_stream_encrypt_kernel_GiBs": gib(S * L, ke),
@@ -510,7 +516,8 @@ def main():
         del plain, wire, out_buf
         print(json.dumps({"R2": out["R2"]}), flush=True)
 
-    print(json.dumps({"configs": out}))
+    print(json.dumps({"configs": out, "timing": f"median of {args.reps} individually timed calls after 2 warm-up calls; "
+                                                  "kernel = HIP events around the main kernel on the engine stream"}))
 
 
 if __name__ == "__main__":
