@@ -222,6 +222,10 @@ struct fpnn_aes_engine {
     uint64_t *d_total = nullptr;  // ragged block total (bstart[count]), device only
     uint8_t *d_ecdh = nullptr;  // ECDH host forms / keyset: peers | keys | ivs | ok (grown, kept)
     uint64_t cap_ecdh = 0;
+    uint8_t *d_sstate = nullptr;  // stream host frames: (iv, pos) of the call's streams (grown, kept)
+    uint64_t cap_sstate = 0;
+    uint8_t *h_sstate = nullptr;  // its pinned twin
+    uint64_t cap_hsstate = 0;
     bool pools = false;            // stream-ordered allocation (hipMallocAsync) for grow()
     std::vector<void *> deferred;  // grown-out scratch awaiting an idle stream (no pools)
     // host staging for fpnn_aes_cfb_host
@@ -417,6 +421,12 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             h.buckets = e->d_buckets;
             h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
             h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
+            if ((b->flags & FPNN_AES_F_WIRE_PREFIX) && !e->variant.hyb_wire_lanes) {
+                // wire frames (htole32(len) || C): every chain on quads -- the lane session's
+                // funnel-shifted, line-aligned steps measured 653 vs 800 GiB/s on R1
+                h.long_bucket = 127;
+                h.quad_waves = 16;
+            }
             HIP_TRY(launch_encrypt_hybrid(k, h, b->keys->nrounds, km, stream, e->variant.fence, e->num_cus, e->stream));
         } else if (queue)
             HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));
@@ -614,6 +624,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_FENCE")) e->variant.fence = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
+    if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
@@ -670,13 +681,14 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     for (void *p : {(void *)e->d_bstart, (void *)e->d_wgsums, (void *)e->d_boundary, (void *)e->d_snap_iv,
                     (void *)e->d_snap_pos, (void *)e->d_perm, (void *)e->d_next, (void *)e->d_buckets,
                     (void *)e->d_fr_off, (void *)e->d_fr_slot, (void *)e->d_plan, (void *)e->d_sink,
-                    (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh})
+                    (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh, (void *)e->d_sstate})
         release_scratch(e, p);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_deferred(e);
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_sstate) (void)hipHostFree(e->h_sstate);
     for (auto &v : e->ev)
         for (auto &p : v) {
             (void)hipEventDestroy(p.beg);
@@ -1256,6 +1268,23 @@ struct Piece {
     uint32_t frame, off, len;
 };
 
+// stream-state scratch of the host-frame calls: device (grow(): no free on the call path)
+// and its pinned twin (grown only between calls' uses: the engine stream is drained)
+int sstate_reserve(fpnn_aes_engine *e, uint64_t bytes) {
+    if (int rc = grow(e, e->d_sstate, e->cap_sstate, bytes)) return rc;
+    if (bytes > e->cap_hsstate) {
+        uint64_t c = e->cap_hsstate ? e->cap_hsstate : 4096;
+        while (c < bytes) c *= 2;
+        HIP_TRY(hipStreamSynchronize(e->stream));  // a previous call's state copies are done
+        if (e->h_sstate) (void)hipHostFree(e->h_sstate);
+        e->h_sstate = nullptr;
+        e->cap_hsstate = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_sstate), c, 0));
+        e->cap_hsstate = c;
+    }
+    return FPNN_AES_OK;
+}
+
 // Host-frame pipeline shared by the package and stream entry points.
 //   package: one segment per frame (key slot frames[i].key_slot, fresh chain).
 //   stream : one segment per distinct stream slot = the concatenation of that
@@ -1326,11 +1355,12 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
     } sr;
     if (stream) {
         const uint64_t bytes = nseg * 20;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_state), bytes, 0));
-        if (hipMalloc(reinterpret_cast<void **>(&d_state), bytes) != hipSuccess) {
-            (void)hipHostFree(h_state);
-            return hip_fail(hipErrorOutOfMemory, "hipMalloc(stream state)");
-        }
+        if (int rc = sstate_reserve(e, bytes)) return rc;
+        h_state = e->h_sstate;
+        d_state = e->d_sstate;
+        // (a fresh d_state is stream-ordered on the engine stream: the upload below waits for it)
+        HIP_TRY(hipEventRecord(e->hs[0].kdone, main_stream));
+        HIP_TRY(hipStreamWaitEvent(e->hs[0].st, e->hs[0].kdone, 0));
         sr.rem.resize(nseg);
         sr.fi.assign(nseg, 0);
         sr.fo.assign(nseg, 0);
@@ -1556,8 +1586,6 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
                 pos_state[segs[t].slot] = hp[t];
             }
         }
-        (void)hipFree(d_state);
-        (void)hipHostFree(h_state);
     }
     if (hst.on)
         fprintf(stderr, "[fpnn_aes host] %s %s: %u frames, %llu segments, %llu chunks, %.2f ms total, gather %.2f, "
@@ -1909,6 +1937,294 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
     return rc;
 }
 
+// Stream-mode host frames that all lie in registered memory: the chunking of host_pipeline
+// (one segment per stream = its frames in array order, round-robin quotas so a chunk
+// advances many chains) with mapped_pipeline's moves: on the move stream one launch per
+// step gathers chunk t's pieces from host memory and scatters chunk t - 2's results to
+// the frames' destinations; the engine stream ciphers chunk t - 1 with the streams'
+// carried (iv, pos) -- chunks in order, so a stream split across chunks continues from
+// the state the previous chunk left -- then uploads chunk t + 1's descriptors.
+// Descriptor block of a chunk: per piece src u64 | so u64 | dst u64 | oo u64 | len u32,
+// then per stream segment off u64 | len u32 | slot u32.
+int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
+                           const fpnn_aes_keyset *keys, const MapView &v, uint8_t *iv_state, uint32_t *pos_state) {
+    static const uint64_t kChunk = [] {
+        const char *x = getenv("FPNN_AES_MAP_CHUNK_MB");
+        return (x && atoi(x) > 0 ? (uint64_t)atoi(x) : 32ull) << 20;
+    }();
+    constexpr int kSlots = (int)(sizeof(e->ms) / sizeof(e->ms[0]));
+    // ---- streams in array order (stable counting sort by slot, as host_pipeline) ----
+    std::vector<uint32_t> order(n);
+    {
+        std::vector<uint32_t> cnt((size_t)keys->count + 1, 0);
+        for (uint32_t i = 0; i < n; i++) cnt[frames[i].key_slot + 1]++;
+        for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
+        for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
+    }
+    struct SSeg {
+        uint32_t slot, first, nframes;
+        uint64_t bytes;
+    };
+    std::vector<SSeg> segs;
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t slot = frames[order[i]].key_slot;
+        uint32_t j = i;
+        uint64_t bytes = 0;
+        while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
+        if (bytes) segs.push_back({slot, i, j - i, bytes});
+        i = j;
+    }
+    if (segs.empty()) return FPNN_AES_OK;
+    const uint64_t nseg = segs.size();
+    HostStats hst;
+    const double t_call = hst.on ? HostStats::now() : 0;
+    DeviceGuard g(e->device);
+    for (auto &m : e->ms)
+        if (int rc = mslot_reserve(m, 0, 0)) return rc;
+    if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
+    hipStream_t ms = e->map_stream;
+    // ---- the streams' (iv, pos), compact, on the device (engine stream) ----
+    if (int rc = sstate_reserve(e, nseg * 20)) return rc;
+    uint8_t *h_state = e->h_sstate, *d_state = e->d_sstate;
+    std::vector<uint64_t> rem(nseg);
+    std::vector<uint32_t> fi(nseg, 0), fo(nseg, 0);
+    uint64_t left = 0;
+    {
+        uint32_t *hp = reinterpret_cast<uint32_t *>(h_state + 16 * nseg);
+        for (uint64_t t = 0; t < nseg; t++) {
+            memcpy(h_state + 16 * t, iv_state + 16ull * segs[t].slot, 16);
+            hp[t] = pos_state[segs[t].slot] & 15u;
+            rem[t] = segs[t].bytes;
+            left += segs[t].bytes;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(d_state, h_state, nseg * 20, hipMemcpyHostToDevice, e->stream));
+    const uint64_t chunk = std::min<uint64_t>(256ull << 20, std::max<uint64_t>(kChunk, left / 4));
+    const uint64_t quota = std::max<uint64_t>(16u << 10, (chunk / nseg + 15) & ~15ull);
+    // the move stream starts after work already queued on the engine stream
+    HIP_TRY(hipEventRecord(e->ms[0].ciphered, e->stream));
+    HIP_TRY(hipStreamWaitEvent(ms, e->ms[0].ciphered, 0));
+    struct Chunk {
+        uint32_t np = 0, ns = 0;  // pieces, stream segments (np = 0: no chunk in the slot)
+        uint64_t state0 = 0, out_at = 0, desc_at = 0, desc_b = 0;
+    } ch[kSlots];
+    uint64_t next = 0;  // round-robin cursor over segs
+    auto jobs_of = [&](int slot, MoveJob &gather, MoveJob &scatter) {
+        const Chunk &c = ch[slot];
+        MapSlot &m = e->ms[slot];
+        const uint64_t *d_src = reinterpret_cast<const uint64_t *>(m.d + c.desc_at);
+        const uint64_t *d_so = d_src + c.np, *d_dst = d_so + c.np, *d_oo = d_dst + c.np;
+        const uint32_t *d_len = reinterpret_cast<const uint32_t *>(d_oo + c.np);
+        gather = MoveJob{0, d_src, (uint64_t)(uintptr_t)m.d, d_so, d_len, 0, c.np};
+        scatter = MoveJob{(uint64_t)(uintptr_t)(m.d + c.out_at), d_oo, 0, d_dst, d_len, 0, c.np};
+    };
+    auto seg_arrays = [&](int slot, const uint64_t *&off, const uint32_t *&len, const uint32_t *&sl) {
+        const Chunk &c = ch[slot];
+        const uint8_t *base = e->ms[slot].d + c.desc_at + (uint64_t)c.np * 36;
+        const uint64_t a = ((uint64_t)(uintptr_t)base + 7) & ~7ull;
+        off = reinterpret_cast<const uint64_t *>(a);
+        len = reinterpret_cast<const uint32_t *>(off + c.ns);
+        sl = len + c.ns;
+    };
+    // host: chunk t's pieces and descriptors into its slot's pinned block
+    auto prepare = [&](uint64_t t, int &rc) -> bool {
+        const int k = (int)(t % kSlots);
+        Chunk &c = ch[k];
+        c.np = c.ns = 0;
+        if (left == 0) return false;
+        MapSlot &m = e->ms[k];
+        if (m.busy) {
+            const double tw = hst.on ? HostStats::now() : 0;
+            if (hipError_t err = hipEventSynchronize(m.done)) {
+                rc = hip_fail(err, "hipEventSynchronize");
+                return false;
+            }
+            if (hst.on) hst.wait += HostStats::now() - tw;
+            m.busy = false;
+        }
+        const double tf = hst.on ? HostStats::now() : 0;
+        std::vector<Piece> pieces;
+        struct CS {
+            uint32_t slot;
+            uint64_t at, len;
+        };
+        std::vector<CS> cs;
+        uint64_t s = next < nseg ? next : 0;
+        while (rem[s] == 0) s = s + 1 < nseg ? s + 1 : 0;  // left > 0: terminates
+        c.state0 = s;
+        uint64_t in_b = 0;
+        for (; s < nseg && in_b < chunk; s++) {
+            const SSeg &sg = segs[s];
+            const uint64_t take = std::min(rem[s], quota);
+            uint64_t took = 0;
+            while (took < take) {
+                const uint32_t fidx = order[sg.first + fi[s]];
+                const fpnn_aes_host_frame &f = frames[fidx];
+                const uint32_t part = (uint32_t)std::min<uint64_t>(f.len - fo[s], take - took);
+                if (part) pieces.push_back({fidx, fo[s], part});
+                took += part;
+                fo[s] += part;
+                if (fo[s] == f.len) {
+                    fi[s]++;
+                    fo[s] = 0;
+                }
+            }
+            cs.push_back({sg.slot, in_b, take});
+            rem[s] -= take;
+            left -= take;
+            in_b += take;
+        }
+        next = s;
+        const uint32_t np = (uint32_t)pieces.size(), ns = (uint32_t)cs.size();
+        const uint64_t in_pad = (in_b + 255) & ~255ull;
+        c.out_at = in_pad;
+        c.desc_at = 2 * in_pad;
+        c.desc_b = (uint64_t)np * 36 + 8 + (uint64_t)ns * 16;
+        if (c.desc_at + c.desc_b + 64 > m.dcap || c.desc_b + 64 > m.hcap) {
+            hipError_t err = hipStreamSynchronize(ms);  // growing frees the slot's buffers
+            if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+            if (err != hipSuccess) {
+                rc = hip_fail(err, "hipStreamSynchronize");
+                return false;
+            }
+            if ((rc = mslot_reserve(m, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
+        }
+        uint64_t *h_src = reinterpret_cast<uint64_t *>(m.h);
+        uint64_t *h_so = h_src + np, *h_dst = h_so + np, *h_oo = h_dst + np;
+        uint32_t *h_len = reinterpret_cast<uint32_t *>(h_oo + np);
+        const unsigned parts = np >= 16384 ? pool_of(e)->parts() : 1u;
+        std::vector<uint64_t> at(np);
+        {
+            uint64_t a = 0;
+            for (uint32_t q = 0; q < np; q++) {
+                at[q] = a;
+                a += pieces[q].len;
+            }
+        }
+        pool_of(e)->run(parts, [&](unsigned p) {
+            const uint32_t a0 = (uint32_t)((uint64_t)np * p / parts), b0 = (uint32_t)((uint64_t)np * (p + 1) / parts);
+            long rs = -1, rd = -1;
+            for (uint32_t q = a0; q < b0; q++) {
+                const Piece &pc = pieces[q];
+                const fpnn_aes_host_frame &f = frames[pc.frame];
+                const uintptr_t xs = (uintptr_t)f.src + pc.off, xd = (uintptr_t)f.dst + pc.off;
+                if (rs < 0 || xs < v.lo[rs] || xs + pc.len > v.hi[rs]) rs = v.find((const void *)xs, pc.len);
+                if (rd < 0 || xd < v.lo[rd] || xd + pc.len > v.hi[rd]) rd = v.find((const void *)xd, pc.len);
+                h_src[q] = (uint64_t)((intptr_t)xs + v.delta[rs]);
+                h_so[q] = at[q];
+                h_dst[q] = (uint64_t)((intptr_t)xd + v.delta[rd]);
+                h_oo[q] = at[q];
+                h_len[q] = pc.len;
+            }
+        });
+        const uint64_t sa = (((uint64_t)(uintptr_t)(m.h + (uint64_t)np * 36)) + 7) & ~7ull;
+        uint64_t *h_off = reinterpret_cast<uint64_t *>(sa);
+        uint32_t *h_slen = reinterpret_cast<uint32_t *>(h_off + ns), *h_sslot = h_slen + ns;
+        for (uint32_t q = 0; q < ns; q++) {
+            h_off[q] = cs[q].at;
+            h_slen[q] = (uint32_t)cs[q].len;
+            h_sslot[q] = cs[q].slot;
+        }
+        c.np = np;
+        c.ns = ns;
+        if (hst.on) hst.gather += HostStats::now() - tf;
+        return true;
+    };
+    auto upload = [&](uint64_t t) -> int {
+        const int k = (int)(t % kSlots);
+        MapSlot &m = e->ms[k];
+        HIP_TRY(hipMemcpyAsync(m.d + ch[k].desc_at, m.h, ch[k].desc_b, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipEventRecord(m.done, e->stream));
+        m.busy = true;
+        return FPNN_AES_OK;
+    };
+    int rc = FPNN_AES_OK;
+    if (prepare(0, rc)) rc = upload(0);
+    const MoveJob none{0, nullptr, 0, nullptr, nullptr, 0, 0};
+    for (uint64_t t = 0; rc == FPNN_AES_OK; t++) {
+        const int kt = (int)(t % kSlots), k1 = (int)((t + kSlots - 1) % kSlots), k2 = (int)((t + kSlots - 2) % kSlots);
+        const bool gather_t = ch[kt].np != 0;
+        const bool cipher_t1 = t >= 1 && ch[k1].np != 0;
+        const bool scatter_t2 = t >= 2 && ch[k2].np != 0;
+        if (!gather_t && !cipher_t1 && !scatter_t2) break;
+        MoveJob gj = none, sj = none, tmp;
+        if (gather_t) {
+            HIP_TRY(hipStreamWaitEvent(ms, e->ms[kt].done, 0));
+            jobs_of(kt, gj, tmp);
+        }
+        if (scatter_t2) {
+            HIP_TRY(hipStreamWaitEvent(ms, e->ms[k2].ciphered, 0));
+            jobs_of(k2, tmp, sj);
+        }
+        HIP_TRY(launch_move_segments(gj, sj, ms));
+        if (gather_t) HIP_TRY(hipEventRecord(e->ms[kt].gathered, ms));
+        const bool more = prepare(t + 1, rc);
+        if (rc) break;
+        if (cipher_t1) {
+            const Chunk &c = ch[k1];
+            MapSlot &m = e->ms[k1];
+            HIP_TRY(hipStreamWaitEvent(e->stream, m.gathered, 0));
+            const uint64_t *off;
+            const uint32_t *len, *sl;
+            seg_arrays(k1, off, len, sl);
+            fpnn_aes_batch bt;
+            memset(&bt, 0, sizeof bt);
+            bt.in = m.d;
+            bt.out = m.d + c.out_at;
+            bt.count = c.ns;
+            bt.in_off = off;
+            bt.len = len;
+            bt.key_slot = keys->count > 1 ? sl : nullptr;
+            bt.keys = keys;
+            uint8_t *ivp = d_state + 16 * c.state0;
+            uint32_t *posp = reinterpret_cast<uint32_t *>(d_state + 16 * nseg) + c.state0;
+            rc = encrypt ? run_encrypt(e, &bt, ivp, posp, true) : run_decrypt(e, &bt, ivp, posp, true);
+            if (rc) break;
+            HIP_TRY(hipEventRecord(m.ciphered, e->stream));
+        }
+        if (more && (rc = upload(t + 1))) break;
+        if (scatter_t2) ch[k2].np = 0;
+    }
+    const double td = hst.on ? HostStats::now() : 0;
+    HIP_TRY(hipStreamSynchronize(ms));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (auto &m : e->ms) m.busy = false;
+    for (auto &c : ch) c.np = 0;
+    if (!rc) {
+        HIP_TRY(hipMemcpy(h_state, d_state, nseg * 20, hipMemcpyDeviceToHost));
+        const uint32_t *hp = reinterpret_cast<const uint32_t *>(h_state + 16 * nseg);
+        for (uint64_t t = 0; t < nseg; t++) {
+            memcpy(iv_state + 16ull * segs[t].slot, h_state + 16 * t, 16);
+            pos_state[segs[t].slot] = hp[t];
+        }
+    }
+    e->host_path = "host_mapped";
+    if (hst.on)
+        fprintf(stderr, "[fpnn_aes host] mapped stream %s: %u frames, %llu streams, %.2f ms total, descriptors %.2f, "
+                "slot waits %.2f, final drain %.2f ms\n", encrypt ? "encrypt" : "decrypt", n,
+                (unsigned long long)nseg, 1e3 * (HostStats::now() - t_call), 1e3 * hst.gather, 1e3 * hst.wait,
+                1e3 * (HostStats::now() - td));
+    return rc;
+}
+
+// every frame of the call (source and destination) inside registered memory
+bool all_mapped(const fpnn_aes_engine *e, const fpnn_aes_host_frame *frames, uint32_t n, const MapView &v) {
+    std::atomic<bool> ok{true};
+    const unsigned parts = n >= 16384 ? pool_of(const_cast<fpnn_aes_engine *>(e))->parts() : 1u;
+    pool_of(const_cast<fpnn_aes_engine *>(e))->run(parts, [&](unsigned p) {
+        const uint32_t a0 = (uint32_t)((uint64_t)n * p / parts), b0 = (uint32_t)((uint64_t)n * (p + 1) / parts);
+        long rs = -1, rd = -1;
+        for (uint32_t q = a0; q < b0 && ok.load(std::memory_order_relaxed); q++) {
+            const fpnn_aes_host_frame &f = frames[q];
+            if (!f.len) continue;
+            const uintptr_t xs = (uintptr_t)f.src, xd = (uintptr_t)f.dst;
+            if ((rs < 0 || xs < v.lo[rs] || xs + f.len > v.hi[rs]) && (rs = v.find(f.src, f.len)) < 0) ok = false;
+            if ((rd < 0 || xd < v.lo[rd] || xd + f.len > v.hi[rd]) && (rd = v.find(f.dst, f.len)) < 0) ok = false;
+        }
+    });
+    return ok.load();
+}
+
 bool mapped_enabled() {
     const char *v = getenv("FPNN_AES_HOST_MAPPED");
     return !v || atoi(v) != 0;
@@ -1987,6 +2303,12 @@ int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_fr
     if (int rc = check_host_frames(e, frames, n, keys)) return rc;
     if (n && (!iv_state || !pos_state)) return FPNN_AES_ERR_ARG;
     if (!n) return FPNN_AES_OK;
+    if (mapped_enabled()) {  // every frame in registered host memory: the GPU moves the bytes
+        MapView v;
+        if (int rc = map_view(e->device, v)) return rc;
+        if (!v.lo.empty() && all_mapped(e, frames, n, v))
+            return mapped_stream_pipeline(e, encrypt != 0, frames, n, keys, v, iv_state, pos_state);
+    }
     return host_pipeline(e, encrypt != 0, true, frames, n, keys, 0, iv_state, pos_state);
 }
 

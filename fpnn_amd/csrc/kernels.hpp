@@ -64,6 +64,7 @@ struct Variant {
     int hybrid = 1;        // ragged batches that take the queue: K2h (lanes + quads) instead of K2q
     int hyb_long = 512;    // K2h: chains of at least this many blocks (bucket-rounded) go to quads
     int hyb_quad_waves = 8;  // K2h: waves per workgroup that start on the long chains
+    int hyb_wire_lanes = 0;  // K2h: wire-prefix batches also use the lane session (else all quads)
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
     int fence = 1;         // K2 / K1d (C2 shape), K1r, K2h: issue each round's 16 lookups before folding

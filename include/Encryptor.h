@@ -27,7 +27,8 @@
 
 namespace fpnn {
 
-class EncryptorBatch;  // EncryptorBatch.h: runs queued calls of many encryptors in one GPU pass
+class EncryptorBatch;       // EncryptorBatch.h: runs queued calls of many encryptors in one GPU pass
+class StreamReceiverBatch;  // StreamReceiverBatch.h: the stream receive side of many connections per pass
 
 /* libfpnn_aes.so: a process-unique number per constructed Encryptor -- the key of its
    slot in an EncryptorBatch's persistent device key table (an address can be reused by
@@ -44,6 +45,7 @@ public:
 
 class Encryptor {
     friend class EncryptorBatch;
+    friend class StreamReceiverBatch;
 
 protected:
     uint8_t _iv[16];
@@ -100,6 +102,7 @@ public:
  * (core/Encryptor.cpp:53-70). */
 class StreamEncryptor : public Encryptor {
     friend class EncryptorBatch;
+    friend class StreamReceiverBatch;
     rijndael_context _ctx;
     size_t _pos;
 

@@ -54,7 +54,13 @@ def test_cpp_encryptor_symbols_exported():
                 "fpnn::EncryptorBatch::flush()",
                 "fpnn::EncryptorBatch::encrypt(fpnn::Encryptor*, std::__cxx11::basic_string",
                 "fpnn::EncryptorBatch::encrypt(fpnn::Encryptor*, unsigned char*, unsigned char*, int)",
-                "fpnn::EncryptorBatch::decrypt(fpnn::Encryptor*, unsigned char*, unsigned char*, int)"):
+                "fpnn::EncryptorBatch::decrypt(fpnn::Encryptor*, unsigned char*, unsigned char*, int)",
+                "fpnn::encryptor_retire(unsigned long)",
+                "fpnn::StreamReceiverBatch::open(fpnn::StreamEncryptor*)",
+                "fpnn::StreamReceiverBatch::received(int, unsigned char const*, unsigned long)",
+                "fpnn::StreamReceiverBatch::flush()",
+                "fpnn::StreamReceiverBatch::messages[abi:cxx11](int) const",
+                "fpnn::StreamReceiverBatch::status(int) const"):
         assert sym in out, sym
 
 
@@ -145,6 +151,18 @@ def build_dropin(outdir) -> str:
                     os.path.join(ROOT, "tests", "cpp", "dropin.cpp"), "-o", exe, "-L", libdir, "-lfpnn_aes",
                     f"-Wl,-rpath,{libdir}"], check=True, capture_output=True, text=True)
     return exe
+
+
+def test_cpp_stream_receiver_compiles_against_headers(tmp_path):
+    """tests/cpp/stream_recv.cpp, the EncryptedStreamReceiver-shaped loop over
+    include/StreamReceiverBatch.h, builds with -std=c++11 -Wall -Werror and links."""
+    import fpnn_amd
+    exe = os.path.join(str(tmp_path), "stream_recv")
+    libdir = os.path.dirname(fpnn_amd.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "stream_recv.cpp"), "-o", exe, "-L", libdir, "-lfpnn_aes",
+                    f"-Wl,-rpath,{libdir}"], check=True, capture_output=True, text=True)
+    assert os.access(exe, os.X_OK)
 
 
 def test_cpp_dropin_compiles_against_headers(tmp_path):

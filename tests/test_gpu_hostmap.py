@@ -218,3 +218,87 @@ def test_staged_many_chunks(engine, oracle, ragged):
     fr2 = frames_array(dst.ctypes.data, offs, dst.ctypes.data, offs, lens, np.zeros(n, dtype=np.uint32))
     engine.package_host_array(False, fr2, ks)
     assert np.array_equal(dst, src)
+
+
+def _stream_expected(oracle, encrypt, keys, keylen, frames, src, dst0, iv_state, pos_state, src_base, dst_base):
+    """StreamEncryptor semantics per key slot, frames in array order (core/Encryptor.cpp:53-70)."""
+    exp = dst0.copy()
+    iv, pos = iv_state.copy(), pos_state.copy()
+    for f in frames:
+        s, n = int(f["key_slot"]), int(f["len"])
+        if not n:
+            continue
+        so, do = int(f["src"]) - src_base, int(f["dst"]) - dst_base
+        key = keys[keylen * s:keylen * (s + 1)].tobytes()
+        out, ivo, po = oracle.cfb(key, encrypt, src[so:so + n].tobytes(), iv[16 * s:16 * s + 16].tobytes(), int(pos[s]))
+        exp[do:do + n] = np.frombuffer(out, np.uint8)
+        iv[16 * s:16 * s + 16] = np.frombuffer(ivo, np.uint8)
+        pos[s] = po
+    return exp, iv, pos
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+@pytest.mark.parametrize("shape", ["many_streams", "split_streams"])
+def test_mapped_stream_frames(engine, oracle, arenas, keylen, shape):
+    """fpnn_aes_stream_host with every frame in registered memory: the GPU gathers and
+    scatters the frames itself (host_mapped), the streams' (iv, pos) carried across frames
+    and -- split_streams: four 16 MiB streams, more than one pipeline chunk each -- across
+    chunks.  Frames of a stream interleave with other streams' in the array and sit at
+    random places of the arenas; bytes between frames stay untouched."""
+    import fpnn_amd
+    rng = np.random.default_rng(4400 + keylen + (shape == "split_streams"))
+    if shape == "many_streams":
+        S, n = 300, 3000
+        lens = rng.integers(0, 5000, n).astype(np.uint32)
+        short = rng.random(n) < 0.1
+        lens[short] = rng.integers(0, 17, short.sum())
+    else:
+        S, n = 4, 64
+        lens = np.full(n, 1 << 20, dtype=np.uint32)
+        lens[::7] -= rng.integers(1, 1000, len(lens[::7])).astype(np.uint32)
+    slots = rng.integers(0, S, n).astype(np.uint32)
+    src_offs, src_size = place(rng, lens)
+    dst_offs, dst_size = place(rng, lens)
+    src = arenas(src_size, 0x11)
+    src[:] = rng.integers(0, 256, src_size, dtype=np.uint8)
+    dst = arenas(dst_size, 0x5A)
+    keys = rng.integers(0, 256, S * keylen, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), keylen, bytes(16 * S))
+    fr = frames_array(src.ctypes.data, src_offs, dst.ctypes.data, dst_offs, lens, slots)
+    for encrypt in (True, False):
+        iv0 = rng.integers(0, 256, 16 * S, dtype=np.uint8)
+        pos0 = rng.integers(0, 16, S).astype(np.uint32)
+        dst[:] = 0x5A
+        exp, iv_e, pos_e = _stream_expected(oracle, encrypt, keys, keylen, fr, src, dst.copy(), iv0, pos0,
+                                            src.ctypes.data, dst.ctypes.data)
+        iv, pos = iv0.copy(), pos0.copy()
+        engine.stream_host_array(encrypt, fr, ks, iv, pos)
+        assert engine.last_kernel(fpnn_amd.K_HOST) == "host_mapped"
+        bad = np.nonzero(dst != exp)[0]
+        assert len(bad) == 0, (encrypt, len(bad), bad[:8])
+        assert np.array_equal(iv, iv_e) and np.array_equal(pos, pos_e), encrypt
+
+
+def test_stream_frames_partly_mapped_go_staged(engine, oracle, arenas):
+    """One frame outside registered memory: the whole stream call takes the staged path
+    (stream frames depend on each other), with the same results."""
+    import fpnn_amd
+    rng = np.random.default_rng(4500)
+    S, n = 20, 200
+    lens = rng.integers(1, 3000, n).astype(np.uint32)
+    slots = rng.integers(0, S, n).astype(np.uint32)
+    src_offs, src_size = place(rng, lens)
+    dst_offs, dst_size = place(rng, lens)
+    src = arenas(src_size, 0x11)
+    src[:] = rng.integers(0, 256, src_size, dtype=np.uint8)
+    dst = aligned(dst_size, 0x5A)  # NOT registered
+    keys = rng.integers(0, 256, S * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), 16, bytes(16 * S))
+    fr = frames_array(src.ctypes.data, src_offs, dst.ctypes.data, dst_offs, lens, slots)
+    iv0, pos0 = rng.integers(0, 256, 16 * S, dtype=np.uint8), np.zeros(S, dtype=np.uint32)
+    exp, iv_e, pos_e = _stream_expected(oracle, True, keys, 16, fr, src, dst.copy(), iv0, pos0, src.ctypes.data,
+                                        dst.ctypes.data)
+    iv, pos = iv0.copy(), pos0.copy()
+    engine.stream_host_array(True, fr, ks, iv, pos)
+    assert engine.last_kernel(fpnn_amd.K_HOST) == "host_staged"
+    assert np.array_equal(dst, exp) and np.array_equal(iv, iv_e) and np.array_equal(pos, pos_e)

@@ -9,6 +9,7 @@ for DESIGN.md -- bench.py's single JSON line covers C2 only.
   C5  65536 keys x 4 KiB AES-256, per-key IV
   U1  1M x 1472 B UDP datagrams over 16384 connections, AES-128
   R1  the receive path: 16384 connections x 64 wire frames, fpnn_aes_package_recv (8f row 3)
+  S1  stream-mode host frames, 16384 streams x 64 x 1 KiB: staged vs registered (mapped) arenas
 """
 import argparse
 import json
@@ -433,6 +434,57 @@ def main():
         del a, wire, plain
         print(json.dumps({"R1": out["R1"]}), flush=True)
 
+    if "S1" in todo:
+        # Stream-mode host frames (StreamEncryptor per connection, core/Encryptor.cpp:53-70):
+        # 16384 streams x 64 frames of 1 KiB = 1 GiB, the array in arrival order (frame j of
+        # every stream before frame j + 1 of any), frames at shuffled places of host arenas.
+        # Staged (pageable, host gather/scatter) vs mapped (arenas registered, the GPU moves).
+        NS, F, L = 16384, 64, 1024
+        P = NS * F
+        rng = np.random.default_rng(5)
+        keys = rng.integers(0, 256, NS * 16, dtype=np.uint8)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), 16, bytes(16 * NS))
+        def page_aligned(nbytes):
+            raw = np.empty(nbytes + 4096, dtype=np.uint8)
+            return raw[(-raw.ctypes.data) % 4096:][:nbytes]
+        src, dst = page_aligned(P * L), page_aligned(P * L)
+        src[:] = rng.integers(0, 256, P * L, dtype=np.uint8)
+        perm = rng.permutation(P).astype(np.uint64)
+        fr = np.zeros(P, dtype=fpnn_amd.engine.HOST_FRAME_DTYPE)
+        fr["src"] = src.ctypes.data + perm * L
+        fr["dst"] = dst.ctypes.data + perm[::-1] * L
+        fr["len"] = L
+        fr["key_slot"] = np.arange(P) % NS
+        res = {}
+        for mode in ("staged", "mapped"):
+            if mode == "mapped":
+                fpnn_amd.host_register(src)
+                fpnn_amd.host_register(dst)
+            for enc in (True, False):
+                times = []
+                for _ in range(1 + args.reps):
+                    iv, pos = np.zeros(16 * NS, np.uint8), np.zeros(NS, np.uint32)
+                    t0 = time.perf_counter()
+                    eng.stream_host_array(enc, fr, ks, iv, pos)
+                    times.append(time.perf_counter() - t0)
+                import statistics
+                res[f"{mode}_{'encrypt' if enc else 'decrypt'}_GiBs"] = gib(P * L, statistics.median(times[1:]))
+                res[f"{mode}_path"] = eng.last_kernel(fpnn_amd.K_HOST)
+                if enc:
+                    got_enc = dst.copy() if mode == "staged" else None
+                    if mode == "mapped":
+                        assert np.array_equal(dst, ref_enc), "mapped stream host frames differ from staged"
+                    else:
+                        ref_enc = got_enc
+            if mode == "mapped":
+                fpnn_amd.host_unregister(src)
+                fpnn_amd.host_unregister(dst)
+        out["S1"] = dict(res, frames=P, streams=NS, frame_bytes=L,
+                         note="stream host frames: 16384 streams x 64 x 1 KiB in arrival order at shuffled arena "
+                              "places; staged = host gather/scatter + pinned DMA, mapped = arenas registered, the "
+                              "GPU gathers/scatters over PCIe; mapped encrypt output checked equal to the staged one")
+        del src, dst
+        print(json.dumps({"S1": out["S1"]}), flush=True)
     if "R1R" in todo:
         # R1 with realistic body lengths: CFB does not pad, so FPNN package bodies have any
         # length -- here uniform 1 .. 2047 bytes (mean ~1 KiB), 64 frames per connection

@@ -48,6 +48,31 @@ def gpu_rate(engine, curve: str, n: int, reps: int):
     return n / best, best * 1e3
 
 
+def gpu_percall(engine, curve: str, calls: int):
+    """The drop-in per-call form (ECCKeyExchange::calcKey through fpnn_ecdh_calc_key_host:
+    one peer, host buffers, synchronous): median microseconds per call."""
+    import statistics
+    import numpy as np
+    import torch
+    import fpnn_amd
+    cv = engine.ecdh_curve(curve)
+    pl = fpnn_amd.lib.fpnn_ecdh_private_len(cv)
+    rng = np.random.default_rng(77)
+    privs = torch.from_numpy(rng.integers(0, 256, (calls, pl), dtype=np.uint8)).to("cuda:0")
+    privs[:, 0] &= 0x7F
+    peers, _ = engine.ecdh_public_keys(curve, privs)
+    peers = peers.cpu().numpy()
+    server = bytes(rng.integers(1, 255, pl, dtype=np.uint8))
+    engine.ecdh_calc_key_host(curve, server, peers[0].tobytes(), 32)  # warm-up (scratch)
+    times = []
+    for i in range(calls):
+        p = peers[i].tobytes()
+        t0 = time.perf_counter()
+        engine.ecdh_calc_key_host(curve, server, p, 32)
+        times.append(time.perf_counter() - t0)
+    return statistics.median(times) * 1e6
+
+
 def cpu_rate(curve: str, procs: int, seconds: float):
     """calcKey/s of the reference, `procs` processes in parallel (one per core)."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "ecdh_cases.json")))
@@ -76,6 +101,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--curves", default="secp256k1,secp256r1,secp224r1,secp192r1")
     ap.add_argument("--no-cpu", action="store_true", help="skip the reference CPU legs (profiling runs)")
+    ap.add_argument("--percall", type=int, default=0, help="also time this many single-peer calcKey calls")
     args = ap.parse_args()
     import fpnn_amd
     eng = fpnn_amd.Engine(0)
@@ -90,11 +116,15 @@ def main():
     for curve in args.curves.split(","):
         g, ms = gpu_rate(eng, curve, args.n, args.reps)
         row = {"gpu_per_s": round(g), "gpu_ms_per_batch": round(ms, 3)}
+        if args.percall:
+            row["gpu_percall_us_median"] = round(gpu_percall(eng, curve, args.percall), 1)
         if os.path.exists(ECDH_REF) and not args.no_cpu:
             c1, _ = cpu_rate(curve, 1, args.cpu_seconds)
             cn, _ = cpu_rate(curve, cores, args.cpu_seconds)
             row.update({"reference_1core_per_s": round(c1), f"reference_{cores}cores_per_s": round(cn),
                         "gpu_over_reference_all_cores": round(g / cn, 1)})
+            if args.percall:
+                row["reference_percall_us"] = round(1e6 / c1, 1)
         out["curves"][curve] = row
         print(json.dumps({curve: row}), flush=True)
     print(json.dumps(out))

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_hybrid.py tests/test_gpu_ragged.py tests/test_gpu_parity.py -k "not slow" \
+  tests/test_gpu_hostmap.py tests/test_gpu_stream_receiver.py tests/test_gpu_hybrid.py tests/test_gpu_ragged.py tests/test_gpu_parity.py -k "not slow" \
   > gpurun_out/r03c_tests.log 2>&1; rc=$?; tail -2 gpurun_out/r03c_tests.log
 if [ $rc -ne 0 ]; then grep -E "^E |Error|FAILED" gpurun_out/r03c_tests.log | head -30; exit $rc; fi
 run() { local name=$1; shift; timeout -k 10 400 python tools/ab_encrypt.py "$@" > gpurun_out/r03c_$name.log 2>&1 || { tail -5 gpurun_out/r03c_$name.log; exit 1; }; grep '^{' gpurun_out/r03c_$name.log; }
