@@ -205,7 +205,7 @@ struct fpnn_aes_engine {
     uint64_t cap_perm = 0;
     uint32_t *d_next = nullptr;  // K2q work-queue counter (one word)
     uint64_t cap_next = 0;
-    uint32_t *d_buckets = nullptr;  // 2 x 128 counters
+    uint32_t *d_buckets = nullptr;  // 2 x 128 counters + the wire flag (kLengthOrderWords)
     uint64_t cap_buckets = 0;
     uint64_t *d_fr_off = nullptr;  // package receive: absolute body offset per frame slot
     uint64_t cap_fr_off = 0;
@@ -400,7 +400,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
         if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
             if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
-            if ((rc = grow(e, e->d_buckets, e->cap_buckets, 256))) return rc;
+            if ((rc = grow(e, e->d_buckets, e->cap_buckets, kLengthOrderWords))) return rc;
             if (stream) {  // bucket sizes read pos_state (the encrypt kernel reads it later)
                 k.pos_snap = pos_state;
             }
@@ -414,6 +414,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if (queue && (rc = grow(e, e->d_next, e->cap_next, 2))) return rc;
         if (queue && e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
         const bool hybrid = queue && e->variant.hybrid && b->count > 1;
+        if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
         if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
             HybridArgs h;
@@ -421,6 +422,8 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             h.buckets = e->d_buckets;
             h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
             h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
+            h.qflags = (uint32_t)e->variant.hyb_qflags;
+            h.sink = e->d_sink;
             if ((b->flags & FPNN_AES_F_WIRE_PREFIX) && !e->variant.hyb_wire_lanes) {
                 // wire frames (htole32(len) || C): every chain on quads -- the lane session's
                 // funnel-shifted, line-aligned steps measured 653 vs 800 GiB/s on R1
@@ -625,6 +628,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_HYB_QFLAGS")) e->variant.hyb_qflags = atoi(v);
     if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
     if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
@@ -1999,8 +2003,12 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         }
     }
     HIP_TRY(hipMemcpyAsync(d_state, h_state, nseg * 20, hipMemcpyHostToDevice, e->stream));
-    const uint64_t chunk = std::min<uint64_t>(256ull << 20, std::max<uint64_t>(kChunk, left / 4));
-    const uint64_t quota = std::max<uint64_t>(16u << 10, (chunk / nseg + 15) & ~15ull);
+    // Chunks of kChunk bytes (as the package path: the moves of chunk t overlap the cipher
+    // of chunk t - 1, so more, smaller chunks pipeline better than a few large ones), each
+    // taking a quota from as many streams as fit: the encrypt of a chunk is one serial CFB
+    // chain per stream, so its parallelism is the number of streams it spans.
+    const uint64_t chunk = kChunk;
+    const uint64_t quota = std::max<uint64_t>(1024, (chunk / nseg + 15) & ~15ull);
     // the move stream starts after work already queued on the engine stream
     HIP_TRY(hipEventRecord(e->ms[0].ciphered, e->stream));
     HIP_TRY(hipStreamWaitEvent(ms, e->ms[0].ciphered, 0));

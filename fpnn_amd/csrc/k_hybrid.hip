@@ -45,6 +45,14 @@ __device__ __forceinline__ uint4 sel4(bool c, const uint4 &x, const uint4 &y) {
     return make_uint4(c ? x.x : y.x, c ? x.y : y.y, c ? x.z : y.z, c ? x.w : y.w);
 }
 
+// Word q - k (mod 4) of x's quad for a quad-uniform runtime rotation k: the three
+// quad_perm rotations, then two levels of selects.
+__device__ __forceinline__ uint32_t quad_rot(uint32_t x, uint32_t k) {
+    const uint32_t r1 = quad_from<3>(x), r2 = quad_from<2>(x), r3 = quad_from<1>(x);
+    const uint32_t l0 = (k & 1u) ? r1 : x, l1 = (k & 1u) ? r3 : r2;
+    return (k & 2u) ? l1 : l0;
+}
+
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
@@ -55,7 +63,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of m
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-template <int NR, int KM, bool STREAM, int NT, int CH, bool SHIFT, bool FENCE>
+template <int NR, int KM, bool STREAM, int NT, int CH, bool SHIFT, bool FENCE, bool LANES = true>
 __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cfb_encrypt_hybrid(KBatch b, HybridArgs h) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -70,11 +78,24 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     const uint64_t n_long = __builtin_amdgcn_readfirstlane(wave_sum32(part));
     // quad tickets below static_q are dealt at start, the rest come from h.ctr[0]
     const uint64_t static_q = (uint64_t)h.quad_waves * 16u * gridDim.x;
+    // wire batches: every body starts on the 4-byte grid (flag set by the length ordering)
+    const bool wm = SHIFT && __builtin_amdgcn_readfirstlane(h.buckets[kWireFlagWord]) == 0u;
 
     RoundKeys<NR> rku;
     if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
 
     // ---------------- quad session: K2q's cipher over perm[0, n_long) ----------------
+    // Steps of 8 blocks; the next step's input words are loaded during this step's rounds.
+    // Where input and output share their offset inside a 128-byte line (C4), a short
+    // first step aligns the steps to the lines.  SHIFT (wire frames: the output sits 4
+    // bytes off the input): steps stay on the INPUT's lines -- aligning them to the output
+    // lines instead measured 412 vs 751 GiB/s on R1 -- and every 16-byte output slot is
+    // the funnel of two cipher blocks, built inside the quad (quad_rot + alignbyte), so
+    // stores are aligned dwords; the slots of a step past the output line boundary at
+    // position mq are held back (held[]) and stored with the next step's first mq slots,
+    // so each output line is written whole in one burst.  The chain's first slot is stored
+    // from byte lo0 on; its last held slots and the d bytes that end its last whole block
+    // are stored at the chain's end.
     auto quad_session = [&](bool first) {
         const int q = (int)(lane & 3u);
         const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
@@ -87,7 +108,25 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint8_t *p = nullptr;
         uint8_t *o = nullptr;
         uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
-        bool active = false, exhausted = false;
+        // SHIFT state: d = o & 15; the funnel's rotation kl, sources (fl, fh) and
+        // byte offset r; pl / ph = the rotated words of the previous raw block, praw its
+        // own word; pv / lo0 as in the lane session
+        uint32_t d = 0, kl = 0, r = 0, pl = 0, ph = 0, praw = 0, pv = 0, lo0 = 0;
+        bool fl = false, fh = false;
+        // hold-back: this lane's words j < jt of a step end an output line (jt = 8: no
+        // boundary in the step); held[j] (j >= jt) = words of the last step, hk its block
+        // count, hdst its base, hv = they are pending
+        uint32_t jt = 8, hk = 0, held[8];
+        uint8_t *hdst = nullptr;
+        bool hv = false;
+#pragma unroll
+        for (int j = 0; j < 8; j++) held[j] = 0u;
+        bool active = false, exhausted = false, fresh = false;
+        uint32_t a[8], nx[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = nx[j] = 0u;
+        const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 16 readable bytes
+        uint8_t *const sinkw = reinterpret_cast<uint8_t *>(h.sink + 2 * ((uint64_t)blockIdx.x * (kThreads / 64) + wave));
         auto begin = [&](uint64_t t) {
             const uint64_t s = b.perm[t];
             sid = s;
@@ -108,9 +147,13 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
             uint32_t rem = g.len;
+            uint32_t pw = 0;  // (SHIFT) this lane's word of the 16 bytes before the body
+            pv = 0;
             if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
                 if (q == 0) store_word_bytes(oo, rem, 0, 4);
                 oo += 4;
+                pw = q == 3 ? rem : 0u;
+                pv = 4;
             }
             if (STREAM && pos != 0 && rem != 0) {  // rest of the partially used keystream block
                 const uint32_t take = rem < 16 - pos ? rem : 16 - pos;
@@ -133,8 +176,42 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             nfull = rem >> 4;
             tail = rem & 15u;
             active = true;
+            fresh = true;
+            if (SHIFT && wm) {  // words stored where they fall (every body 4-byte aligned)
+                d = 0;
+                lo0 = 0;
+                const int bnd = (int)((128u - ((uint32_t)(uintptr_t)oo & 127u)) & 127u) - wlo;  // line end - word
+                jt = (h.qflags & 1u) || bnd + wlo == 0 ? 8u : bnd <= 0 ? 0u : (uint32_t)(bnd + 15) >> 4;
+                hv = false;
+            } else if (SHIFT) {
+                d = (uint32_t)(uintptr_t)oo & 15u;
+                const uint32_t e = (d + 3u) >> 2;  // slot word q starts in word q - e of its block
+                kl = e & 3u;
+                fl = (uint32_t)q < e;
+                fh = (uint32_t)q + 1u < e;
+                r = (0u - d) & 3u;
+                pl = quad_rot(pw, kl);
+                ph = quad_from<1>(pl);
+                praw = pw;
+                lo0 = d > pv ? d - pv : 0u;
+                const uint32_t m = (8u - (((uint32_t)((uintptr_t)(oo - d) >> 4)) & 7u)) & 7u;
+                jt = (h.qflags & 1u) || m == 0 ? 8u : m;
+                hv = false;
+            }
         };
-        auto finish = [&]() {  // partial final block and the stream state
+        auto finish = [&]() {  // the shifted remainder, the partial final block, the stream state
+            if (SHIFT) {
+                if (hv) {  // the held words of the last step
+#pragma unroll
+                    for (int j = 0; j < 8; j++)
+                        if (j >= (int)jt && j < (int)hk) *reinterpret_cast<uint32_t *>(hdst + 16 * j) = held[j];
+                    hv = false;
+                }
+                // bytes [16 - k, 16) of the last raw block end at o
+                const uint32_t k = d < pv ? d : pv;
+                const int lo = (int)(16u - k) - wlo;
+                if (k && lo < 4) store_word_bytes(o - 16 + wlo, praw, lo > 0 ? lo : 0, 4);
+            }
             if (tail) {
                 const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
                 const int hi = min((int)tail, wlo + 4) - wlo;
@@ -153,13 +230,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 if (q == 0) b.pos_state[sid] = n;
             }
         };
-        auto ticket = [&]() -> uint64_t {  // the quad leader's atomic, broadcast over the quad
-            uint32_t t = 0;
-            if (q == 0) t = atomicAdd(&h.ctr[0], 1u);
-            return (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x00, 0xf, 0xf, true) + static_q;
-        };
+        // Tickets: the wave's quads that need a chain take consecutive ones with one atomic,
+        // so neighbouring chains (adjacent frames of a send buffer) run side by side in one
+        // wave and the output line they share is written in the same step.  The first
+        // chains are dealt the same way, 16 per wave: wave w of workgroup g takes chains
+        // [16 (w * grid + g), +16) -- the longest 16 * grid (perm[] order) start at once,
+        // in the first wave of every workgroup.
         if (first) {
-            const uint64_t t0 = (uint64_t)(threadIdx.x >> 2) * gridDim.x + blockIdx.x;
+            const uint64_t qi = threadIdx.x >> 2;
+            const uint64_t t0 = ((qi >> 4) * gridDim.x + blockIdx.x) * 16u + (qi & 15u);
             if (t0 < n_long) begin(t0);
             else exhausted = true;
         }
@@ -169,29 +248,108 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 finish();
                 active = false;
             }
-            if (!active && !exhausted) {
-                const uint64_t t = ticket();
-                if (t < n_long) begin(t);
-                else exhausted = true;
+            const uint64_t need = __builtin_amdgcn_ballot_w64(q == 0 && !active && !exhausted);
+            if (need) {
+                const uint32_t leader = (uint32_t)__builtin_ctzll(need);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&h.ctr[0], (uint32_t)__builtin_popcountll(need));
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+                if (!active && !exhausted) {
+                    const uint64_t below = need & ((1ull << (lane & ~3u)) - 1ull);  // needing quads before mine
+                    const uint64_t t = (uint64_t)base + (uint64_t)__builtin_popcountll(below) + static_q;
+                    if (t < n_long) begin(t);
+                    else exhausted = true;
+                }
             }
             if (__builtin_amdgcn_ballot_w64(active) == 0) break;
             if (__builtin_amdgcn_ballot_w64(active && nfull != 0) == 0) continue;
-            const uint32_t kk = active ? (nfull < 8u ? nfull : 8u) : 0u;
-            uint32_t a[8];
+            // this step: 8 blocks, or up to the next line boundary where input and output
+            // share their line offset; the next step is loaded during this one's rounds
+            uint32_t lim = 8u;
+            if (!SHIFT && !(h.qflags & 1u)) {
+                const uint32_t xo = (uint32_t)(uintptr_t)o & 127u, xi = (uint32_t)(uintptr_t)p & 127u;
+                if (xo == xi && !(xo & 15u)) lim = 8u - (xo >> 4);
+            }
+            const uint32_t kk = active ? (nfull < lim ? nfull : lim) : 0u;
+            const uint32_t rest = active ? nfull - kk : 0u;
+            const uint32_t kk2 = (h.qflags & 2u) ? 0u : rest < 8u ? rest : 8u;
+            if (h.qflags & 2u) fresh = true;
+            // Memory ops of the steady state are unconditional (lanes with nothing to load
+            // read the key table, lanes with nothing to store write the wave's sink slot),
+            // so the waitcnt pass counts them exactly: the rounds wait only for this step's
+            // words (loaded one step earlier), never for the stores or the next prefetch.
+            if (__builtin_amdgcn_ballot_w64(fresh) != 0) {  // chains that start: their first words
 #pragma unroll
-            for (int j = 0; j < 8; j++) a[j] = j < (int)kk ? *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo) : 0u;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t c = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
-                iv = j < (int)kk ? c : iv;
-                a[j] = c;
+                for (int j = 0; j < 8; j++)
+                    if (fresh) a[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk ? p + 16 * j + wlo : dummy + wlo);
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), inside the rare branch
             }
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                if (j < (int)kk) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = a[j];
+                nx[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk2 ? p + 16 * (kk + j) + wlo : dummy + wlo);
+            // the rounds and the stores; FUN: the in-quad funnel (wire bodies off the 4-byte
+            // grid somewhere in the batch), else block words are output words
+            uint8_t *const dst = o - d + wlo;
+            const bool head = SHIFT && lo0 != 0 && kk != 0;  // the chain's first slot: from byte lo0 on
+            auto body = [&](auto fun_c) {
+                constexpr bool FUN = decltype(fun_c)::value;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t c = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                    const bool use = j < (int)kk;
+                    iv = use ? c : iv;
+                    if (FUN) {  // slot j = the last d bytes of block j - 1 ‖ the first 16 - d of block j
+                        // word q of the slot = bytes of block words q - e and q - e + 1
+                        // (cl, ch), from the previous block where those indices wrap (fl, fh)
+                        const uint32_t cl = quad_rot(c, kl), ch = quad_from<1>(cl);
+                        a[j] = __builtin_amdgcn_alignbyte(fh ? ph : ch, fl ? pl : cl, r);
+                        // (after a short step the chain ends: only praw is read again)
+                        pl = cl;
+                        ph = ch;
+                        praw = use ? c : praw;
+                    } else {
+                        a[j] = c;
+                    }
+                }
+                if (SHIFT) {
+                    // one output line: the last step's held words [jt, 8), then this step's
+                    // [0, jt) (4-aligned dwords); then this step's [jt, kk) are held
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const bool now = j < (int)jt;
+                        const bool st = now ? j < (int)kk && !(j == 0 && head) : hv && kk != 0;
+                        *reinterpret_cast<uint32_t *>(st ? (now ? dst : hdst) + 16 * j : sinkw + wlo) = now ? a[j] : held[j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++) held[j] = j >= (int)jt ? a[j] : held[j];
+                    if (kk) {
+                        hv = jt < 8u;
+                        hk = kk;
+                        hdst = dst;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++)
+                        *reinterpret_cast<uint32_u *>(j < (int)kk ? dst + 16 * j : sinkw + wlo) = a[j];
+                }
+            };
+            if (SHIFT && !wm) body(std::true_type{});
+            else body(std::false_type{});
+            if (SHIFT && __builtin_amdgcn_ballot_w64(head) != 0) {
+                const int lo = (int)lo0 - wlo;
+                if (head && lo < 4) store_word_bytes(dst, a[0], lo > 0 ? lo : 0, 4);
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), inside the rare branch
+            }
+            if (SHIFT && kk) {
+                lo0 = 0;
+                pv = 16;
+            }
             p += 16 * kk;
             o += 16 * kk;
             nfull -= kk;
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = nx[j];
+            fresh = false;
         }
         __builtin_amdgcn_s_setprio(0);
     };
@@ -368,6 +526,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         }
     };
 
+    if (!LANES) {  // every chain on quads (the host routes here with quad_waves = 16)
+        quad_session(true);
+        return;
+    }
     if (wave < h.quad_waves) quad_session(true);
     lane_session();
     // long chains left (fewer quad waves than the long queue needs): join them
@@ -376,19 +538,22 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 
 template <int NR, bool F>
 static void hybrid_nrf(const KBatch &b, const HybridArgs &h, KeyMode km, bool stream, int grid, hipStream_t st) {
-#define FPNN_HYB(K, STR, CH, SH) \
-    hipLaunchKernelGGL((k_cfb_encrypt_hybrid<NR, K, STR, 4, CH, SH, F || SH>), dim3(grid), dim3(kThreads), 0, st, b, h)
+#define FPNN_HYB(K, STR, CH, SH, LN) \
+    hipLaunchKernelGGL((k_cfb_encrypt_hybrid<NR, K, STR, 4, CH, SH, F || SH, LN>), dim3(grid), dim3(kThreads), 0, st, b, h)
     // the funnel-shifted whole-slot stores only where outputs sit off the block grid by
     // construction (the wire prefix); other ragged outputs are stored as they fall
     const bool shift = !stream && (b.flags & F_WIRE_PREFIX);
+    const bool quads = shift && h.quad_waves >= 16 && h.long_bucket >= 127;  // no lane session
     if (km == KEY_UNIFORM) {
-        if (stream) FPNN_HYB(KEY_UNIFORM, true, 8, false);
-        else if (shift) FPNN_HYB(KEY_UNIFORM, false, 8, true);
-        else FPNN_HYB(KEY_UNIFORM, false, 8, false);
+        if (stream) FPNN_HYB(KEY_UNIFORM, true, 8, false, true);
+        else if (quads) FPNN_HYB(KEY_UNIFORM, false, 8, true, false);
+        else if (shift) FPNN_HYB(KEY_UNIFORM, false, 8, true, true);
+        else FPNN_HYB(KEY_UNIFORM, false, 8, false, true);
     } else {  // per-lane round keys (up to 60 VGPRs): half-line steps
-        if (stream) FPNN_HYB(KEY_LANE, true, 4, false);
-        else if (shift) FPNN_HYB(KEY_LANE, false, 4, true);
-        else FPNN_HYB(KEY_LANE, false, 4, false);
+        if (stream) FPNN_HYB(KEY_LANE, true, 4, false, true);
+        else if (quads) FPNN_HYB(KEY_LANE, false, 4, true, false);
+        else if (shift) FPNN_HYB(KEY_LANE, false, 4, true, true);
+        else FPNN_HYB(KEY_LANE, false, 4, false, true);
     }
 #undef FPNN_HYB
 }

@@ -331,7 +331,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 uint4 e;
                 if (NR == 10) {
                     if (slotk != key_slot) {
-                        set_keys(rku, (ConstDevKeyR *)b.keys + slotk);
+                        // fenced rounds hold 16 lookups in flight: 12 key words then stay in SGPRs
+                        // (all in VGPRs spill to scratch, more in SGPRs spill SGPRs)
+                        set_keys<NR, FENCE ? 12 : 0>(rku, (ConstDevKeyR *)b.keys + slotk);
                         key_slot = slotk;
                     }
                     e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
@@ -429,7 +431,8 @@ static void ragged_nrf(const KBatch &b, KeyMode km, bool stream, const RaggedPla
 template <int NR>
 static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, bool fence,
                       int grid, hipStream_t st) {
-    if (fence) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
+    // fenced AES-192/256 per-slot passes run out of SGPRs for their round keys (spills)
+    if (fence && (NR == 10 || km == KEY_UNIFORM)) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
     else ragged_nrf<NR, false>(b, km, stream, plan, sink, grid, st);
 }
 

@@ -174,12 +174,20 @@ uint32_t length_bucket_of(uint64_t nblocks) {
 template <bool STREAM>
 __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts) {
     __shared__ uint32_t h[kBuckets];
+    __shared__ uint32_t off4;
     if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
+    if (threadIdx.x == 0) off4 = 0;
     __syncthreads();
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += (uint64_t)gridDim.x * blockDim.x)
+    const bool wire = !STREAM && (b.flags & F_WIRE_PREFIX);
+    uint32_t mis = 0;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += (uint64_t)gridDim.x * blockDim.x) {
         atomicAdd(&h[length_bucket<STREAM>(b, s)], 1u);
+        if (wire) mis |= (uint32_t)(uintptr_t)get_seg<LAYOUT_GENERAL>(b, s).out & 3u;  // K2h's funnel needed
+    }
+    if (mis) off4 = 1;
     __syncthreads();
     if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+    if (threadIdx.x == 0 && off4) atomicOr(&counts[kWireFlagWord], 1u);
 }
 
 __global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
@@ -218,7 +226,7 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *curs
 
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st) {
     uint32_t *cursor = counts + kBuckets;
-    hipError_t e = hipMemsetAsync(counts, 0, kBuckets * sizeof(uint32_t), st);
+    hipError_t e = hipMemsetAsync(counts, 0, kLengthOrderWords * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)((b.count + 255) / 256 < 1024 ? (b.count + 255) / 256 : 1024);
     if (stream)

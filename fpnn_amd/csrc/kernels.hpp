@@ -65,6 +65,7 @@ struct Variant {
     int hyb_long = 512;    // K2h: chains of at least this many blocks (bucket-rounded) go to quads
     int hyb_quad_waves = 8;  // K2h: waves per workgroup that start on the long chains
     int hyb_wire_lanes = 0;  // K2h: wire-prefix batches also use the lane session (else all quads)
+    int hyb_qflags = 0;      // K2h quad-session A/B flags (HybridArgs::qflags)
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
     int fence = 1;         // K2 / K1d (C2 shape), K1r, K2h: issue each round's 16 lookups before folding
@@ -117,11 +118,18 @@ hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool s
 // in length buckets <= long_bucket run on quads (K2c's cipher), the rest one per lane
 // (K2's); quad_waves waves per workgroup start on the long ones.  ctr: 2 device words
 // (zeroed here, on the stream); buckets: launch_length_order's counts.
+// launch_length_order's counts array: 128 bucket counts, 128 cursors, then (wire-prefix
+// batches) a flag word, nonzero when some frame starts off the 4-byte grid
+constexpr int kWireFlagWord = 256;
+constexpr int kLengthOrderWords = 257;
+
 struct HybridArgs {
     uint32_t *ctr;
-    const uint32_t *buckets;
+    const uint32_t *buckets;  // launch_length_order's counts (kLengthOrderWords)
     uint32_t long_bucket;
     uint32_t quad_waves;
+    uint4 *sink;      // 2 x uint4 per wave (grid * kThreads / 64 waves): stores with nothing to store
+    uint32_t qflags;  // A/B of the quad session: 1 = 8-block steps (not line-aligned), 2 = no prefetch
 };
 hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, bool fence,
                                  int grid, hipStream_t st);

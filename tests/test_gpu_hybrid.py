@@ -40,12 +40,15 @@ def _wire_expected(oracle, plain, dst0, n, in_off, out_off, lens, slots, keys, k
 
 @pytest.mark.parametrize("eng_kind", ENGINES)
 @pytest.mark.parametrize("keylen,nkeys", [(16, 1), (24, 5), (32, 1), (32, 200)])
-def test_wire_frames_every_offset(request, oracle, eng_kind, keylen, nkeys):
+@pytest.mark.parametrize("grid", [1, 4])
+def test_wire_frames_every_offset(request, oracle, eng_kind, keylen, nkeys, grid):
     """Ragged bodies (0..3000 B, incl. sub-block and block-multiple lengths) into wire
-    frames packed with 0..17-byte gaps, so frame starts take every offset mod 16."""
+    frames packed with 0..17-byte gaps, so frame starts take every offset mod 16
+    (grid 1: K2h's quads funnel-shift the blocks into 16-byte slots) or every multiple of 4
+    (grid 4: every body on the 4-byte grid, blocks stored as words where they fall)."""
     import fpnn_amd
     engine = request.getfixturevalue(eng_kind)
-    rng = np.random.default_rng(7000 + 10 * keylen + nkeys + len(eng_kind))
+    rng = np.random.default_rng(7000 + 10 * keylen + nkeys + len(eng_kind) + 100 * grid)
     n = 2500
     lens = rng.integers(0, 3001, n)
     special = np.array([0, 1, 4, 11, 12, 15, 16, 17, 28, 32, 124, 127, 128, 129, 1024, 1025])
@@ -53,7 +56,8 @@ def test_wire_frames_every_offset(request, oracle, eng_kind, keylen, nkeys):
     lens[pick] = rng.choice(special, pick.sum())
     in_off = np.concatenate([[0], np.cumsum(lens[:-1] + 5)]).astype(np.int64) + 3
     gaps = rng.integers(0, 18, n)
-    out_off = np.concatenate([[0], np.cumsum(lens[:-1] + 4 + gaps[:-1])]).astype(np.int64) + int(gaps[-1])
+    span = (lens + 4 + gaps + grid - 1) // grid * grid
+    out_off = np.concatenate([[0], np.cumsum(span[:-1])]).astype(np.int64) + int(gaps[-1]) // grid * grid
     plain = rng.integers(0, 256, int(in_off[-1] + lens[-1] + 32), dtype=np.uint8)
     dst0 = rng.integers(0, 256, int(out_off[-1] + lens[-1] + 4 + 64), dtype=np.uint8)
     keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
