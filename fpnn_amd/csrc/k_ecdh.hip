@@ -20,21 +20,24 @@ struct Fe {
     uint32_t v[NW];
 };
 
-// t[0..NW] (t < 2p) -> t mod p
+#include "ecc_chains.hpp"
+
+// Carry chains are written with clang's multiprecision builtins: each limb is one
+// v_add_co / v_addc (v_sub_co / v_subb) with the carry in vcc.  (The 64-bit form
+// `s = (uint64_t)a - b - borrow; borrow = s >> 63` costs 3-4 instructions per limb: 64-bit
+// shifts, register-pair moves.)
+__device__ __forceinline__ uint32_t addc(uint32_t x, uint32_t y, uint32_t &c) {
+    unsigned co;
+    const uint32_t r = __builtin_addc(x, y, c, &co);
+    c = co;
+    return r;
+}
+
+// t[0..NW] (t < 2p) -> t mod p (one borrow chain through top, one select; ecc_chains.hpp)
 template <int NW>
 __device__ __forceinline__ Fe<NW> reduce_once(const uint32_t *t, uint32_t top, const EccConst &c) {
-    Fe<NW> d;
-    uint32_t borrow = 0;
-#pragma unroll
-    for (int j = 0; j < NW; j++) {
-        const uint64_t s = (uint64_t)t[j] - c.p[j] - borrow;
-        d.v[j] = (uint32_t)s;
-        borrow = (uint32_t)(s >> 63);
-    }
-    const bool use_d = top != 0 || borrow == 0;
     Fe<NW> r;
-#pragma unroll
-    for (int j = 0; j < NW; j++) r.v[j] = use_d ? d.v[j] : t[j];
+    reduce_n<NW>(r.v, t, top, c.p);
     return r;
 }
 
@@ -69,31 +72,36 @@ __device__ __forceinline__ void mac_s(uint64_t &lo, uint32_t &hi, uint32_t x, ui
 // a special-prime reduction of the full 512-bit product (R = 1 on the host side).
 enum : int { FK_MONT = 0, FK_K1 = 1, FK_P256 = 2, FK_P224 = 3, FK_P192 = 4 };
 
-// t (512 bits) mod p: t = L + H*(2^32 + 977) folded twice, every column sum < 2^43,
-// then U + top*(2^32 + 977) < 2^256 + 2^67 < 2p and one conditional subtraction
+// t (512 bits) mod p: t = L + H*(2^32 + 977) as three carry chains over the limbs --
+// L + lo(H_i * 977), then + H << 32, then + hi(H_i * 977) << 32 -- leaving a top
+// u8 + u9 * 2^32 < 2^34; that folds once more the same way into one chain
+// (U + top * (2^32 + 977) < 2^256 + 2^67 < 2p, a carry-out of at most 1) and one
+// conditional subtraction.
 template <int NW>
 __device__ __forceinline__ Fe<NW> k1_fold(const uint32_t (&t)[16], const EccConst &c) {
-    uint32_t u[8];
-    uint64_t acc = 0;
+    uint32_t u[8], ml[8], mh[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        acc = (uint64_t)t[8 + i] * 977u + acc + t[i] + (i ? t[7 + i] : 0u);
-        u[i] = (uint32_t)acc;
-        acc >>= 32;
+        const uint64_t m = (uint64_t)t[8 + i] * 977u;
+        ml[i] = (uint32_t)m;
+        mh[i] = (uint32_t)(m >> 32);
     }
-    const uint64_t top = acc + t[15];  // < 2^34
-    uint64_t x = (uint64_t)u[0] + top * 977u;
-    u[0] = (uint32_t)x;
-    x = (x >> 32) + u[1] + top;
-    u[1] = (uint32_t)x;
-    x >>= 32;
+    const uint32_t c1 = add_n<8>(u, t, ml);
+    uint32_t x[8], w[8];
 #pragma unroll
-    for (int i = 2; i < 8; i++) {
-        x += u[i];
-        u[i] = (uint32_t)x;
-        x >>= 32;
-    }
-    return reduce_once<NW>(u, (uint32_t)x, c);
+    for (int i = 0; i < 8; i++) x[i] = i < 7 ? u[i + 1] : c1;
+    const uint32_t c2 = add_n<8>(w, x, t + 8);  // + H << 32: limbs 1..8
+    const uint32_t c3 = add_n<8>(x, w, mh);     // + hi(H * 977) << 32
+#pragma unroll
+    for (int i = 1; i < 8; i++) u[i] = x[i - 1];
+    const uint32_t u8 = x[7], u9 = c2 + c3;  // top = u8 + u9 * 2^32
+    const uint64_t a = (uint64_t)u8 * 977u;
+    const uint32_t a1 = (uint32_t)(a >> 32) + u9 * 977u;  // < 2^11
+    uint32_t k = 0;
+    const uint32_t s1 = addc(a1, u8, k);  // limb 1: hi(u8 * 977) + u9 * 977 + u8 (top << 32)
+    const uint32_t z[8] = {(uint32_t)a, s1, u9 + k, 0u, 0u, 0u, 0u, 0u};
+    const uint32_t cy = add_n<8>(u, u, z);
+    return reduce_once<NW>(u, cy, c);
 }
 
 // secp256r1 (p = 2^256 - 2^224 + 2^192 + 2^96 - 1): the NIST word-sum reduction (FIPS
@@ -150,51 +158,84 @@ __device__ __forceinline__ Fe<NW> p256_fold(const uint32_t (&t)[16], const EccCo
     return r;
 }
 
-// 2*NW-limb product of two NW-limb values, product scanning
+// column i of a product scan: partial products a[j] * b[i - j] for j in [col_first, col_last]
+// (a square's cross products: j < i - j only)
 template <int NW>
-__device__ __forceinline__ void prodN(const uint32_t *a, const uint32_t *b, uint32_t (&t)[2 * NW]) {
-    uint64_t lo = 0;
-    uint32_t hi = 0;
+__device__ constexpr int col_first(int i) { return i > NW - 1 ? i - (NW - 1) : 0; }
+template <int NW, bool SQ>
+__device__ constexpr int col_last(int i) { return SQ ? (i + 1) / 2 - 1 : (i < NW - 1 ? i : NW - 1); }
+
+// Product scanning: one 96-bit column accumulator (lo 64 + hi 32); each column's partial
+// products are one asm block (mac_col, ecc_chains.hpp: hi from the carries alone), the carried
+// value of the next column is (lo >> 32 | hi << 32).  SQ: the square's cross products only
+// (finished by sqr_finish).  Columns by template recursion: a column's length is a template
+// argument of mac_col.
+template <int NW, bool SQ, int I>
+__device__ __forceinline__ void scan_col(const uint32_t *a, const uint32_t *b, uint32_t (&t)[2 * NW], uint64_t &lo) {
+    if constexpr (I < 2 * NW - 1) {
+        constexpr int f = col_first<NW>(I), n = col_last<NW, SQ>(I) - f + 1;
+        uint32_t hi = 0;
+        if constexpr (n > 0) {
+            uint32_t x[n], y[n];
 #pragma unroll
-    for (int i = 0; i < 2 * NW - 1; i++) {
-#pragma unroll
-        for (int j = (i > NW - 1 ? i - (NW - 1) : 0); j <= (i < NW - 1 ? i : NW - 1); j++) mac(lo, hi, a[j], b[i - j]);
-        t[i] = (uint32_t)lo;
+            for (int k = 0; k < n; k++) {
+                x[k] = a[f + k];
+                y[k] = b[I - f - k];
+            }
+            mac_col<n>(lo, hi, x, y);
+        }
+        t[I] = (uint32_t)lo;
         lo = (lo >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
+        scan_col<NW, SQ, I + 1>(a, b, t, lo);
     }
+}
+
+template <int NW, bool SQ>
+__device__ __forceinline__ void prod_scan(const uint32_t *a, const uint32_t *b, uint32_t (&t)[2 * NW]) {
+    uint64_t lo = 0;
+    scan_col<NW, SQ, 0>(a, b, t, lo);
     t[2 * NW - 1] = (uint32_t)lo;
 }
 
-// a^2: the NW(NW-1)/2 cross products once (product scanning), doubled by a one-bit shift
-// of the 2*NW-limb sum, plus the NW squares (36 partial products instead of 64 at NW = 8)
+// 2*NW-limb product of two NW-limb values
 template <int NW>
-__device__ __forceinline__ void sqrN(const uint32_t *a, uint32_t (&t)[2 * NW]) {
-    uint64_t lo = 0;
-    uint32_t hi = 0;
-    t[0] = 0;
-#pragma unroll
-    for (int i = 1; i < 2 * NW - 1; i++) {
-#pragma unroll
-        for (int j = (i > NW - 1 ? i - (NW - 1) : 0); 2 * j < i; j++) mac(lo, hi, a[j], a[i - j]);
-        t[i] = (uint32_t)lo;
-        lo = (lo >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
-    }
-    t[2 * NW - 1] = (uint32_t)lo;
-#pragma unroll
-    for (int i = 2 * NW - 1; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
-    t[0] = 0;  // (the cross sum has no limb-0 term)
-    uint32_t cin = 0;
+__device__ __forceinline__ void prodN(const uint32_t *a, const uint32_t *b, uint32_t (&t)[2 * NW]) {
+    prod_scan<NW, false>(a, b, t);
+}
+
+// the square's second half: the cross-product sum t doubled by a one-bit shift, plus the
+// NW squares a_i^2 on the diagonal in one carry chain (the total a^2 < 2^(64 NW): no carry out)
+template <int NW>
+__device__ __forceinline__ void sqr_finish(const uint32_t *a, uint32_t (&t)[2 * NW]) {
+    uint32_t d[2 * NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) {
-        uint64_t w = (((uint64_t)t[2 * i + 1] << 32) | t[2 * i]) + cin;
-        uint32_t h = w < cin;
-        mac(w, h, a[i], a[i]);
-        t[2 * i] = (uint32_t)w;
-        t[2 * i + 1] = (uint32_t)(w >> 32);
-        cin = h;
+        const uint64_t q = (uint64_t)a[i] * a[i];
+        d[2 * i] = (uint32_t)q;
+        d[2 * i + 1] = (uint32_t)(q >> 32);
     }
+#pragma unroll
+    for (int i = 2 * NW - 1; i > 0; i--) t[i] = __builtin_amdgcn_alignbit(t[i], t[i - 1], 31);
+    t[0] = 0;  // (the cross sum has no limb-0 term)
+    add_n<2 * NW>(t, t, d);
+}
+
+// a^2: the NW(NW-1)/2 cross products once, doubled, plus the NW squares (36 partial
+// products instead of 64 at NW = 8)
+template <int NW>
+__device__ __forceinline__ void sqrN(const uint32_t *a, uint32_t (&t)[2 * NW]) {
+    prod_scan<NW, true>(a, a, t);
+    sqr_finish<NW>(a, t);
+}
+
+// Two independent 2*NW-limb products (SQ: a square's cross-product half).  The ladder's
+// field products come in independent pairs (xycz_add / xycz_addc below); the two scans are
+// independent instruction streams the scheduler may interleave.
+template <int NW, bool SQ1, bool SQ2>
+__device__ __forceinline__ void prod_dual(const uint32_t *a1, const uint32_t *b1, uint32_t (&t1)[2 * NW],
+                                          const uint32_t *a2, const uint32_t *b2, uint32_t (&t2)[2 * NW]) {
+    prod_scan<NW, SQ1>(a1, b1, t1);
+    prod_scan<NW, SQ2>(a2, b2, t2);
 }
 
 // secp192r1 (p = 2^192 - 2^64 - 1): t = L + H*(2^64 + 1), all terms positive; the top
@@ -334,37 +375,38 @@ __device__ __forceinline__ Fe<NW> fsqr(const Fe<NW> &a, const EccConst &c) {
     }
 }
 
+// r1 = a1 * b1 (a1^2 if SQ1), r2 = a2 * b2 (a2^2 if SQ2) -- two independent field products
+// computed together (prod_dual); every operand is read before either result is written, so
+// r1 / r2 may alias any input.  The Montgomery form (the A/B baseline) runs them one by one.
+template <int NW, int FK, bool SQ1, bool SQ2>
+__device__ __forceinline__ void fdual(Fe<NW> &r1, const Fe<NW> &a1, const Fe<NW> &b1, Fe<NW> &r2, const Fe<NW> &a2,
+                                      const Fe<NW> &b2, const EccConst &c) {
+    if constexpr (FK != FK_MONT) {
+        uint32_t t1[2 * NW], t2[2 * NW];
+        prod_dual<NW, SQ1, SQ2>(a1.v, SQ1 ? a1.v : b1.v, t1, a2.v, SQ2 ? a2.v : b2.v, t2);
+        if (SQ1) sqr_finish<NW>(a1.v, t1);
+        if (SQ2) sqr_finish<NW>(a2.v, t2);
+        r1 = fold_nf<NW, FK>(t1, c);
+        r2 = fold_nf<NW, FK>(t2, c);
+    } else {
+        const Fe<NW> x = SQ1 ? fsqr<NW, FK>(a1, c) : fmul<NW, FK>(a1, b1, c);
+        const Fe<NW> y = SQ2 ? fsqr<NW, FK>(a2, c) : fmul<NW, FK>(a2, b2, c);
+        r1 = x;
+        r2 = y;
+    }
+}
+
 template <int NW>
 __device__ __forceinline__ Fe<NW> fadd(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
     uint32_t t[NW];
-    uint32_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < NW; j++) {
-        const uint64_t s = (uint64_t)a.v[j] + b.v[j] + carry;
-        t[j] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
+    const uint32_t carry = add_n<NW>(t, a.v, b.v);
     return reduce_once<NW>(t, carry, c);
 }
 
 template <int NW>
 __device__ __forceinline__ Fe<NW> fsub(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
-    Fe<NW> d, r;
-    uint32_t borrow = 0;
-#pragma unroll
-    for (int j = 0; j < NW; j++) {
-        const uint64_t s = (uint64_t)a.v[j] - b.v[j] - borrow;
-        d.v[j] = (uint32_t)s;
-        borrow = (uint32_t)(s >> 63);
-    }
-    const uint32_t mask = 0u - borrow;  // a < b: add p back
-    uint32_t carry = 0;
-#pragma unroll
-    for (int j = 0; j < NW; j++) {
-        const uint64_t s = (uint64_t)d.v[j] + (c.p[j] & mask) + carry;
-        r.v[j] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
+    Fe<NW> r;
+    fsub_n<NW>(r.v, a.v, b.v, c.p);  // a - b, plus p where that borrowed
     return r;
 }
 
@@ -375,15 +417,11 @@ __device__ __forceinline__ Fe<NW> fhalf(const Fe<NW> &a, const EccConst &c) {
     uint32_t t[NW];
     uint32_t carry = 0;
 #pragma unroll
-    for (int j = 0; j < NW; j++) {
-        const uint64_t s = (uint64_t)a.v[j] + (c.p[j] & mask) + carry;
-        t[j] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
+    for (int j = 0; j < NW; j++) t[j] = addc(a.v[j], c.p[j] & mask, carry);
     Fe<NW> r;
 #pragma unroll
-    for (int j = 0; j < NW - 1; j++) r.v[j] = (t[j] >> 1) | (t[j + 1] << 31);
-    r.v[NW - 1] = (t[NW - 1] >> 1) | (carry << 31);
+    for (int j = 0; j < NW - 1; j++) r.v[j] = __builtin_amdgcn_alignbit(t[j + 1], t[j], 1);
+    r.v[NW - 1] = __builtin_amdgcn_alignbit(carry, t[NW - 1], 1);
     return r;
 }
 
@@ -533,46 +571,44 @@ __device__ __forceinline__ void apply_z(Fe<NW> &X, Fe<NW> &Y, const Fe<NW> &Z, c
 
 // XYcZ_add (uECC.c:788-813): (P, Q) co-Z -> P into P', Q into P + Q
 template <int NW, int FK>
+// The same operation sequence, its six field products taken in three independent pairs
+// (fdual): (X2 - X1)^2 with (Y2 - Y1)^2, X1 * t5 with X2 * t5, Y1 * (X2 - X1) with
+// Y2 * (X1 - t5).
 __device__ __forceinline__ void xycz_add(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
-    Fe<NW> t5 = fsub<NW>(X2, X1, c);
-    t5 = fsqr<NW, FK>(t5, c);
-    X1 = fmul<NW, FK>(X1, t5, c);
-    X2 = fmul<NW, FK>(X2, t5, c);
+    Fe<NW> t5 = fsub<NW>(X2, X1, c), s2;
     Y2 = fsub<NW>(Y2, Y1, c);
-    t5 = fsqr<NW, FK>(Y2, c);
-    t5 = fsub<NW>(t5, X1, c);
+    fdual<NW, FK, true, true>(t5, t5, t5, s2, Y2, Y2, c);  // t5 = (X2 - X1)^2, s2 = Y2^2
+    fdual<NW, FK, false, false>(X1, X1, t5, X2, X2, t5, c);
+    t5 = fsub<NW>(s2, X1, c);
     t5 = fsub<NW>(t5, X2, c);
     X2 = fsub<NW>(X2, X1, c);
-    Y1 = fmul<NW, FK>(Y1, X2, c);
-    X2 = fsub<NW>(X1, t5, c);
-    Y2 = fmul<NW, FK>(Y2, X2, c);
+    const Fe<NW> x2b = fsub<NW>(X1, t5, c);
+    fdual<NW, FK, false, false>(Y1, Y1, X2, Y2, Y2, x2b, c);
     Y2 = fsub<NW>(Y2, Y1, c);
     X2 = t5;
 }
 
 // XYcZ_addC (uECC.c:819-854): (P, Q) co-Z -> P into P - Q, Q into P + Q
 template <int NW, int FK>
+// Its eight field products in four independent pairs: (X2 - X1)^2 with (Y2 - Y1)^2,
+// X1 * t5 with X2 * t5, Y1 * (X2 - X1) with (Y2 + Y1)^2, Y2 * t7 with t6 * (Y2 + Y1).
 __device__ __forceinline__ void xycz_addc(Fe<NW> &X1, Fe<NW> &Y1, Fe<NW> &X2, Fe<NW> &Y2, const EccConst &c) {
-    Fe<NW> t5 = fsub<NW>(X2, X1, c);
-    t5 = fsqr<NW, FK>(t5, c);
-    X1 = fmul<NW, FK>(X1, t5, c);
-    X2 = fmul<NW, FK>(X2, t5, c);
-    t5 = fadd<NW>(Y2, Y1, c);
+    Fe<NW> t5 = fsub<NW>(X2, X1, c), sy, t7s;
+    const Fe<NW> yp = fadd<NW>(Y2, Y1, c);  // uECC's t5 = Y2 + Y1
     Y2 = fsub<NW>(Y2, Y1, c);
+    fdual<NW, FK, true, true>(t5, t5, t5, sy, Y2, Y2, c);  // t5 = (X2 - X1)^2, sy = Y2^2
+    fdual<NW, FK, false, false>(X1, X1, t5, X2, X2, t5, c);
     Fe<NW> t6 = fsub<NW>(X2, X1, c);
-    Y1 = fmul<NW, FK>(Y1, t6, c);
+    fdual<NW, FK, false, true>(Y1, Y1, t6, t7s, yp, yp, c);  // Y1 *= X2 - X1, t7s = (Y2 + Y1)^2
     t6 = fadd<NW>(X1, X2, c);
-    X2 = fsqr<NW, FK>(Y2, c);
-    X2 = fsub<NW>(X2, t6, c);
-    Fe<NW> t7 = fsub<NW>(X1, X2, c);
-    Y2 = fmul<NW, FK>(Y2, t7, c);
+    X2 = fsub<NW>(sy, t6, c);
+    const Fe<NW> t7 = fsub<NW>(X1, X2, c);
+    const Fe<NW> t7b = fsub<NW>(t7s, t6, c);
+    t6 = fsub<NW>(t7b, X1, c);
+    fdual<NW, FK, false, false>(Y2, Y2, t7, t6, t6, yp, c);
     Y2 = fsub<NW>(Y2, Y1, c);
-    t7 = fsqr<NW, FK>(t5, c);
-    t7 = fsub<NW>(t7, t6, c);
-    t6 = fsub<NW>(t7, X1, c);
-    t6 = fmul<NW, FK>(t6, t5, c);
     Y1 = fsub<NW>(t6, Y1, c);
-    X1 = t7;
+    X1 = t7b;
 }
 
 template <int NW>
@@ -590,7 +626,7 @@ __device__ __forceinline__ void cswap(bool s, Fe<NW> &a, Fe<NW> &b) {
 // step; `sw` records whether they currently hold (R0, R1) so that swaps happen only
 // when consecutive bits differ.
 template <int NW, bool AM3, int FK>
-__device__ void ladder(Fe<NW> &rx, Fe<NW> &ry, const Fe<NW> &xp, const Fe<NW> &yp, const uint32_t *s, int nbits,
+__device__ __forceinline__ void ladder(Fe<NW> &rx, Fe<NW> &ry, const Fe<NW> &xp, const Fe<NW> &yp, const uint32_t *s, int nbits,
                        const EccConst &c) {
     Fe<NW> ax = xp, ay = yp;  // R1
     Fe<NW> bx = xp, by = yp;  // R0

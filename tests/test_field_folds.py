@@ -38,22 +38,40 @@ def settle(u, cr, p, nw):
     return U
 
 
-def k1_fold(t):  # k_ecdh.hip k1_fold
+def k1_fold(t):  # k_ecdh.hip k1_fold: three carry chains, a top fold, one subtraction
     p = P["secp256k1"]
-    u, acc = [0] * 8, 0
+
+    def addc(x, y, c):
+        s = x + y + c
+        assert 0 <= x < M and 0 <= y < M and c in (0, 1)
+        return s & (M - 1), s >> 32
+
+    ml = [(t[8 + i] * 977) & (M - 1) for i in range(8)]
+    mh = [(t[8 + i] * 977) >> 32 for i in range(8)]
+    u, c1 = [0] * 8, 0
     for i in range(8):
-        acc = t[8 + i] * 977 + acc + t[i] + (t[7 + i] if i else 0)
-        assert acc < 1 << 64
-        u[i], acc = acc & (M - 1), acc >> 32
-    top = acc + t[15]
-    assert top < 1 << 34
-    x = u[0] + top * 977
-    u[0], x = x & (M - 1), (x >> 32) + u[1] + top
-    u[1], x = x & (M - 1), x >> 32
-    for i in range(2, 8):
-        x += u[i]
-        u[i], x = x & (M - 1), x >> 32
-    v = value(u) + (x << 256)
+        u[i], c1 = addc(t[i], ml[i], c1)
+    c2 = 0
+    for i in range(1, 8):
+        u[i], c2 = addc(u[i], t[7 + i], c2)
+    u8, c2 = addc(c1, t[15], c2)
+    c3 = 0
+    for i in range(1, 8):
+        u[i], c3 = addc(u[i], mh[i - 1], c3)
+    u8, c3 = addc(u8, mh[7], c3)
+    u9 = c2 + c3
+    assert value(u) + ((u8 + (u9 << 32)) << 256) == value(t[:8]) + value(t[8:]) * ((1 << 32) + 977)
+    a = u8 * 977
+    a1 = (a >> 32) + u9 * 977
+    assert a1 < 1 << 11
+    s1, k = addc(a1, u8, 0)
+    cy = 0
+    u[0], cy = addc(u[0], a & (M - 1), cy)
+    u[1], cy = addc(u[1], s1, cy)
+    u[2], cy = addc(u[2], u9 + k, cy)
+    for i in range(3, 8):
+        u[i], cy = addc(u[i], 0, cy)
+    v = value(u) + (cy << 256)
     assert v < 2 * p
     return v - p if v >= p else v
 
