@@ -1141,6 +1141,9 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     memcpy(h_iv, ivec, 16);
     *h_pos = (uint32_t)*p_num;
     memcpy(e->h_stage + hdr, in, len);
+    // (Letting the kernels read and write the pinned staging block directly instead of the
+    // three copies measured the same per-call time, 71 / 32 us: the launches and the sync
+    // are the cost, not the copies.)
     HIP_TRY(hipMemcpyAsync(e->d_stage, e->h_stage, hdr + len, hipMemcpyHostToDevice, e->stream));
 
     fpnn_aes_keyset ks;
@@ -1692,6 +1695,13 @@ int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
 // written by the host threads during step t), so the move stream never waits for a copy.
 // Events hand each chunk between the two streams.  The host threads only write
 // descriptors.
+// FPNN_AES_MAP_PREP_FIRST=1: the mapped pipelines prepare chunk t + 1's descriptors before
+// queueing the cipher of chunk t - 1 (the round-2 order; A/B only)
+bool map_prep_first() {
+    const char *v = getenv("FPNN_AES_MAP_PREP_FIRST");
+    return v && atoi(v) != 0;
+}
+
 int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                     const fpnn_aes_keyset *keys, uint32_t flags, const MapView &v, uint32_t *done) {
     const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
@@ -1709,6 +1719,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
         if (int rc = mslot_reserve(m, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
+    const bool prep_first = map_prep_first();
     // the move stream starts after work already queued on the engine stream
     HIP_TRY(hipEventRecord(e->ms[0].ciphered, e->stream));
     HIP_TRY(hipStreamWaitEvent(ms, e->ms[0].ciphered, 0));
@@ -1890,11 +1901,15 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
         }
         HIP_TRY(launch_move_segments(gj, sj, ms));
         if (gather_t) HIP_TRY(hipEventRecord(e->ms[kt].gathered, ms));
-        // host: chunk t + 1's descriptors while the GPU moves
-        const bool next = prepare(t + 1, rc);
-        if (rc) break;
         // engine stream: cipher t - 1, then upload chunk t + 1 (its slot's previous chunk,
-        // t - 3, was scattered by step t - 1's launch, which the cipher waited for)
+        // t - 3, was scattered by step t - 1's launch, which the cipher waited for); the
+        // cipher is queued before the host prepares chunk t + 1's descriptors
+        bool next = false, prepared = false;
+        if (prep_first) {
+            next = prepare(t + 1, rc);
+            if (rc) break;
+            prepared = true;
+        }
         if (cipher_t1) {
             const Chunk &c = ch[k1];
             MapSlot &m = e->ms[k1];
@@ -1921,6 +1936,9 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
             if (rc) break;
             HIP_TRY(hipEventRecord(m.ciphered, e->stream));
         }
+        // host: chunk t + 1's descriptors while the GPU moves and ciphers
+        if (!prepared) next = prepare(t + 1, rc);
+        if (rc) break;
         // (chunk t + 1 exists only if chunk t - 1 does, for t >= 1: the upload always
         // follows a cipher; at t = 0 the slot is unused)
         if (next && (rc = upload(t + 1))) break;
@@ -1958,6 +1976,9 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     }();
     constexpr int kSlots = (int)(sizeof(e->ms) / sizeof(e->ms[0]));
     // ---- streams in array order (stable counting sort by slot, as host_pipeline) ----
+    // (Round 3 measured a parallel sort plus parallel piece building -- per-range
+    // histograms, two pool passes per chunk -- at 22-25 GiB/s against this serial form's
+    // 27-29 on the same box: tools/gpu_r03t.sh.)
     std::vector<uint32_t> order(n);
     {
         std::vector<uint32_t> cnt((size_t)keys->count + 1, 0);
@@ -1987,6 +2008,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         if (int rc = mslot_reserve(m, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
+    const bool prep_first = map_prep_first();
     // ---- the streams' (iv, pos), compact, on the device (engine stream) ----
     if (int rc = sstate_reserve(e, nseg * 20)) return rc;
     uint8_t *h_state = e->h_sstate, *d_state = e->d_sstate;
@@ -2166,8 +2188,14 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         }
         HIP_TRY(launch_move_segments(gj, sj, ms));
         if (gather_t) HIP_TRY(hipEventRecord(e->ms[kt].gathered, ms));
-        const bool more = prepare(t + 1, rc);
-        if (rc) break;
+        // the cipher of chunk t - 1 is queued before the host prepares chunk t + 1 (the
+        // engine stream is not left empty while the host works)
+        bool more = false, prepared = false;
+        if (prep_first) {
+            more = prepare(t + 1, rc);
+            if (rc) break;
+            prepared = true;
+        }
         if (cipher_t1) {
             const Chunk &c = ch[k1];
             MapSlot &m = e->ms[k1];
@@ -2190,6 +2218,8 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             if (rc) break;
             HIP_TRY(hipEventRecord(m.ciphered, e->stream));
         }
+        if (!prepared) more = prepare(t + 1, rc);
+        if (rc) break;
         if (more && (rc = upload(t + 1))) break;
         if (scatter_t2) ch[k2].np = 0;
     }

@@ -26,26 +26,30 @@ import torch  # noqa: E402
 import workloads as W  # noqa: E402
 
 
-def timed(eng, which, fn, reps):
-    """Median over `reps` individually timed calls, after two warm-up calls (clocks ramp;
-    the first calls grow scratch buffers): (wall s per call, kernel s per launch of the
-    main kernel `which`, launches per call)."""
+def timed(eng, which, fn, reps, rounds=3):
+    """Steady state, as bench.py: after two warm-up calls (clocks ramp; the first calls grow
+    scratch buffers), `rounds` rounds of `reps` calls issued back to back (no host sync
+    between them -- an idle gap lets the clock drop, which individually timed calls of a
+    ~1 ms kernel measure instead of the kernel).  Returns the medians over rounds of (wall s
+    per call, kernel s per launch of the main kernel `which` from HIP events on the engine
+    stream) and the launches per call."""
     import statistics
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
     walls, kern, launches = [], [], 0
-    for _ in range(max(1, reps)):
+    for _ in range(max(1, rounds)):
         eng.reset_stats()
         eng.set_timing(True)
         t0 = time.perf_counter()
-        fn()
+        for _ in range(max(1, reps)):
+            fn()
         torch.cuda.synchronize()
-        walls.append(time.perf_counter() - t0)
+        walls.append((time.perf_counter() - t0) / max(1, reps))
         eng.set_timing(False)
         n, ms = eng.kernel_stats(which)
         kern.append(ms / max(1, n) / 1e3)
-        launches = n
+        launches = n // max(1, reps)
     return statistics.median(walls), statistics.median(kern), launches
 
 
@@ -55,7 +59,7 @@ def gib(nbytes, sec):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=5, help="timed calls per measurement (the median is reported)")
+    ap.add_argument("--reps", type=int, default=5, help="calls per timed round (3 rounds; the median round is reported)")
     ap.add_argument("--configs", default="C2,C3,C4,C5,U1,R1")
     ap.add_argument("--no-host", action="store_true", help="skip the host-memory / PCIe legs (profiling runs)")
     args = ap.parse_args()
@@ -568,8 +572,9 @@ def main():
         del plain, wire, out_buf
         print(json.dumps({"R2": out["R2"]}), flush=True)
 
-    print(json.dumps({"configs": out, "timing": f"median of {args.reps} individually timed calls after 2 warm-up calls; "
-                                                  "kernel = HIP events around the main kernel on the engine stream"}))
+    print(json.dumps({"configs": out, "timing": f"median of 3 rounds of {args.reps} back-to-back calls after 2 warm-up calls "
+                                                  "(steady state, as bench.py); kernel = HIP events around the main "
+                                                  "kernel on the engine stream, per launch"}))
 
 
 if __name__ == "__main__":
