@@ -1045,6 +1045,26 @@ void devkey_from_schedule(DevKey *hk, const fpnn_aes_schedule *ctx) {
 
 bool valid_rounds(int nr) { return nr == 10 || nr == 12 || nr == 14; }
 
+// Synchronous per-call forms (the drop-in Encryptor / rijndael.h / calcKey calls) wait for
+// the engine stream with the blocking hipStreamSynchronize.  FPNN_AES_SYNC_SPIN=1 polls
+// hipStreamQuery for up to 2 ms first: measured slower (1 KiB per-call decrypt 43-50 vs
+// 32-33 us, encrypt 79 vs 73 us; tools/gpu_r03v.sh), so it is an A/B switch only.
+hipError_t sync_spin(hipStream_t st) {
+    static const bool on = [] {
+        const char *v = getenv("FPNN_AES_SYNC_SPIN");
+        return v && atoi(v) != 0;
+    }();
+    if (on) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+    }
+    return hipStreamSynchronize(st);
+}
+
 // One synchronous rijndael.h call in the non-CFB modes (k_modes.hip).  Staging:
 // [DevKey 272][iv 16][pos 4 | pad 12][in: in_bytes, 16-padded][out: out_bytes]
 int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const uint8_t *in, uint64_t in_copy,
@@ -1077,7 +1097,7 @@ int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const
     e->last_kernel[FPNN_AES_K_ENCRYPT] = last_launched();
     HIP_TRY(hipMemcpyAsync(h_iv, a.iv, 32, hipMemcpyDeviceToHost, e->stream));
     if (out_copy) HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + ipad, a.out, out_copy, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(sync_spin(e->stream));
     if (out_copy) memcpy(out, e->h_stage + hdr + ipad, out_copy);
     if (ivec && mode != MODE_CBC_DEC) memcpy(ivec, h_iv, 16);
     if (p_num) *p_num = *h_pos;
@@ -1167,7 +1187,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h_iv, d_iv, 32, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + pay, e->d_stage + hdr + pay, len, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(sync_spin(e->stream));
     memcpy(out, e->h_stage + hdr + pay, len);
     memcpy(ivec, h_iv, 16);
     *p_num = *h_pos;
@@ -2632,7 +2652,7 @@ int fpnn_ecdh_calc_key_host(fpnn_aes_engine *e, const char *curve, const uint8_t
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
         if ((rc = fpnn_ecdh_calc_keys(e, cv, private_key, d, 1, keylen, d + 64, d + 96, d + 112))) break;
         err = hipMemcpyAsync(res, d + 64, sizeof res, hipMemcpyDeviceToHost, e->stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err == hipSuccess) err = sync_spin(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
     if (rc) return rc;
@@ -2657,7 +2677,7 @@ int fpnn_ecdh_public_key_host(fpnn_aes_engine *e, int curve, const uint8_t *priv
         if ((rc = fpnn_ecdh_public_keys(e, curve, d, 1, d + 32, d + 96))) break;
         err = hipMemcpyAsync(res, d + 32, 64, hipMemcpyDeviceToHost, e->stream);
         if (err == hipSuccess) err = hipMemcpyAsync(res + 64, d + 96, 1, hipMemcpyDeviceToHost, e->stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+        if (err == hipSuccess) err = sync_spin(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
     if (rc) return rc;
