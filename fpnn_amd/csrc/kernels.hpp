@@ -62,8 +62,12 @@ struct Variant {
     int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
     int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
     int hybrid = 1;        // ragged batches that take the queue: K2h (lanes + quads) instead of K2q
-    int hyb_long = 512;    // K2h: chains of at least this many blocks (bucket-rounded) go to quads
-    int hyb_quad_waves = 8;  // K2h: waves per workgroup that start on the long chains
+    // K2h: chains of at least hyb_long blocks (bucket-rounded) go to quads; hyb_quad_waves
+    // of a workgroup's 16 waves start on them.  Round-3 sweep on C4 (tools/gpu_r03w.sh,
+    // gpu_r03x.sh; profiles/r03/sweep_c4_r03x.json): 1024 / 12 at 790-799 GiB/s against
+    // 738 for round 2's 512 / 8 on the same box.
+    int hyb_long = 1024;
+    int hyb_quad_waves = 12;
     int hyb_wire_lanes = 0;  // K2h: wire-prefix batches also use the lane session (else all quads)
     int hyb_qflags = 0;      // K2h quad-session A/B flags (HybridArgs::qflags)
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
