@@ -227,3 +227,116 @@ def test_inversion_chain_is_fermat(curve):
     rng = random.Random(7 * len(curve))
     for a in [0, 1, 2, p - 1] + [rng.randrange(p) for _ in range(20)]:
         assert inv_chain(curve, a) == pow(a, p - 2, p)
+
+
+# ---- ecc_chains.hpp: the generated asm blocks, interpreted -------------------------------
+# Every asm block of fpnn_amd/csrc/ecc_chains.hpp is parsed and run here instruction by
+# instruction (one lane: carries as 0/1) on random and all-carry operands, and its outputs are
+# checked against big-integer arithmetic -- operand order (v_subrev / v_subbrev), carry
+# hand-offs and the borrow run through the top word are pinned on CPU before any GPU run.
+import os  # noqa: E402
+import re  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fpnn_amd", "csrc")
+
+
+def test_ecc_chains_header_matches_generator():
+    out = subprocess.run([sys.executable, os.path.join(CSRC, "gen_chains.py")], capture_output=True, text=True,
+                         check=True).stdout
+    assert out == open(os.path.join(CSRC, "ecc_chains.hpp")).read(), "regenerate: python3 gen_chains.py > ecc_chains.hpp"
+
+
+def _blocks():
+    src = open(os.path.join(CSRC, "ecc_chains.hpp")).read()
+    pat = re.compile(r"template <>\n__device__ __forceinline__ \w+ (\w+)<(\d+)>\((.*?)\) \{(.*?)\n\}\n", re.S)
+    for m in pat.finditer(src):
+        name, n, body = m.group(1), int(m.group(2)), m.group(4)
+        asm = re.search(r"asm\((.*?)\n\s*: (.*?)\n\s*: (.*?)\n\s*: ", body, re.S)
+        lines = [ln for ln in re.findall(r'"(.*?)(?:\\n\\t)?"', asm.group(1))]
+        outs = re.findall(r'"[=+&]*(\w)"\((.*?)\)', asm.group(2))
+        ins = re.findall(r'"(\w)"\((.*?)\)', asm.group(3))
+        yield name, n, lines, [(c, v, True) for c, v in outs] + [(c, v, False) for c, v in ins]
+
+
+def _run(lines, operands, env):
+    """env: variable name -> value (inputs); returns the outputs by variable name."""
+    reg = {}
+    nout = sum(1 for _, _, o in operands if o)
+    for k, (_, var, is_out) in enumerate(operands):
+        reg[f"%{k}"] = env.get(var, 0)
+    # "+v" outputs are also inputs (tied): the parser marks them as outputs whose value is read
+    regs = dict(reg)
+    regs["vcc"] = 0
+
+    def val(x):
+        return int(x) if re.fullmatch(r"\d+", x) else regs[x]
+
+    for ln in lines:
+        op, args = ln.split(None, 1)
+        a = [x.strip() for x in args.split(",")]
+        if op == "v_add_co_u32":
+            s = val(a[2]) + val(a[3]); regs[a[0]], regs[a[1]] = s % M, s >> 32
+        elif op == "v_addc_co_u32":
+            s = val(a[2]) + val(a[3]) + val(a[4]); regs[a[0]], regs[a[1]] = s % M, s >> 32
+        elif op in ("v_sub_co_u32", "v_subrev_co_u32", "v_subb_co_u32", "v_subbrev_co_u32"):
+            x, y = (val(a[3]), val(a[2])) if "rev" in op else (val(a[2]), val(a[3]))
+            b = val(a[4]) if "subb" in op else 0
+            s = x - y - b; regs[a[0]], regs[a[1]] = s % M, 1 if s < 0 else 0
+        elif op == "v_cndmask_b32":
+            regs[a[0]] = val(a[2]) if val(a[3]) else val(a[1])
+        elif op == "v_mad_u64_u32":
+            s = val(a[2]) * val(a[3]) + val(a[4]); regs[a[0]], regs[a[1]] = s % (1 << 64), s >> 64
+        else:
+            raise AssertionError(f"unmodelled instruction {op}")
+    return {operands[k][1]: regs[f"%{k}"] for k in range(nout)}
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_ecc_chains_asm_semantics(seed):
+    rng = random.Random(seed)
+    p = P["secp256k1"]
+    pl = {6: limbs(P["secp192r1"], 6), 7: limbs(P["secp224r1"], 7), 8: limbs(p, 8)}
+    seen = set()
+    for name, n, lines, ops in _blocks():
+        seen.add(name)
+        for trial in range(300):
+            def rnd(k):
+                return [rng.choice([0, 1, M - 1, M - 2, rng.randrange(M)]) for _ in range(k)]
+            if name in ("add_n", "sub_n"):
+                a, b = rnd(n), rnd(n)
+                env = {f"a[{i}]": a[i] for i in range(n)} | {f"b[{i}]": b[i] for i in range(n)}
+                out = _run(lines, ops, env)
+                r = [out[f"r[{i}]"] for i in range(n)]
+                A, B = value(a), value(b)
+                want = A + B if name == "add_n" else A - B
+                assert value(r) == want % (1 << (32 * n)), (name, n)
+                assert out["c"] == (1 if (want >= 1 << (32 * n) or want < 0) else 0), (name, n)
+            elif name == "reduce_n":
+                pp = pl[n]
+                P_ = value(pp)
+                v = rng.randrange(2 * P_)
+                t, top = limbs(v % (1 << (32 * n)), n), v >> (32 * n)
+                env = {f"t[{i}]": t[i] for i in range(n)} | {f"p[{i}]": pp[i] for i in range(n)} | {"top": top}
+                out = _run(lines, ops, env)
+                assert value([out[f"r[{i}]"] for i in range(n)]) == v % P_, (name, n)
+            elif name == "fsub_n":
+                pp = pl[n]
+                P_ = value(pp)
+                x, y = rng.randrange(P_), rng.randrange(P_)
+                a, b = limbs(x, n), limbs(y, n)
+                env = {f"a[{i}]": a[i] for i in range(n)} | {f"b[{i}]": b[i] for i in range(n)} | \
+                      {f"p[{i}]": pp[i] for i in range(n)}
+                out = _run(lines, ops, env)
+                assert value([out[f"r[{i}]"] for i in range(n)]) == (x - y) % P_, (name, n)
+            elif name == "mac_col":
+                x, y = rnd(n), rnd(n)
+                lo = rng.randrange(1 << 64)
+                env = {f"x[{j}]": x[j] for j in range(n)} | {f"y[{j}]": y[j] for j in range(n)} | {"lo": lo}
+                out = _run(lines, ops, env)
+                want = lo + sum(x[j] * y[j] for j in range(n))
+                assert out["lo"] + (out["hi"] << 64) == want, (name, n)
+            else:
+                raise AssertionError(f"untested block {name}")
+    assert seen == {"add_n", "sub_n", "reduce_n", "fsub_n", "mac_col"}
