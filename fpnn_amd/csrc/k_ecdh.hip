@@ -105,52 +105,42 @@ __device__ __forceinline__ Fe<NW> k1_fold(const uint32_t (&t)[16], const EccCons
 }
 
 // secp256r1 (p = 2^256 - 2^224 + 2^192 + 2^96 - 1): the NIST word-sum reduction (FIPS
-// 186-4 D.2.3) t = s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9 as signed column sums,
-// the signed carry k (|k| <= 6) folded back as k * (2^224 - 2^192 - 2^96 + 1), and the
-// final carry c2 in {-1, 0, 1} settled by one add or subtract of p (all selects).
+// 186-4 D.2.3) t = s1 + 2 s2 + 2 s3 + s4 + s5 - s6 - s7 - s8 - s9, as nine 8-limb carry
+// chains (ecc_chains.hpp; 2 (s2 + s3) as one sum doubled) whose carries and borrows add up
+// to a signed top k in [-4, 6]; k * 2^256 is folded back as k * (2^224 - 2^192 - 2^96 + 1)
+// in one add and one subtract chain ([kp,0,0,kn,0,0,kn,kp] and [kn,0,0,kp,0,0,kp,kn] with
+// kp = max(k, 0), kn = max(-k, 0)); their carry minus borrow (-1, 0 or 1) is settled by
+// one add or subtract of p (selects).  (Round 2 summed the words as signed 64-bit column
+// sums: ~50 more instructions per fold.)
 template <int NW>
 __device__ __forceinline__ Fe<NW> p256_fold(const uint32_t (&t)[16], const EccConst &c) {
-    const int64_t c0 = t[0], c1 = t[1], c2 = t[2], c3 = t[3], c4 = t[4], c5 = t[5], c6 = t[6], c7 = t[7];
-    const int64_t c8 = t[8], c9 = t[9], c10 = t[10], c11 = t[11], c12 = t[12], c13 = t[13], c14 = t[14],
-                  c15 = t[15];
-    int64_t a[8];
-    a[0] = c0 + c8 + c9 - c11 - c12 - c13 - c14;
-    a[1] = c1 + c9 + c10 - c12 - c13 - c14 - c15;
-    a[2] = c2 + c10 + c11 - c13 - c14 - c15;
-    a[3] = c3 + 2 * (c11 + c12) + c13 - c15 - c8 - c9;
-    a[4] = c4 + 2 * (c12 + c13) + c14 - c9 - c10;
-    a[5] = c5 + 2 * (c13 + c14) + c15 - c10 - c11;
-    a[6] = c6 + 3 * c14 + 2 * c15 + c13 - c8 - c9;
-    a[7] = c7 + 3 * c15 + c8 - c10 - c11 - c12 - c13;
-    uint32_t u[8];
-    int64_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        acc += a[j];
-        u[j] = (uint32_t)acc;
-        acc >>= 32;  // arithmetic
-    }
-    const int64_t k = acc;
-    int64_t b[8] = {(int64_t)u[0] + k, u[1], u[2], (int64_t)u[3] - k, u[4], u[5], (int64_t)u[6] - k,
-                    (int64_t)u[7] + k};
-    acc = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        acc += b[j];
-        u[j] = (uint32_t)acc;
-        acc >>= 32;
-    }
-    const int32_t cr = (int32_t)acc;  // -1, 0 or 1: value = U + cr * 2^256
-    uint32_t d[8], e[8], borrow = 0, carry = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint64_t sd = (uint64_t)u[j] - c.p[j] - borrow;
-        d[j] = (uint32_t)sd;
-        borrow = (uint32_t)(sd >> 63);
-        const uint64_t se = (uint64_t)u[j] + c.p[j] + carry;
-        e[j] = (uint32_t)se;
-        carry = (uint32_t)(se >> 32);
-    }
+    const uint32_t z = 0;
+    const uint32_t s2[8] = {z, z, z, t[11], t[12], t[13], t[14], t[15]};
+    const uint32_t s3[8] = {z, z, z, t[12], t[13], t[14], t[15], z};
+    const uint32_t s4[8] = {t[8], t[9], t[10], z, z, z, t[14], t[15]};
+    const uint32_t s5[8] = {t[9], t[10], t[11], t[13], t[14], t[15], t[13], t[8]};
+    const uint32_t s6[8] = {t[11], t[12], t[13], z, z, z, t[8], t[10]};
+    const uint32_t s7[8] = {t[12], t[13], t[14], t[15], z, z, t[9], t[11]};
+    const uint32_t s8[8] = {t[13], t[14], t[15], t[8], t[9], t[10], z, t[12]};
+    const uint32_t s9[8] = {t[14], t[15], z, t[9], t[10], t[11], z, t[13]};
+    uint32_t v[8], w[8], u[8];
+    const uint32_t cv = add_n<8>(v, s2, s3);
+    const uint32_t cw = add_n<8>(w, v, v);  // 2 (s2 + s3) = w + (2 cv + cw) 2^256
+    int32_t k = (int32_t)(2 * cv + cw);
+    k += (int32_t)add_n<8>(u, t, w);  // s1 = t[0..7]
+    k += (int32_t)add_n<8>(v, u, s4);
+    k += (int32_t)add_n<8>(u, v, s5);
+    k -= (int32_t)sub_n<8>(v, u, s6);
+    k -= (int32_t)sub_n<8>(u, v, s7);
+    k -= (int32_t)sub_n<8>(v, u, s8);
+    k -= (int32_t)sub_n<8>(u, v, s9);
+    const uint32_t kp = k > 0 ? (uint32_t)k : 0u, kn = k < 0 ? (uint32_t)-k : 0u;
+    const uint32_t fa[8] = {kp, z, z, kn, z, z, kn, kp};
+    const uint32_t fb[8] = {kn, z, z, kp, z, z, kp, kn};
+    const int32_t cr = (int32_t)add_n<8>(v, u, fa) - (int32_t)sub_n<8>(u, v, fb);  // value = U + cr 2^256
+    uint32_t d[8], e[8];
+    const uint32_t borrow = sub_n<8>(d, u, c.p);
+    add_n<8>(e, u, c.p);
     const bool use_e = cr < 0, use_d = cr > 0 || (cr == 0 && borrow == 0);
     Fe<NW> r;
 #pragma unroll

@@ -76,28 +76,42 @@ def k1_fold(t):  # k_ecdh.hip k1_fold: three carry chains, a top fold, one subtr
     return v - p if v >= p else v
 
 
-def p256_fold(t):  # k_ecdh.hip p256_fold
+def p256_fold(t):  # k_ecdh.hip p256_fold: nine 8-limb chains, a signed top, one fold, settle
+    W = 1 << 256
+
+    def add(x, y):  # add_n<8>: (sum mod 2^256, carry)
+        s = value(x) + value(y)
+        return limbs(s % W, 8), s >> 256
+
+    def sub(x, y):  # sub_n<8>: (difference mod 2^256, borrow)
+        s = value(x) - value(y)
+        return limbs(s % W, 8), 1 if s < 0 else 0
+
     c = t
-    a = [c[0] + c[8] + c[9] - c[11] - c[12] - c[13] - c[14],
-         c[1] + c[9] + c[10] - c[12] - c[13] - c[14] - c[15],
-         c[2] + c[10] + c[11] - c[13] - c[14] - c[15],
-         c[3] + 2 * (c[11] + c[12]) + c[13] - c[15] - c[8] - c[9],
-         c[4] + 2 * (c[12] + c[13]) + c[14] - c[9] - c[10],
-         c[5] + 2 * (c[13] + c[14]) + c[15] - c[10] - c[11],
-         c[6] + 3 * c[14] + 2 * c[15] + c[13] - c[8] - c[9],
-         c[7] + 3 * c[15] + c[8] - c[10] - c[11] - c[12] - c[13]]
-    u, acc = [0] * 8, 0
-    for j in range(8):
-        acc += a[j]
-        u[j], acc = acc & (M - 1), acc >> 32
-    k = acc
-    assert -6 <= k <= 6
-    b = [u[0] + k, u[1], u[2], u[3] - k, u[4], u[5], u[6] - k, u[7] + k]
-    acc = 0
-    for j in range(8):
-        acc += b[j]
-        u[j], acc = acc & (M - 1), acc >> 32
-    return settle(u, acc, P["secp256r1"], 8)
+    s2 = [0, 0, 0, c[11], c[12], c[13], c[14], c[15]]
+    s3 = [0, 0, 0, c[12], c[13], c[14], c[15], 0]
+    s4 = [c[8], c[9], c[10], 0, 0, 0, c[14], c[15]]
+    s5 = [c[9], c[10], c[11], c[13], c[14], c[15], c[13], c[8]]
+    s6 = [c[11], c[12], c[13], 0, 0, 0, c[8], c[10]]
+    s7 = [c[12], c[13], c[14], c[15], 0, 0, c[9], c[11]]
+    s8 = [c[13], c[14], c[15], c[8], c[9], c[10], 0, c[12]]
+    s9 = [c[14], c[15], 0, c[9], c[10], c[11], 0, c[13]]
+    v, cv = add(s2, s3)
+    w, cw = add(v, v)
+    k = 2 * cv + cw
+    u, cy = add(c[:8], w)
+    k += cy
+    for s_ in (s4, s5):
+        u, cy = add(u, s_)
+        k += cy
+    for s_ in (s6, s7, s8, s9):
+        u, bo = sub(u, s_)
+        k -= bo
+    assert -4 <= k <= 6
+    kp, kn = max(k, 0), max(-k, 0)
+    u, ca = add(u, [kp, 0, 0, kn, 0, 0, kn, kp])
+    u, cb = sub(u, [kn, 0, 0, kp, 0, 0, kp, kn])
+    return settle(u, ca - cb, P["secp256r1"], 8)
 
 
 def p224_fold(t):  # k_ecdh.hip p224_fold
