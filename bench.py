@@ -40,7 +40,7 @@ METRIC = "AES-256 GiB/s on device-resident packet batch; 1/2/4/8-GPU scaling"  #
 # newest committed PMC summary of the bench command (tools/pmc_summary.py output), per workload
 # (C2: profiles of this bench command, tools/profile_session.sh; C4 / C5: tools/profile_configs.sh
 # runs of the same kernels on the same batches through tools/bench_configs.py)
-PMC_SUMMARIES = {"C2": "profiles/r02/bench/pmc_summary.json", "C4": "profiles/r02/C4/pmc_summary.json",
+PMC_SUMMARIES = {"C2": "profiles/r03/bench/pmc_summary.json", "C4": "profiles/r03/C4_r03y/pmc_summary.json",
                  "C5": "profiles/r02/C5/pmc_summary.json"}
 
 
