@@ -252,49 +252,34 @@ __device__ __forceinline__ Fe<NW> p192_fold(const uint32_t (&t)[12], const EccCo
     return reduce_once<NW>(u, (uint32_t)acc, c);
 }
 
-// secp224r1 (p = 2^224 - 2^96 + 1): t = L + H*(2^96 - 1) as signed column sums, the
-// signed top (weight 2^224, < 2^97) folded once more, the last carry (-1, 0 or 1)
-// settled by one add or subtract of p (selects)
+// secp224r1 (p = 2^224 - 2^96 + 1): the NIST word-sum reduction (FIPS 186-4 D.2.2)
+// t = s1 + s2 + s3 - s4 - s5 as four 7-limb carry chains whose carries and borrows sum to a
+// signed top k in [-2, 2]; k * 2^224 is folded back as k * (2^96 - 1) in one add and one
+// subtract chain ([kn,0,0,kp,0,0,0] and [kp,0,0,kn,0,0,0]); their carry minus borrow
+// (-1, 0 or 1) is settled by one add or subtract of p (selects), as p256_fold.
 template <int NW>
 __device__ __forceinline__ Fe<NW> p224_fold(const uint32_t (&t)[14], const EccConst &c) {
-    uint32_t u[7];
-    int64_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        acc += (int64_t)t[j] - (int64_t)t[7 + j] + (j >= 3 ? (int64_t)t[4 + j] : 0);
-        u[j] = (uint32_t)acc;
-        acc >>= 32;  // arithmetic
-    }
-    int64_t tl[4];  // the top in limbs: tl[0..2] unsigned 32-bit, tl[3] the signed rest
-    acc += t[11];
-    tl[0] = (uint32_t)acc;
-    acc = (acc >> 32) + t[12];
-    tl[1] = (uint32_t)acc;
-    acc = (acc >> 32) + t[13];
-    tl[2] = (uint32_t)acc;
-    tl[3] = acc >> 32;
-    acc = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        acc += (int64_t)u[j] - (j < 4 ? tl[j] : 0) + (j >= 3 ? tl[j - 3] : 0);
-        u[j] = (uint32_t)acc;
-        acc >>= 32;
-    }
-    const int32_t cr = (int32_t)acc;
-    uint32_t d[7], e[7], borrow = 0, carry = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        const uint64_t sd = (uint64_t)u[j] - c.p[j] - borrow;
-        d[j] = (uint32_t)sd;
-        borrow = (uint32_t)(sd >> 63);
-        const uint64_t se = (uint64_t)u[j] + c.p[j] + carry;
-        e[j] = (uint32_t)se;
-        carry = (uint32_t)(se >> 32);
-    }
+    const uint32_t z = 0;
+    const uint32_t s2[7] = {z, z, z, t[7], t[8], t[9], t[10]};
+    const uint32_t s3[7] = {z, z, z, t[11], t[12], t[13], z};
+    const uint32_t s4[7] = {t[7], t[8], t[9], t[10], t[11], t[12], t[13]};
+    const uint32_t s5[7] = {t[11], t[12], t[13], z, z, z, z};
+    uint32_t u[7], v[7];
+    int32_t k = (int32_t)add_n<7>(u, t, s2);  // s1 = t[0..6]
+    k += (int32_t)add_n<7>(v, u, s3);
+    k -= (int32_t)sub_n<7>(u, v, s4);
+    k -= (int32_t)sub_n<7>(v, u, s5);
+    const uint32_t kp = k > 0 ? (uint32_t)k : 0u, kn = k < 0 ? (uint32_t)-k : 0u;
+    const uint32_t fa[7] = {kn, z, z, kp, z, z, z};
+    const uint32_t fb[7] = {kp, z, z, kn, z, z, z};
+    const int32_t cr = (int32_t)add_n<7>(u, v, fa) - (int32_t)sub_n<7>(v, u, fb);  // value = V + cr 2^224
+    uint32_t d[7], e[7];
+    const uint32_t borrow = sub_n<7>(d, v, c.p);
+    add_n<7>(e, v, c.p);
     const bool use_e = cr < 0, use_d = cr > 0 || (cr == 0 && borrow == 0);
     Fe<NW> r;
 #pragma unroll
-    for (int j = 0; j < 7; j++) r.v[j] = use_e ? e[j] : (use_d ? d[j] : u[j]);
+    for (int j = 0; j < 7; j++) r.v[j] = use_e ? e[j] : (use_d ? d[j] : v[j]);
     return r;
 }
 

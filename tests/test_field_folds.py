@@ -114,23 +114,30 @@ def p256_fold(t):  # k_ecdh.hip p256_fold: nine 8-limb chains, a signed top, one
     return settle(u, ca - cb, P["secp256r1"], 8)
 
 
-def p224_fold(t):  # k_ecdh.hip p224_fold
-    u, acc = [0] * 7, 0
-    for j in range(7):
-        acc += t[j] - t[7 + j] + (t[4 + j] if j >= 3 else 0)
-        u[j], acc = acc & (M - 1), acc >> 32
-    acc += t[11]
-    tl = [acc & (M - 1)]
-    acc = (acc >> 32) + t[12]
-    tl.append(acc & (M - 1))
-    acc = (acc >> 32) + t[13]
-    tl += [acc & (M - 1), acc >> 32]
-    assert -2 <= tl[3] <= 1
-    acc = 0
-    for j in range(7):
-        acc += u[j] - (tl[j] if j < 4 else 0) + (tl[j - 3] if j >= 3 else 0)
-        u[j], acc = acc & (M - 1), acc >> 32
-    return settle(u, acc, P["secp224r1"], 7)
+def p224_fold(t):  # k_ecdh.hip p224_fold: four 7-limb chains, a signed top, one fold, settle
+    W = 1 << 224
+
+    def add(x, y):
+        s = value(x) + value(y)
+        return limbs(s % W, 7), s >> 224
+
+    def sub(x, y):
+        s = value(x) - value(y)
+        return limbs(s % W, 7), 1 if s < 0 else 0
+
+    c = t
+    u, k = add(c[:7], [0, 0, 0, c[7], c[8], c[9], c[10]])
+    u, cy = add(u, [0, 0, 0, c[11], c[12], c[13], 0])
+    k += cy
+    u, bo = sub(u, [c[7], c[8], c[9], c[10], c[11], c[12], c[13]])
+    k -= bo
+    u, bo = sub(u, [c[11], c[12], c[13], 0, 0, 0, 0])
+    k -= bo
+    assert -2 <= k <= 2
+    kp, kn = max(k, 0), max(-k, 0)
+    u, ca = add(u, [kn, 0, 0, kp, 0, 0, 0])
+    u, cb = sub(u, [kp, 0, 0, kn, 0, 0, 0])
+    return settle(u, ca - cb, P["secp224r1"], 7)
 
 
 def p192_fold(t):  # k_ecdh.hip p192_fold
