@@ -228,28 +228,23 @@ __device__ __forceinline__ void prod_dual(const uint32_t *a1, const uint32_t *b1
     prod_scan<NW, SQ2>(a2, b2, t2);
 }
 
-// secp192r1 (p = 2^192 - 2^64 - 1): t = L + H*(2^64 + 1), all terms positive; the top
-// (< 2^66, weight 2^192) folds once more the same way; the result is < 2^192 + 2^131 < 2p
+// secp192r1 (p = 2^192 - 2^64 - 1): the NIST word-sum reduction (FIPS 186-4 D.2.1)
+// t = s1 + s2 + s3 + s4 as three 6-limb carry chains, the top k in [0, 3] folded back as
+// k * (2^64 + 1) in one chain, and one conditional subtraction through its carry
+// (U + c 2^192 < 2p: c = 1 only when U < 2^66)
 template <int NW>
 __device__ __forceinline__ Fe<NW> p192_fold(const uint32_t (&t)[12], const EccConst &c) {
-    uint32_t u[6];
-    uint64_t acc = 0;
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-        acc += (uint64_t)t[j] + t[6 + j] + (j >= 2 ? t[4 + j] : 0u);
-        u[j] = (uint32_t)acc;
-        acc >>= 32;
-    }
-    const uint64_t top = acc + t[10] + ((uint64_t)t[11] << 32);  // < 2^66
-    const uint64_t tl[2] = {(uint32_t)top, top >> 32};
-    acc = 0;
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-        acc += (uint64_t)u[j] + (j < 2 ? tl[j] : 0u) + (j >= 2 && j < 4 ? tl[j - 2] : 0u);
-        u[j] = (uint32_t)acc;
-        acc >>= 32;
-    }
-    return reduce_once<NW>(u, (uint32_t)acc, c);
+    const uint32_t z = 0;
+    const uint32_t s2[6] = {t[6], t[7], t[6], t[7], z, z};
+    const uint32_t s3[6] = {z, z, t[8], t[9], t[8], t[9]};
+    const uint32_t s4[6] = {t[10], t[11], t[10], t[11], t[10], t[11]};
+    uint32_t u[6], v[6];
+    uint32_t k = add_n<6>(u, t, s2);  // s1 = t[0..5]
+    k += add_n<6>(v, u, s3);
+    k += add_n<6>(u, v, s4);
+    const uint32_t fk[6] = {k, z, k, z, z, z};
+    const uint32_t cy = add_n<6>(v, u, fk);
+    return reduce_once<NW>(v, cy, c);
 }
 
 // secp224r1 (p = 2^224 - 2^96 + 1): the NIST word-sum reduction (FIPS 186-4 D.2.2)

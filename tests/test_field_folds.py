@@ -140,21 +140,23 @@ def p224_fold(t):  # k_ecdh.hip p224_fold: four 7-limb chains, a signed top, one
     return settle(u, ca - cb, P["secp224r1"], 7)
 
 
-def p192_fold(t):  # k_ecdh.hip p192_fold
+def p192_fold(t):  # k_ecdh.hip p192_fold: three 6-limb chains, one fold chain, one subtraction
+    W = 1 << 192
+
+    def add(x, y):
+        s = value(x) + value(y)
+        return limbs(s % W, 6), s >> 192
+
+    c = t
+    u, k = add(c[:6], [c[6], c[7], c[6], c[7], 0, 0])
+    u, cy = add(u, [0, 0, c[8], c[9], c[8], c[9]])
+    k += cy
+    u, cy = add(u, [c[10], c[11], c[10], c[11], c[10], c[11]])
+    k += cy
+    assert 0 <= k <= 3
+    u, cy = add(u, [k, 0, k, 0, 0, 0])
     p = P["secp192r1"]
-    u, acc = [0] * 6, 0
-    for j in range(6):
-        acc += t[j] + t[6 + j] + (t[4 + j] if j >= 2 else 0)
-        u[j], acc = acc & (M - 1), acc >> 32
-    top = acc + t[10] + (t[11] << 32)
-    assert top < 1 << 66
-    tl = [top & (M - 1), top >> 32]
-    acc = 0
-    for j in range(6):
-        acc += u[j] + (tl[j] if j < 2 else 0) + (tl[j - 2] if 2 <= j < 4 else 0)
-        u[j], acc = acc & (M - 1), acc >> 32
-    assert acc in (0, 1)
-    v = value(u) + (acc << 192)
+    v = value(u) + (cy << 192)
     assert v < 2 * p
     return v - p if v >= p else v
 
