@@ -531,7 +531,12 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if (!k.out_off) k.out_off = k.in_off;
         EventPair *ev = nullptr;
         if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, e->d_sink, e->variant.fence, grid, e->stream));
+        // in place (in == out, identical offsets: fpnn_aes.h) the predecessor blocks of the
+        // waves' first chunks are saved by a plan launch before any wave writes; otherwise
+        // every wave finds its own at the start of the decrypt kernel (one launch fewer)
+        const bool plan_launch = inplace || e->variant.k1r_plan;
+        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, e->d_sink, e->variant.fence,
+                                      plan_launch, grid, e->stream));
         return timing_end(e, ev, FPNN_AES_K_DECRYPT);
     }
     EventPair *ev = nullptr;
@@ -573,7 +578,8 @@ const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
 const char *fpnn_aes_version(void) {
     return "fpnn_aes 0.1 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
            "decrypt: K1d dense/keyed, K1k lane keys, K1r ragged (no host sync), K1 uniform, one lane per block; "
-           "encrypt: K2 lane per chain, K2c/K2q quad per chain)";
+           "encrypt: K2 lane per chain, K2c quad per chain, K2h lanes + quads for ragged batches; "
+           "ECDH: one lane per derivation, special-prime folds as carry chains)";
 }
 
 int fpnn_aes_setup_encrypt(fpnn_aes_schedule *ctx, const uint8_t *key, size_t keylen) {
@@ -625,6 +631,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
     if (const char *v = getenv("FPNN_AES_HYBRID")) e->variant.hybrid = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_FENCE")) e->variant.fence = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K1R_PLAN")) e->variant.k1r_plan = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;

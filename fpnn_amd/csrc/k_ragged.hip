@@ -169,18 +169,24 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     // which is read through constant-address loads the compiler may repeat anywhere)
     uint8_t *scratch = reinterpret_cast<uint8_t *>(sink + 2 * w);
 
+    // the wave's first segment and the ciphertext block in front of its first chunk: from
+    // the plan launch (in place), or found here when no wave writes what another reads
+    uint64_t wb;
+    uint4 fill;
+    if (plan) {
+        wb = ((ConstU64R *)&plan[w].s0)[0];
+        ConstU32R *fp = (ConstU32R *)&plan[w].fill;
+        fill = make_uint4(fp[0], fp[1], fp[2], fp[3]);
+    } else {
+        wb = readfirst64(wave_find_segment(b.bstart, count, c0 << 6, lane));
+        fill = predecessor_block<STREAM>(b, wb, c0 << 6);
+    }
     // window: wv = bstart[wb + lane] (all-ones past bstart[count])
-    uint64_t wb = ((ConstU64R *)&plan[w].s0)[0];
     auto load_window = [&]() -> uint64_t {
         const uint64_t i = wb + lane;
         return i <= count ? b.bstart[i] : ~0ull;
     };
     uint64_t wv = load_window();
-    uint4 fill;
-    {
-        ConstU32R *fp = (ConstU32R *)&plan[w].fill;
-        fill = make_uint4(fp[0], fp[1], fp[2], fp[3]);
-    }
 
     // descriptors of the segment of the last fetched single-segment chunk (SGPRs)
     uint32_t last_s = ~0u, last_len = 0, last_slot = 0, last_n0 = 0;
@@ -437,10 +443,12 @@ static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan
 }
 
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
-                                 bool fence, int grid, hipStream_t st) {
+                                 bool fence, bool plan_launch, int grid, hipStream_t st) {
     const uint64_t nwaves = (uint64_t)grid * (kThreads / 64);
     const unsigned pgrid = (unsigned)((nwaves * 64 + 255) / 256);
-    if (stream)
+    if (!plan_launch)
+        plan = nullptr;  // out of place: each wave plans itself (k_cfb_decrypt_ragged)
+    else if (stream)
         hipLaunchKernelGGL((k_ragged_plan<true>), dim3(pgrid), dim3(256), 0, st, b, nwaves, plan);
     else
         hipLaunchKernelGGL((k_ragged_plan<false>), dim3(pgrid), dim3(256), 0, st, b, nwaves, plan);

@@ -87,49 +87,95 @@ constexpr int kSmallScanThreads = 1024;
 constexpr int kSmallScanItems = 16;
 constexpr uint64_t kSmallScanMax = (uint64_t)kSmallScanThreads * kSmallScanItems;
 
+// Round k covers segments [k·1024, k·1024 + 1024), one per thread, so every load and
+// store is coalesced and all of a thread's loads are in flight together.  Segment order
+// is (round, wave, lane): each round's values are scanned inside the wave (DPP-free
+// shuffles, 6 steps), the ≤ 256 wave totals in that same order are scanned by wave 0,
+// and two barriers join the halves (the round-1 form held contiguous runs per thread and
+// paid 20 barriers of a 1024-wide Hillis-Steele scan: ≈ 10 µs per framed call).
 template <bool STREAM>
-__global__ __launch_bounds__(kSmallScanThreads) void k_scan_small(KBatch b, const uint4 *iv_src, const uint32_t *pos_src,
-                                                                  uint4 *snap_iv, uint32_t *snap_pos, uint64_t *bstart,
-                                                                  uint64_t *total_out) {
-    __shared__ uint64_t sh[kSmallScanThreads];
-    const int t = threadIdx.x;
-    const uint64_t per = (b.count + kSmallScanThreads - 1) / kSmallScanThreads;  // <= kSmallScanItems
-    const uint64_t lo = (uint64_t)t * per;
-    uint64_t v[kSmallScanItems], sum = 0;
+__global__ __launch_bounds__(kSmallScanThreads) void k_scan_small(KBatch b, const uint4 *__restrict__ iv_src,
+                                                                  const uint32_t *__restrict__ pos_src,
+                                                                  uint4 *__restrict__ snap_iv,
+                                                                  uint32_t *__restrict__ snap_pos,
+                                                                  uint64_t *__restrict__ bstart,
+                                                                  uint64_t *__restrict__ total_out) {
+    constexpr int kWaves = kSmallScanThreads / 64;
+    __shared__ uint64_t grp[kSmallScanItems * kWaves + 1];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t count = b.count;  // 1 <= count <= kSmallScanMax (host)
+    const uint32_t per = (count + kSmallScanThreads - 1) / kSmallScanThreads;
+    const uint32_t *__restrict__ lens = b.len;
+    uint32_t len[kSmallScanItems], pos[kSmallScanItems];
 #pragma unroll
-    for (int k = 0; k < kSmallScanItems; k++) {
-        const uint64_t s = lo + k;
-        v[k] = 0;
-        if ((uint64_t)k < per && s < b.count) {
-            const uint32_t len = b.len ? b.len[s] : b.uniform_len;
-            uint32_t pos = 0;
-            if (STREAM) {
-                pos = pos_src[s];
-                snap_pos[s] = pos;
-                snap_iv[s] = iv_src[s];
-            }
-            v[k] = seg_blocks(len, pos);
+    for (int k = 0; k < kSmallScanItems; k++) {  // loads of every round first
+        if ((uint32_t)k < per) {
+            const uint32_t s = k * kSmallScanThreads + t, sc = s < count ? s : count - 1;
+            len[k] = lens ? lens[sc] : b.uniform_len;
+            pos[k] = STREAM ? pos_src[sc] : 0u;
         }
-        sum += v[k];
     }
-    sh[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < kSmallScanThreads; off <<= 1) {
-        const uint64_t add = t >= off ? sh[t - off] : 0;
-        __syncthreads();
-        sh[t] += add;
-        __syncthreads();
+    if (STREAM) {  // the (iv, pos) snapshot the decrypt kernels read
+#pragma unroll
+        for (int k = 0; k < kSmallScanItems; k++) {
+            const uint32_t s = k * kSmallScanThreads + t;
+            if ((uint32_t)k < per && s < count) {
+                snap_iv[s] = iv_src[s];
+                snap_pos[s] = pos[k];
+            }
+        }
     }
-    uint64_t run = sh[t] - sum;
+    uint64_t ex[kSmallScanItems];  // exclusive prefix inside the wave, then the segment's bstart
 #pragma unroll
     for (int k = 0; k < kSmallScanItems; k++) {
-        const uint64_t s = lo + k;
-        if ((uint64_t)k < per && s < b.count) bstart[s] = run;
-        run += v[k];
+        if ((uint32_t)k < per) {
+            const uint32_t s = k * kSmallScanThreads + t;
+            const uint64_t v = s < count ? seg_blocks(len[k], pos[k]) : 0;
+            uint64_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(x, d, 64);
+                if (lane >= (uint32_t)d) x += y;
+            }
+            ex[k] = x - v;
+            if (lane == 63) grp[k * kWaves + wv] = x;
+        }
     }
-    if (t == kSmallScanThreads - 1) {
-        bstart[b.count] = sh[t];
-        *total_out = sh[t];
+    __syncthreads();
+    if (wv == 0) {  // exclusive scan of the per * 16 wave totals, 4 per lane
+        const uint32_t n = per * kWaves;
+        uint64_t g[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t j = lane * 4 + i;
+            g[i] = j < n ? grp[j] : 0;
+            sum += g[i];
+        }
+        uint64_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        uint64_t run = x - sum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t j = lane * 4 + i;
+            if (j < n) grp[j] = run;
+            run += g[i];
+        }
+        if (lane == 63) grp[kSmallScanItems * kWaves] = x;  // the block total
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmallScanItems; k++) {
+        const uint32_t s = k * kSmallScanThreads + t;
+        if ((uint32_t)k < per && s < count) bstart[s] = grp[k * kWaves + wv] + ex[k];
+    }
+    if (t == 0) {
+        const uint64_t total = grp[kSmallScanItems * kWaves];
+        bstart[count] = total;
+        *total_out = total;
     }
 }
 

@@ -73,6 +73,9 @@ struct Variant {
     int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
     int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
     int fence = 1;         // K2 / K1d (C2 shape), K1r, K2h: issue each round's 16 lookups before folding
+    // K1r per-wave plan: 0 = in the decrypt kernel itself when in != out (no other wave
+    // can overwrite a predecessor block then), 1 = always the separate k_ragged_plan launch
+    int k1r_plan = 0;
 };
 
 int blocks_per_cu(const Variant &v, KeyMode km);
@@ -157,7 +160,7 @@ struct RaggedPlan {
 // ones from stride / uniform_len; out_off may be in_off).
 // sink: 2 x uint4 per wave of the grid, written by lanes with nothing to store, never read.
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
-                                 bool fence, int grid, hipStream_t st);
+                                 bool fence, bool plan_launch, int grid, hipStream_t st);
 hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len, uint64_t *in_off, uint32_t *len,
                               hipStream_t st);
 // In-place K1 / K1d: save the ciphertext block before every 64-block chunk.
