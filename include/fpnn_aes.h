@@ -111,7 +111,8 @@ int fpnn_aes_keyset_get_schedule(fpnn_aes_keyset *ks, uint32_t slot, fpnn_aes_sc
  *   len     == NULL -> len_i      = uniform_len
  *   key_slot== NULL -> slot_i     = 0            (index into the key set)
  * Offsets/lengths/slots are device arrays.  `in` and `out` may be the same
- * buffer with identical offsets (in-place); any other overlap is undefined. */
+ * buffer with identical offsets (in-place: in == out as pointers); any other overlap
+ * -- including in != out pointers whose ranges meet -- is undefined. */
 typedef struct {
     const uint8_t *in;          /* dev */
     uint8_t *out;               /* dev */

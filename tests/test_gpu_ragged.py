@@ -118,6 +118,41 @@ def test_stream_segments_random_positions(engine, oracle, keylen):
         assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 1023, 1024, 1025, 5000, 16383, 16384, 16385])
+def test_block_map_round_boundaries(engine, oracle, n):
+    """The single-workgroup block map (k_scan_small, up to 16 384 segments) takes segment
+    k*1024 + t in thread t and scans per wave, then the wave totals: segment counts at and
+    around the 64 / 1024 multiples and the small/large switch (16 385 takes the 3-launch
+    scan), stream mode (the (iv, pos) snapshot comes from the same kernel) and package mode
+    out of place (per-wave plan inside K1r) and in place (plan launch)."""
+    rng = np.random.default_rng(9000 + n)
+    lens = rng.integers(0, 300, n)
+    lens[rng.random(n) < 0.05] = 0
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + 1)]).astype(np.int64)
+    for inplace in (False, True):
+        _package_case(engine, oracle, rng, lens.astype(np.int64), offs, keylen=16, inplace=inplace)
+    total = int(offs[-1] + lens[-1] + 64)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    keys = rng.integers(0, 256, 4 * 16, dtype=np.uint8)
+    iv_state = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    pos_state = rng.integers(0, 16, n).astype(np.uint32)
+    slots = rng.integers(0, 4, n).astype(np.uint32)
+    exp = inp.copy()
+    iv_exp, pos_exp = iv_state.copy(), pos_state.copy()
+    oracle.stream_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                        lens=lens.astype(np.uint32), key_slot=slots, keys=keys, keylen=16, iv_state=iv_exp,
+                        pos_state=pos_exp, threads=8)
+    ks = keyset(engine, keys, 16, np.zeros(4 * 16, np.uint8))
+    src, dst = to_dev(inp), to_dev(inp)
+    ivd, posd = to_dev(iv_state), to_dev(pos_state.astype(np.int32))
+    engine.stream_decrypt(src, dst, n, ks, ivd, posd, in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)),
+                          key_slot=to_dev(slots.astype(np.int32)))
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(dst), exp)
+    assert np.array_equal(to_host(ivd), iv_exp)
+    assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
+
+
 # ------------------------------------------------------------------------------------
 # queue-only: the C-ABI's ragged calls must not wait for the GPU (fpnn_aes.h)
 
