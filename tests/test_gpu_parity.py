@@ -380,7 +380,7 @@ def test_dense_keyed_layout(engine, oracle, length, inplace):
     rng = np.random.default_rng(length + inplace)
     n, nkeys = 777, 97
     inp = rng.integers(0, 256, n * length + 64, dtype=np.uint8)
-    for keylen in (16, 32):
+    for keylen in (16, 24, 32):
         keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
         ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
         slots = rng.integers(0, nkeys, n).astype(np.int32)
