@@ -63,6 +63,10 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of m
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+#ifndef FPNN_K2H_VKEYS
+#define FPNN_K2H_VKEYS 0
+#endif
+
 template <int NR, int KM, bool STREAM, int NT, int CH, bool SHIFT, bool FENCE, bool LANES = true>
 __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cfb_encrypt_hybrid(KBatch b, HybridArgs h) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
@@ -82,7 +86,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     const bool wm = SHIFT && __builtin_amdgcn_readfirstlane(h.buckets[kWireFlagWord]) == 0u;
 
     RoundKeys<NR> rku;
-    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+    if (KM == KEY_UNIFORM) {
+        rku = load_round_keys<NR>(b.keys);
+        // the last FPNN_K2H_VKEYS round-key words in VGPRs (every lane the same word): the
+        // sessions' scalar state then leaves fewer SGPRs to spill into VGPR lanes
+#pragma unroll
+        // (not for wire frames' lane session, an A/B-only path: it would spill VGPRs)
+        for (int i = 4 * (NR + 1) - FPNN_K2H_VKEYS; i < 4 * (NR + 1); i++)
+            if (i >= 0 && !(SHIFT && LANES)) asm volatile("v_mov_b32 %0, %1" : "=v"(rku.k[i]) : "s"(rku.k[i]));
+    }
 
     // ---------------- quad session: K2q's cipher over perm[0, n_long) ----------------
     // Steps of 8 blocks; the next step's input words are loaded during this step's rounds.
