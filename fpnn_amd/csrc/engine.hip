@@ -2013,38 +2013,16 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
         for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
     }
-    // The frames themselves in that order (gathered on the host pool): the serial quota
-    // walk below then reads them sequentially -- in arrival order a stream's frames lie
-    // one stream-count apart, a cache and TLB miss each.  Opt-in (FPNN_AES_MAP_SORTED=1)
-    // until it is measured on the box; the default walks frames[order[i]].
-    static const bool sorted_copy = [] {
-        const char *x = getenv("FPNN_AES_MAP_SORTED");
-        return x && atoi(x) != 0;
-    }();
-    std::vector<fpnn_aes_host_frame> sfv;
-    const fpnn_aes_host_frame *sf = frames;  // sf[k] = frames[order[k]] (via ord)
-    const uint32_t *ord = order.data();
-    if (sorted_copy) {
-        sfv.resize(n);
-        const unsigned parts = n >= 16384 ? pool_of(e)->parts() : 1u;
-        pool_of(e)->run(parts, [&](unsigned p) {
-            const uint32_t a0 = (uint32_t)((uint64_t)n * p / parts), b0 = (uint32_t)((uint64_t)n * (p + 1) / parts);
-            for (uint32_t k = a0; k < b0; k++) sfv[k] = frames[order[k]];
-        });
-        sf = sfv.data();
-        ord = nullptr;
-    }
-    auto frame_at = [&](uint32_t k) -> const fpnn_aes_host_frame & { return ord ? sf[ord[k]] : sf[k]; };
     struct SSeg {
         uint32_t slot, first, nframes;
         uint64_t bytes;
     };
     std::vector<SSeg> segs;
     for (uint32_t i = 0; i < n;) {
-        const uint32_t slot = frame_at(i).key_slot;
+        const uint32_t slot = frames[order[i]].key_slot;
         uint32_t j = i;
         uint64_t bytes = 0;
-        while (j < n && frame_at(j).key_slot == slot) bytes += frame_at(j++).len;
+        while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
         if (bytes) segs.push_back({slot, i, j - i, bytes});
         i = j;
     }
@@ -2137,8 +2115,8 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             const uint64_t take = std::min(rem[s], quota);
             uint64_t took = 0;
             while (took < take) {
-                const uint32_t fidx = sg.first + fi[s];  // sorted position
-                const fpnn_aes_host_frame &f = frame_at(fidx);
+                const uint32_t fidx = order[sg.first + fi[s]];
+                const fpnn_aes_host_frame &f = frames[fidx];
                 const uint32_t part = (uint32_t)std::min<uint64_t>(f.len - fo[s], take - took);
                 if (part) pieces.push_back({fidx, fo[s], part});
                 took += part;
@@ -2185,7 +2163,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             long rs = -1, rd = -1;
             for (uint32_t q = a0; q < b0; q++) {
                 const Piece &pc = pieces[q];
-                const fpnn_aes_host_frame &f = frame_at(pc.frame);
+                const fpnn_aes_host_frame &f = frames[pc.frame];
                 const uintptr_t xs = (uintptr_t)f.src + pc.off, xd = (uintptr_t)f.dst + pc.off;
                 if (rs < 0 || xs < v.lo[rs] || xs + pc.len > v.hi[rs]) rs = v.find((const void *)xs, pc.len);
                 if (rd < 0 || xd < v.lo[rd] || xd + pc.len > v.hi[rd]) rd = v.find((const void *)xd, pc.len);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 session zn: S1's mapped stream path with the frames copied in slot order before
-# the quota walk (FPNN_AES_MAP_SORTED=1, opt-in) vs walking frames[order[i]] (=0, default):
+# the quota walk (FPNN_AES_MAP_SORTED=1 with tools/probe/mapped_stream_sorted_copy.patch applied) vs walking frames[order[i]] (=0):
 # host-frame tests, then S1 alternating in fresh processes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out/r03zn
 export TMPDIR=/tmp
