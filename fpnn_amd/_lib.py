@@ -92,6 +92,8 @@ SIGNATURES = {
     "fpnn_aes_engine_destroy": (C.c_int, [_vp]),
     "fpnn_aes_engine_sync": (C.c_int, [_vp]),
     "fpnn_aes_engine_stream": (_vp, [_vp]),
+    "fpnn_aes_thread_engine_device": (C.c_int, [C.c_uint32, C.c_int]),
+    "fpnn_aes_max_thread_engines": (C.c_int, [C.c_int]),
     "fpnn_aes_engine_reserve": (C.c_int, [_vp, C.c_uint64, C.c_uint64]),
     "fpnn_aes_keyset_create": (C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int, C.POINTER(_vp)]),
     "fpnn_aes_keyset_from_schedules": (C.c_int, [_vp, C.c_uint32, C.POINTER(Schedule), _vp, C.POINTER(_vp)]),

@@ -32,7 +32,8 @@ std::string describe(int rc) {
 int cfb(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16],
         size_t *p_num) {
     int rc;
-    fpnn_aes_engine *e = thread_engine(&rc);
+    const fpnn_aes::Lease lease = thread_engine(&rc);
+    fpnn_aes_engine *e = lease.engine();
     if (!e) return rc ? rc : FPNN_AES_ERR_NODEV;
     static_assert(sizeof(rijndael_context) == sizeof(fpnn_aes_schedule), "context layout");
     return fpnn_aes_cfb_host(e, reinterpret_cast<const fpnn_aes_schedule *>(ctx), encrypt ? 1 : 0, in, out, len, ivec,
@@ -46,11 +47,12 @@ void or_abort(int rc, const char *fn) {
     abort();
 }
 
-fpnn_aes_engine *engine_or_abort(const char *fn) {
+// the calling thread's engine, locked while the returned lease lives
+fpnn_aes::Lease engine_or_abort(const char *fn) {
     int rc;
-    fpnn_aes_engine *e = thread_engine(&rc);
-    if (!e) or_abort(rc ? rc : FPNN_AES_ERR_NODEV, fn);
-    return e;
+    fpnn_aes::Lease lease = thread_engine(&rc);
+    if (!lease.engine()) or_abort(rc ? rc : FPNN_AES_ERR_NODEV, fn);
+    return lease;
 }
 
 const fpnn_aes_schedule *sched(const rijndael_context *ctx) {
@@ -76,24 +78,24 @@ bool rijndael_setup_decrypt(rijndael_context *ctx, const uint8_t *key, size_t ke
 }
 
 void rijndael_encrypt(const rijndael_context *ctx, const uint8_t plain[16], uint8_t cipher[16]) {
-    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_encrypt"), sched(ctx), 1, plain, cipher, 1),
+    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_encrypt").engine(), sched(ctx), 1, plain, cipher, 1),
              "rijndael_encrypt");
 }
 
 void rijndael_decrypt(const rijndael_context *ctx, const uint8_t cipher[16], uint8_t plain[16]) {
-    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_decrypt"), sched(ctx), 0, cipher, plain, 1),
+    or_abort(fpnn_aes_ecb_host(engine_or_abort("rijndael_decrypt").engine(), sched(ctx), 0, cipher, plain, 1),
              "rijndael_decrypt");
 }
 
 void rijndael_cbc_encrypt(const rijndael_context *ctx, const uint8_t *plain, uint8_t *cipher, size_t len,
                           uint8_t ivec[16]) {
-    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_encrypt"), sched(ctx), 1, plain, cipher, len, ivec),
+    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_encrypt").engine(), sched(ctx), 1, plain, cipher, len, ivec),
              "rijndael_cbc_encrypt");
 }
 
 void rijndael_cbc_decrypt(const rijndael_context *ctx, const uint8_t *cipher, uint8_t *plain, size_t len,
                           uint8_t ivec[16]) {
-    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_decrypt"), sched(ctx), 0, cipher, plain, len, ivec),
+    or_abort(fpnn_aes_cbc_host(engine_or_abort("rijndael_cbc_decrypt").engine(), sched(ctx), 0, cipher, plain, len, ivec),
              "rijndael_cbc_decrypt");
 }
 
@@ -104,7 +106,7 @@ void rijndael_cfb_encrypt(const rijndael_context *ctx, bool encrypt, const uint8
 
 void rijndael_ofb_encrypt(const rijndael_context *ctx, const uint8_t *in, uint8_t *out, size_t len, uint8_t ivec[16],
                           size_t *p_num) {
-    or_abort(fpnn_aes_ofb_host(engine_or_abort("rijndael_ofb_encrypt"), sched(ctx), in, out, len, ivec, p_num),
+    or_abort(fpnn_aes_ofb_host(engine_or_abort("rijndael_ofb_encrypt").engine(), sched(ctx), in, out, len, ivec, p_num),
              "rijndael_ofb_encrypt");
 }
 
@@ -187,20 +189,19 @@ void EncryptorBatch::decrypt(Encryptor *enc, uint8_t *dest, uint8_t *src, int le
     add(enc, false, dest, src, len, nullptr);
 }
 
-// Persistent per-key-length table: slot per Encryptor serial, uploaded once
-// (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
-// like the table, so a flush never touches more than its own connections.
 namespace {
 
-// Serials retired by ~Encryptor / Encryptor::operator=, delivered to every live key
-// table (each drops them from its slot map at its next flush).
+// Serials retired by ~Encryptor / Encryptor::operator=, delivered only to the key tables
+// that hold a slot for them (each drops them from its slot map at its next flush): a
+// table's inbox never holds more serials than the table registered, however many
+// Encryptors the process creates and destroys.
 struct RetireInbox {
     std::vector<uint64_t> serials;
 };
 struct RetireRegistry {
     std::mutex mu;
-    std::vector<RetireInbox *> inboxes;
-    std::atomic<size_t> n{0};
+    std::unordered_map<uint64_t, std::vector<RetireInbox *>> held;  // serial -> tables holding it
+    std::atomic<size_t> n{0};                                       // live key tables
 };
 RetireRegistry &registry() {
     static RetireRegistry *r = new RetireRegistry();  // never destroyed: Encryptors may die at exit
@@ -218,14 +219,16 @@ void encryptor_retire(uint64_t serial) {
     RetireRegistry &r = registry();
     if (r.n.load(std::memory_order_acquire) == 0) return;  // no EncryptorBatch key table exists
     std::lock_guard<std::mutex> lk(r.mu);
-    for (RetireInbox *b : r.inboxes) b->serials.push_back(serial);
+    auto it = r.held.find(serial);
+    if (it == r.held.end()) return;
+    for (RetireInbox *b : it->second) b->serials.push_back(serial);
+    r.held.erase(it);
 }
 
 // Persistent per-key-length table: slot per Encryptor serial, uploaded once
 // (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
 // like the table, so a flush never touches more than its own connections.  The table
-// belongs to one engine, identified by its id (not its address, which a later thread's
-// engine may reuse).
+// belongs to one engine, identified by its id.
 struct EncryptorBatch::KeyTable {
     uint64_t engine_id = 0;
     fpnn_aes_keyset *ks = nullptr;
@@ -234,20 +237,29 @@ struct EncryptorBatch::KeyTable {
     std::vector<uint8_t> iv;
     std::vector<uint32_t> pos;
     RetireInbox inbox;
-    KeyTable() {
-        RetireRegistry &r = registry();
-        std::lock_guard<std::mutex> lk(r.mu);
-        r.inboxes.push_back(&inbox);
-        r.n.fetch_add(1, std::memory_order_release);
-    }
+    std::unordered_map<uint64_t, bool> registered;  // serials whose retirement reaches this inbox
+    KeyTable() { registry().n.fetch_add(1, std::memory_order_release); }
     ~KeyTable() {
         {
             RetireRegistry &r = registry();
             std::lock_guard<std::mutex> lk(r.mu);
-            r.inboxes.erase(std::find(r.inboxes.begin(), r.inboxes.end(), &inbox));
+            for (const auto &kv : registered) {
+                auto it = r.held.find(kv.first);
+                if (it == r.held.end()) continue;
+                auto &v = it->second;
+                v.erase(std::remove(v.begin(), v.end(), &inbox), v.end());
+                if (v.empty()) r.held.erase(it);
+            }
             r.n.fetch_sub(1, std::memory_order_release);
         }
         if (ks) fpnn_aes_keyset_destroy(ks);
+    }
+    // ask to hear of these serials' retirement (slots just handed out)
+    void watch(const std::vector<uint64_t> &serials) {
+        RetireRegistry &r = registry();
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (uint64_t sr : serials)
+            if (registered.emplace(sr, true).second) r.held[sr].push_back(&inbox);
     }
     // forget the slots of retired encryptors; true when most slots are dead, so the table
     // should start over (slots are handed out in order and never reused in place)
@@ -257,7 +269,10 @@ struct EncryptorBatch::KeyTable {
             std::lock_guard<std::mutex> lk(registry().mu);
             dead.swap(inbox.serials);
         }
-        for (uint64_t s : dead) slot.erase(s);
+        for (uint64_t sr : dead) {
+            slot.erase(sr);
+            registered.erase(sr);
+        }
         return next >= kTableMinReset && next > 2 * (uint32_t)slot.size();
     }
     static constexpr uint32_t kTableMinReset = 1024;
@@ -283,8 +298,9 @@ void EncryptorBatch::flush() {
     _bytes = 0;
     if (ops.empty()) return;
     int rc;
-    uint64_t eid = 0;
-    fpnn_aes_engine *e = thread_engine(&rc, &eid);
+    const fpnn_aes::Lease lease = thread_engine(&rc);
+    fpnn_aes_engine *e = lease.engine();
+    const uint64_t eid = lease.id();
     if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
     // group by (mode, direction, wire prefix, rounds); queue order is kept inside a group
     struct Group {
@@ -340,6 +356,7 @@ void EncryptorBatch::flush() {
         for (int attempt = 0;; attempt++) {
             std::vector<fpnn_aes_schedule> scheds;
             std::vector<uint8_t> ivs;
+            std::vector<uint64_t> fresh;
             const uint32_t first_new = t.next;
             members.clear();
             std::unordered_map<uint64_t, bool> seen;
@@ -351,6 +368,7 @@ void EncryptorBatch::flush() {
                                                             : static_cast<const PackageEncryptor *>(enc)->_ctx;
                     scheds.push_back(*reinterpret_cast<const fpnn_aes_schedule *>(&ctx));
                     ivs.insert(ivs.end(), enc->_iv, enc->_iv + 16);
+                    fresh.push_back(enc->_serial);
                     t.next++;
                 }
                 slots[k] = ins.first->second;
@@ -368,6 +386,7 @@ void EncryptorBatch::flush() {
                 tp = nullptr;
                 throw EncryptorError("EncryptorBatch: key table upload: " + describe(rc));
             }
+            t.watch(fresh);
             break;
         }
         std::vector<fpnn_aes_host_frame> frames(gr.idx.size());

@@ -737,6 +737,41 @@ int fpnn_aes_engine_sync(fpnn_aes_engine *e) {
 
 void *fpnn_aes_engine_stream(fpnn_aes_engine *e) { return e ? (void *)e->stream : nullptr; }
 
+// Devices the C++ classes' engine pool uses, in round-robin order (thread_engine.hpp).
+static int pool_devices(int ndev, int *d, int cap) {
+    int n = 0;
+    if (const char *v = getenv("FPNN_AES_DEVICES")) {
+        for (const char *p = v; *p && n < cap;) {
+            char *end = nullptr;
+            const long x = strtol(p, &end, 10);
+            if (end == p) {
+                p++;
+                continue;
+            }
+            if (x >= 0 && x < ndev) d[n++] = (int)x;
+            p = end;
+        }
+    } else if (const char *one = getenv("FPNN_AES_DEVICE")) {
+        const int x = atoi(one);
+        if (x >= 0 && x < ndev) d[n++] = x;
+    } else {
+        for (int i = 0; i < ndev && n < cap; i++) d[n++] = i;
+    }
+    return n;
+}
+
+int fpnn_aes_thread_engine_device(uint32_t k, int ndev) {
+    int d[256];
+    const int n = pool_devices(ndev, d, 256);
+    return n ? d[k % (uint32_t)n] : -1;
+}
+
+int fpnn_aes_max_thread_engines(int ndev) {
+    if (const char *v = getenv("FPNN_AES_MAX_ENGINES")) return std::max(1, atoi(v));
+    int d[256];
+    return std::max(1, 16 * pool_devices(ndev, d, 256));
+}
+
 int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t max_blocks) {
     if (!e) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);

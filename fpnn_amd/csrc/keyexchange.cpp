@@ -15,11 +15,13 @@
 
 namespace {
 
-fpnn_aes_engine *engine_or_throw() {
+// the calling thread's engine, locked while the returned lease lives
+fpnn_aes::Lease engine_or_throw() {
     int rc;
-    fpnn_aes_engine *e = fpnn_aes::thread_engine(&rc);
-    if (!e) throw fpnn::EncryptorError(std::string("fpnn_aes ECDH: no GPU engine: ") + fpnn_aes_strerror(rc));
-    return e;
+    fpnn_aes::Lease lease = fpnn_aes::thread_engine(&rc);
+    if (!lease.engine())
+        throw fpnn::EncryptorError(std::string("fpnn_aes ECDH: no GPU engine: ") + fpnn_aes_strerror(rc));
+    return lease;
 }
 
 void throw_if_error(int rc, const char *what) {
@@ -84,7 +86,7 @@ bool ECCKeyExchange::init(const std::string &curve, const std::string &privateKe
 bool ECCKeyExchange::calcKey(uint8_t *key, uint8_t *iv, int keylen, const std::string &peerPublicKey) {
     if (_curve < 0) return false;  // "ECC Private Key Config ERROR."
     if ((int)peerPublicKey.length() != _secertLen * 2) return false;
-    const int r = fpnn_ecdh_calc_key_host(engine_or_throw(), curve_name(_curve),
+    const int r = fpnn_ecdh_calc_key_host(engine_or_throw().engine(), curve_name(_curve),
                                           reinterpret_cast<const uint8_t *>(_privateKey.data()), _privateKey.size(),
                                           reinterpret_cast<const uint8_t *>(peerPublicKey.data()),
                                           peerPublicKey.size(), keylen, key, iv);
@@ -99,7 +101,7 @@ bool ECCKeyExchange::calcKeys(size_t count, const uint8_t *peerPublicKeys, int k
         memset(ok, 0, count);
         return true;
     }
-    const int rc = fpnn_ecdh_calc_keys_host(engine_or_throw(), _curve,
+    const int rc = fpnn_ecdh_calc_keys_host(engine_or_throw().engine(), _curve,
                                             reinterpret_cast<const uint8_t *>(_privateKey.data()), peerPublicKeys,
                                             (uint32_t)count, keylen, keys, ivs, ok);
     throw_if_error(rc, "calcKeys");
@@ -121,7 +123,8 @@ std::string ECCKeysMaker::publicKey(bool reGen) {
     if (_publicKey.empty() || reGen) {
         // uECC_make_key (core/micro-ecc/uECC.c:1004-1032): up to 64 draws of a private key
         // whose public key is not the point at infinity
-        fpnn_aes_engine *e = engine_or_throw();
+        const fpnn_aes::Lease lease = engine_or_throw();
+        fpnn_aes_engine *e = lease.engine();
         uint8_t priv[32], pub[64];
         for (int tries = 0; tries < 64; tries++) {
             if (!random_below_n(_curve, priv)) return std::string();  // "Gen public key & private key failed."

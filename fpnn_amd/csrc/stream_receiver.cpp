@@ -37,7 +37,10 @@ size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 }  // namespace
 
-// Device and pinned buffers of one batch, on the flushing thread's engine (grown, kept).
+// Device and pinned buffers of one batch, on the engine of the thread that flushes it
+// (grown, kept).  Pool engines are never destroyed (thread_engine.hpp), so the cached
+// stream stays valid when the batch is destroyed or flushed by another thread after the
+// first one has exited.  Plain hipMalloc / hipFree: no dependence on memory-pool support.
 struct StreamReceiverBatch::Dev {
     fpnn_aes_engine *e = nullptr;
     uint64_t eid = 0;
@@ -47,32 +50,29 @@ struct StreamReceiverBatch::Dev {
     size_t cap_d = 0, cap_h = 0;
 
     void release() {
-        if (st) (void)hipStreamSynchronize(st);
+        if (st) (void)hipStreamSynchronize(st);  // a pass that threw may have left copies queued
         for (fpnn_aes_keyset *&k : ks) {
             if (k) fpnn_aes_keyset_destroy(k);
             k = nullptr;
         }
-        if (d) (void)hipFreeAsync(d, st);
+        if (d) (void)hipFree(d);
         if (h) (void)hipHostFree(h);
-        if (st) (void)hipStreamSynchronize(st);
         d = h = nullptr;
         cap_d = cap_h = 0;
     }
     void reserve(size_t need) {
+        if (need > cap_d || need > cap_h) check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
         if (need > cap_d) {
             size_t n = std::max<size_t>(cap_d * 2, std::max<size_t>(need, 1 << 20));
-            if (d) check_hip(hipFreeAsync(d, st), "hipFreeAsync");  // behind the stream's earlier work
+            if (d) (void)hipFree(d);
             d = nullptr;
             cap_d = 0;
-            check_hip(hipMallocAsync(reinterpret_cast<void **>(&d), n, st), "hipMallocAsync");
+            check_hip(hipMalloc(reinterpret_cast<void **>(&d), n), "hipMalloc");
             cap_d = n;
         }
         if (need > cap_h) {
             size_t n = std::max<size_t>(cap_h * 2, std::max<size_t>(need, 1 << 20));
-            if (h) {
-                check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");  // the staging may still feed a copy
-                (void)hipHostFree(h);
-            }
+            if (h) (void)hipHostFree(h);
             h = nullptr;
             cap_h = 0;
             check_hip(hipHostMalloc(reinterpret_cast<void **>(&h), n, 0), "hipHostMalloc");
@@ -128,10 +128,11 @@ size_t StreamReceiverBatch::pending(int conn) const { return _conns.at(conn).car
 
 void StreamReceiverBatch::flush() {
     int rc;
-    uint64_t eid = 0;
-    fpnn_aes_engine *e = fpnn_aes::thread_engine(&rc, &eid);
+    const fpnn_aes::Lease lease = fpnn_aes::thread_engine(&rc);
+    fpnn_aes_engine *e = lease.engine();
+    const uint64_t eid = lease.id();
     if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
-    if (_dev && _dev->eid != eid) {  // flushed from another thread: that thread's engine
+    if (_dev && _dev->eid != eid) {  // flushed from a thread with another engine: move there
         _dev->release();
         delete _dev;
         _dev = nullptr;

@@ -74,6 +74,17 @@ void *fpnn_aes_engine_stream(fpnn_aes_engine *e);
  * max_blocks total 16-byte blocks, so later calls never allocate (graph-safe). */
 int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t max_blocks);
 
+/* Placement of the engines behind the C++ classes (Encryptor, EncryptorBatch,
+ * StreamReceiverBatch, ECCKeyExchange): one pool per process, engine k created on the
+ * device returned here for (k, ndev = fpnn_aes_device_count) -- k % ndev, or the k-th
+ * entry (cyclically) of the comma list FPNN_AES_DEVICES, or FPNN_AES_DEVICE alone;
+ * -1 when no device is usable.  Pure functions of their arguments and the environment
+ * (no HIP call), so the plan can be checked without a GPU. */
+int fpnn_aes_thread_engine_device(uint32_t k, int ndev);
+/* Engines the pool creates before calling threads start to share one (calls on a shared
+ * engine serialise): FPNN_AES_MAX_ENGINES, default 16 per usable device, at least 1. */
+int fpnn_aes_max_thread_engines(int ndev);
+
 /* ---- key sets: the per-connection (key, IV) table on the device -------------- */
 /* A key set holds `count` expanded keys of ONE key length plus one 16-byte IV each
  * (the connection IV of package mode, core/Encryptor.h:14).  keys: count*keylen

@@ -284,6 +284,38 @@ def gen_framing_cases(ref: Oracle):
                       "fed over a socketpair in 1-, 7- and 65536-byte pieces", "cases": cases}
 
 
+ECHO_REF = os.path.join(HERE, "_ref", "io_echo_ref")
+PERCALL_REF = os.path.join(HERE, "_ref", "percall_ref")
+# (mode, keylen, quests, payload bytes, window): C1 itself first (BASELINE.json configs[0])
+C1_ECHO_CASES = [("package", 32, 10000, 1024, 1), ("package", 16, 400, 1, 1), ("package", 32, 400, 15, 4),
+                 ("package", 24, 300, 4000, 2), ("stream", 32, 2000, 1024, 8), ("stream", 16, 500, 333, 3),
+                 ("stream", 32, 300, 17, 1)]
+
+
+def gen_c1_cases():
+    """Config C1 through the reference's own IO plumbing (oracle/io_echo.cpp built on the
+    reference's core/IOBuffer.cpp SendBuffer, EncryptedPackageReceiver /
+    EncryptedStreamReceiver and core/Encryptor.cpp + base/rijndael.c: `make -C oracle echo`):
+    an encrypted echo over loopback TCP, the wire checksums of both directions per case; and
+    C1's per-call shape (oracle/percall.cpp, `make -C oracle percall`): the checksum of 10 000
+    PackageEncryptor::encrypt / encrypt(std::string*) outputs of 1 KiB."""
+    import subprocess
+    cases = []
+    for mode, kl, n, plen, win in C1_ECHO_CASES:
+        out = subprocess.run([ECHO_REF, "1" if mode == "stream" else "0", str(kl), str(n), str(plen), str(win)],
+                             capture_output=True, text=True, check=True, timeout=300).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+        assert d["answers_ok"], d
+        cases.append({k: d[k] for k in ("mode", "keylen", "quests", "payload", "window", "wire_c2s_bytes",
+                                        "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv")})
+        print("  echo", cases[-1])
+    pc = json.loads(subprocess.run([PERCALL_REF, "10000", "1024"], capture_output=True, text=True, check=True,
+                                   timeout=300).stdout.strip().splitlines()[-1])
+    return {"source": "reference SendBuffer + encrypted receivers (oracle/_ref/io_echo_ref) and reference "
+                      "PackageEncryptor per call (oracle/_ref/percall_ref)",
+            "echo": cases, "percall": {"frames": pc["frames"], "len": pc["len"], "checksum": pc["checksum"]}}
+
+
 ECDH_REF = os.path.join(HERE, "_ref", "ecdh_ref")
 
 
@@ -487,6 +519,7 @@ def main():
     ap.add_argument("--modes-only", action="store_true", help="only (re)write modes_cases.json")
     ap.add_argument("--framing-only", action="store_true", help="only (re)write framing_cases.json")
     ap.add_argument("--ecdh-only", action="store_true", help="only (re)write ecdh_cases.json")
+    ap.add_argument("--c1-only", action="store_true", help="only (re)write c1_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -506,6 +539,9 @@ def main():
     if args.ecdh_only:
         dump("ecdh_cases.json", gen_ecdh_cases())
         return
+    if args.c1_only:
+        dump("c1_cases.json", gen_c1_cases())
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -519,6 +555,7 @@ def main():
     dump("modes_cases.json", gen_modes_cases(ref))
     dump("framing_cases.json", gen_framing_cases(ref))
     dump("ecdh_cases.json", gen_ecdh_cases())
+    dump("c1_cases.json", gen_c1_cases())
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

@@ -37,3 +37,24 @@ def expected(case):
         raws.append(bytes.fromhex(ev["raw"]) if ev["fetch"] else None)
         at += pre + ev["total"]
     return frames, _EXPECT[case["expect"]], at, raws
+
+
+def run_receiver(exe, case, piece):
+    """Feed one fixture's wire to a receiver driver built from oracle/framing_ref.cpp
+    (oracle/_ref/framing_ref: the reference's receivers on the reference Encryptor;
+    oracle/_ref/framing_dropin: the same receivers compiled unchanged against
+    include/Encryptor.h on libfpnn_aes.so) -> (frame events, end event)."""
+    import struct
+    import subprocess
+    import tempfile
+    key, iv, wire = bytes.fromhex(case["key"]), bytes.fromhex(case["iv"]), bytes.fromhex(case["wire"])
+    with tempfile.TemporaryDirectory() as d:
+        cin, cout = os.path.join(d, "case.bin"), os.path.join(d, "out.jsonl")
+        with open(cin, "wb") as f:
+            f.write(b"FRG1" + struct.pack("<II", 0 if case["mode"] == "package" else 1, len(key)) + key + iv
+                    + struct.pack("<iIQ", case["max_len"], piece, len(wire)) + wire)
+        subprocess.run([exe, cin, cout], check=True, timeout=120, stdout=subprocess.DEVNULL)
+        with open(cout) as f:
+            lines = [json.loads(x) for x in f]
+    assert lines and "end" in lines[-1], lines
+    return lines[:-1], lines[-1]

@@ -217,3 +217,29 @@ def test_rijndael_surface_links_without_reference_object(tmp_path):
         assert name in undef, f"{name} not imported"
         assert name not in defined_in_exe, f"{name} defined in the program itself"
         assert name in lib_syms, f"{name} not exported by libfpnn_aes.so"
+
+
+def _plan(env, k, ndev):
+    """fpnn_aes_thread_engine_device / _max_thread_engines in a child process with `env`
+    (the library reads the environment on each call; a child keeps this one clean)."""
+    code = ("import sys; sys.path.insert(0, %r); import fpnn_amd; "
+            "print([fpnn_amd.lib.fpnn_aes_thread_engine_device(i, %d) for i in range(%d)], "
+            "fpnn_amd.lib.fpnn_aes_max_thread_engines(%d))" % (ROOT, ndev, k, ndev))
+    e = {kk: v for kk, v in os.environ.items() if not kk.startswith("FPNN_AES_")}
+    e.update(env)
+    out = subprocess.run(["python", "-c", code], env=e, capture_output=True, text=True, check=True).stdout
+    devs, cap = out.strip().rsplit(" ", 1)
+    return eval(devs), int(cap)
+
+
+def test_thread_engine_device_plan():
+    """The C++ classes' engine pool (thread_engine.hpp): engine k on device k % ndev, or
+    cyclically over FPNN_AES_DEVICES, or all on FPNN_AES_DEVICE; -1 without devices; at
+    most 16 engines per device before threads share."""
+    assert _plan({}, 10, 8) == ([0, 1, 2, 3, 4, 5, 6, 7, 0, 1], 128)
+    assert _plan({}, 3, 1) == ([0, 0, 0], 16)
+    assert _plan({}, 2, 0) == ([-1, -1], 1)
+    assert _plan({"FPNN_AES_DEVICES": "3,5,9"}, 5, 8) == ([3, 5, 3, 5, 3], 32)  # 9 is not a device
+    assert _plan({"FPNN_AES_DEVICE": "2"}, 3, 4) == ([2, 2, 2], 16)
+    assert _plan({"FPNN_AES_DEVICE": "7"}, 2, 4) == ([-1, -1], 1)
+    assert _plan({"FPNN_AES_MAX_ENGINES": "3"}, 4, 8)[1] == 3

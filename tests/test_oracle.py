@@ -258,3 +258,48 @@ def test_ecdh_restatement_vs_reference():
             assert (int(ok), key.hex(), iv.hex()) == (s["ok"], s["key"], s["iv"]), (cv["curve"], s)
             fails += 1 - s["ok"]
     assert fails >= 4 * 5  # zero point, short peer, bad keylen, private 1, short private per curve
+
+
+def _ref_exe(name):
+    p = os.path.join(ROOT, "oracle", "_ref", name)
+    if not os.access(p, os.X_OK):
+        pytest.skip(f"oracle/_ref/{name} not built (needs /root/reference)")
+    return p
+
+
+def test_c1_echo_reference_reproduces_fixture():
+    """oracle/_ref/io_echo_ref (the reference's SendBuffer + encrypted receivers on its own
+    Encryptor, C1's encrypted echo) reproduces tests/golden/c1_cases.json -- the fixture the
+    drop-in build is checked against on the GPU (tests/test_gpu_dropin.py)."""
+    import json
+    import subprocess
+    exe = _ref_exe("io_echo_ref")
+    with open(os.path.join(ROOT, "tests", "golden", "c1_cases.json")) as f:
+        cases = json.load(f)["echo"]
+    for g in cases[1:]:  # the small cases (C1 itself is 10 000 quests)
+        out = subprocess.run([exe, "1" if g["mode"] == "stream" else "0", str(g["keylen"]), str(g["quests"]),
+                              str(g["payload"]), str(g["window"])], capture_output=True, text=True, check=True,
+                             timeout=120).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+        assert d["answers_ok"]
+        assert [d[k] for k in ("wire_c2s_fnv", "wire_s2c_fnv")] == [g["wire_c2s_fnv"], g["wire_s2c_fnv"]], g
+
+
+def test_dropin_builds_bind_the_cipher_to_libfpnn_aes():
+    """The drop-in builds of the reference callers (oracle/Makefile `dropin`) define no
+    cipher of their own: every Encryptor method and rijndael_* call they make is an
+    undefined symbol resolved from libfpnn_aes.so (core/Encryptor.cpp and base/rijndael.c
+    are not linked), and the receivers' objects were compiled against include/Encryptor.h
+    (PackageEncryptor carries this header's _ctx member: the layout differs from
+    core/Encryptor.h, so a wrong header would not link against these symbols consistently)."""
+    import subprocess
+    for name in ("framing_dropin", "io_echo_dropin"):
+        exe = _ref_exe(name)
+        ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
+        assert "libfpnn_aes.so" in ldd, ldd
+        syms = subprocess.run(["nm", "-C", exe], capture_output=True, text=True, check=True).stdout.splitlines()
+        defined = [s for s in syms if " T " in s or " t " in s]
+        assert not [s for s in defined if "rijndael_" in s or "Encryptor::encrypt" in s or "Encryptor::decrypt" in s]
+        undef = [s.split(" U ")[-1] for s in syms if " U " in s]
+        assert "fpnn::encryptor_serial()" in undef  # only include/Encryptor.h's constructor calls this
+        assert any("fpnn::PackageEncryptor::decrypt" in u for u in undef)

@@ -1,0 +1,84 @@
+#!/bin/bash
+# One parametrised GPU-box session (replaces the per-session one-off scripts of rounds 1-3).
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# Steps (each under its own time limit; output in gpurun_out/<tag>/<step>.log; the first
+# crash / timeout / abort ends the session, a plain test failure (rc 1) does not):
+#   smoke            __graft_entry__.smoke()
+#   tests            the whole GPU suite (pytest -m gpu, incl. slow)
+#   tests_fast       pytest -m "gpu and not slow"
+#   tests:<expr>     pytest -m gpu -k <expr>
+#   bench            python bench.py (the contract line)
+#   bench_trace      bench.py under rocprofv3 --kernel-trace --stats (profiles the line's kernels)
+#   bench_pmc        bench.py under the four PMC passes (HBM bytes, LDS, VALU, waits)
+#   configs          tools/bench_configs.py --no-host, every device config (steady-state medians)
+#   configs:<list>   the same for a comma list, e.g. configs:C4,R1
+#   host             tools/bench_configs.py --configs C2,S1 with the host / PCIe legs
+#   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
+#   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
+#   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
+#   prof:<cfg>       rocprofv3 trace + 4 PMC passes of one bench_configs config (or ECDH)
+#   ecdh             tools/bench_ecdh.py
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+PASSES="FETCH_SIZE|WRITE_SIZE|SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_LDS,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES|SQ_WAIT_INST_LDS,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,GRBM_GUI_ACTIVE"
+
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; grep -E '^\{|passed|failed|error' "$OUT/$name.log" | tail -3 | cut -c1-600
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -8 "$OUT/$name.log"; echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+
+pmc_passes() {  # pmc_passes <dir> <kernel regex> <cmd...>
+  local dir=$1 rx=$2; shift 2
+  mkdir -p "$OUT/$dir"
+  run "$dir/trace" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$dir/trace" -o run -- "$@"
+  local i=0 g
+  IFS="|" read -ra PG <<< "$PASSES"
+  for g in "${PG[@]}"; do
+    i=$((i+1))
+    run "$dir/pmc$i" 120 rocprofv3 --kernel-trace --pmc ${g//,/ } --kernel-include-regex "$rx" --output-format csv \
+      -d "$OUT/$dir/pmc$i" -o run -- "$@"
+  done
+}
+
+percall_exe() {
+  g++ -std=c++11 -O2 -I include oracle/percall.cpp -o "$OUT/percall_gpu" -L fpnn_amd -lfpnn_aes \
+    -Wl,-rpath,"$PWD/fpnn_amd" || exit 3
+}
+
+for step in "$@"; do
+  case "$step" in
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 1100 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread ;;
+    tests_fast) run tests_fast 600 python -u -m pytest tests -q -m "gpu and not slow" -x --timeout 120 --timeout-method thread ;;
+    tests:*) run "tests_k" 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread -k "${step#tests:}" ;;
+    bench) run bench 300 python -u bench.py ;;
+    bench_trace) mkdir -p "$OUT/bench_prof"
+      run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_prof/trace" -o run -- \
+        python3 bench.py --no-cpu-baseline ;;
+    bench_pmc) pmc_passes bench_prof 'cfb_' python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
+    configs) run configs 700 python -u tools/bench_configs.py --reps 3 --no-host ;;
+    configs:*) run "configs_${step#configs:}" 600 python -u tools/bench_configs.py --reps 3 --no-host --configs "${step#configs:}" ;;
+    host) run host 600 python -u tools/bench_configs.py --reps 3 --configs C2,S1 ;;
+    timer) run timer 300 python -u tools/timer_probe.py ;;
+    percall) run percall 300 python -u tools/bench_percall.py ;;
+    percall_trace) percall_exe
+      run percall_trace 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv \
+        -d "$OUT/percall_prof" -o run -- "$OUT/percall_gpu" 1000 1024 ;;
+    prof:ECDH) pmc_passes prof_ECDH 'k_ecdh' python3 tools/bench_ecdh.py --curves secp256k1 --no-cpu --reps 3 ;;
+    prof:*) c=${step#prof:}; pmc_passes "prof_$c" 'cfb_' python3 tools/bench_configs.py --configs "$c" --no-host --reps 3 ;;
+    ecdh) run ecdh 300 python -u tools/bench_ecdh.py ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session $TAG done $(date +%T)"
