@@ -228,6 +228,11 @@ struct fpnn_aes_engine {
     uint64_t cap_hsstate = 0;
     bool pools = false;            // stream-ordered allocation (hipMallocAsync) for grow()
     std::vector<void *> deferred;  // grown-out scratch awaiting an idle stream (no pools)
+    // K0 (k_small.hip): pinned staging of the small synchronous calls, its device view,
+    // and the sequence number the kernel stores when a call is done
+    uint8_t *h_small = nullptr;
+    uint8_t *d_small = nullptr;
+    uint32_t small_seq = 0;
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
@@ -699,6 +704,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_small) (void)hipHostFree(e->h_small);
     if (e->h_sstate) (void)hipHostFree(e->h_sstate);
     for (auto &v : e->ev)
         for (auto &p : v) {
@@ -1107,6 +1113,68 @@ hipError_t sync_spin(hipStream_t st) {
     return hipStreamSynchronize(st);
 }
 
+// K0 for calls of up to kSmallMaxBytes (FPNN_AES_SMALL=0 routes them through the batch
+// kernels, the A/B baseline).
+bool small_enabled() {
+    static const bool on = [] {
+        const char *v = getenv("FPNN_AES_SMALL");
+        return !v || atoi(v) != 0;
+    }();
+    return on;
+}
+
+// One small synchronous CFB call through K0 (k_small.hip): the bytes go into pinned
+// staging, one launch ciphers them in place there, and the kernel's sequence-number store
+// says the results are in.  The wait spins on that word; after 20 ms it falls back to the
+// stream sync, which also reports a kernel that failed.
+constexpr uint64_t kSmallStage = kSmallBodyAt + kSmallMaxBytes + 64;
+int cfb_small(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, const uint8_t *in, uint8_t *out,
+              size_t len, uint8_t ivec[16], size_t *p_num) {
+    DeviceGuard g(e->device);
+    if (!e->h_small) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_small), kSmallStage, hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&e->d_small), e->h_small, 0));
+    }
+    const uint32_t pos = (uint32_t)*p_num;
+    const uint32_t head = pos ? (uint32_t)std::min<size_t>(len, 16 - pos) : 0u;
+    memcpy(e->h_small + kSmallBodyAt - head, in, len);
+    SmallArgs a;
+    a.io = e->d_small;
+    a.len = (uint32_t)len;
+    a.head = head;
+    a.pos = pos;
+    a.seq = ++e->small_seq;
+    memcpy(&a.iv, ivec, 16);
+    for (int k = 0; k < 4 * (ctx->nrounds + 1); k++) a.rk[k] = bswap32(ctx->rk[k]);
+    a.t0le = t0le_of(e);
+    a.state = reinterpret_cast<uint32_t *>(e->d_small + kSmallStage - 32);
+    volatile uint32_t *hstate = reinterpret_cast<volatile uint32_t *>(e->h_small + kSmallStage - 32);
+    const int which = encrypt ? FPNN_AES_K_ENCRYPT : FPNN_AES_K_DECRYPT;
+    EventPair *ev;
+    if (int rc = timing_begin(e, which, &ev)) return rc;
+    HIP_TRY(launch_cfb_single(a, ctx->nrounds, encrypt, e->stream));
+    if (int rc = timing_end(e, ev, which)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0; __atomic_load_n(&hstate[5], __ATOMIC_ACQUIRE) != a.seq; spins++) {
+        __builtin_ia32_pause();
+        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+            HIP_TRY(hipStreamSynchronize(e->stream));
+            if (__atomic_load_n(&hstate[5], __ATOMIC_ACQUIRE) != a.seq) {
+                g_last_error = "small-call kernel finished without publishing its result";
+                return FPNN_AES_ERR_HIP;
+            }
+            break;
+        }
+    }
+    memcpy(out, e->h_small + kSmallBodyAt - head, len);
+    for (int i = 0; i < 4; i++) {
+        const uint32_t w = hstate[i];
+        memcpy(ivec + 4 * i, &w, 4);
+    }
+    *p_num = hstate[4];
+    return FPNN_AES_OK;
+}
+
 // One synchronous rijndael.h call in the non-CFB modes (k_modes.hip).  Staging:
 // [DevKey 272][iv 16][pos 4 | pad 12][in: in_bytes, 16-padded][out: out_bytes]
 int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const uint8_t *in, uint64_t in_copy,
@@ -1192,6 +1260,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     if (*p_num > 15) return FPNN_AES_ERR_ARG;
     if (len == 0) return FPNN_AES_OK;
     if (len > 0xffffffffull) return FPNN_AES_ERR_RANGE;
+    if (len <= kSmallMaxBytes && small_enabled()) return cfb_small(e, ctx, encrypt != 0, in, out, len, ivec, p_num);
     DeviceGuard g(e->device);
     // staging layout: [DevKey 272][iv 16][pos 4 | pad 12][payload len] ... [out len]
     const uint64_t hdr = sizeof(DevKey) + 32;

@@ -189,6 +189,24 @@ struct ModeArgs {
     const uint8_t *isbox;
 };
 hipError_t launch_block_modes(const ModeArgs &a, int nrounds, int mode, int num_cus, hipStream_t st);
+// K0 (k_small.hip): one synchronous CFB call of up to kSmallMaxBytes bytes, in place in
+// pinned host staging: body at io + kSmallBodyAt (16-aligned), the head's bytes (pos != 0)
+// right before it.  state (pinned): [ivec 16 B][pos u32][seq u32], the kernel stores seq
+// last (system-scope release) once everything else is visible to the host.
+constexpr uint32_t kSmallMaxBytes = 16384;
+constexpr uint32_t kSmallBodyAt = 32;
+struct SmallArgs {
+    uint8_t *io;
+    uint32_t len;   // bytes in the call (head + body)
+    uint32_t head;  // min(len, (16 - pos) % 16): bytes finishing the current keystream block
+    uint32_t pos;   // *p_num on entry
+    uint32_t seq;
+    uint4 iv;       // ivec on entry
+    uint32_t rk[60];
+    const uint32_t *t0le;
+    uint32_t *state;
+};
+hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
 // Host-mapped frame moves: a job copies n segments, segment i from address sbase + soff[i]

@@ -95,6 +95,35 @@ def test_golden_cfb_cases_host_path(engine, golden):
         assert (out.hex(), iv.hex(), pos) == (c["out"], c["iv_out"], c["pos_out"])
 
 
+@pytest.mark.parametrize("keylen", [16, 24, 32])
+def test_small_call_kernel_vs_oracle(engine, oracle, keylen):
+    """K0 (k_small.hip), the single-call kernel behind every fpnn_aes_cfb_host call of up to
+    16 KiB (the drop-in Encryptor's per-call path): random lengths around every edge (1,
+    15/16/17, one block short of / at / one past the 16 KiB limit, which takes the batch
+    kernels), random entry positions, both directions, and chains of calls carrying
+    (ivec, pos) as StreamEncryptor does -- byte-exact against the oracle's
+    rijndael_cfb_encrypt, output and state."""
+    import fpnn_amd
+    rng = np.random.default_rng(404 + keylen)
+    key = rng.bytes(keylen)
+    ctx = fpnn_amd.setup_encrypt(key)
+    lens = [1, 2, 15, 16, 17, 31, 32, 33, 1023, 1024, 1025, 4096, 16368, 16383, 16384, 16385, 20000]
+    lens += [int(x) for x in rng.integers(1, 16384, 24)]
+    for enc in (True, False):
+        iv_g, pos_g = rng.bytes(16), 0
+        iv_o, pos_o = iv_g, 0
+        for n in lens:
+            data = rng.bytes(n)
+            pos_in = int(rng.integers(0, 16)) if rng.random() < 0.3 else None
+            if pos_in is not None:  # a fresh entry state, else carry the chain's
+                iv_g = iv_o = rng.bytes(16)
+                pos_g = pos_o = pos_in
+            out, iv_g, pos_g = engine.cfb(ctx, enc, data, iv_g, pos_g)
+            exp, iv_o, pos_o = oracle.cfb(key, enc, data, iv_o, pos_o)
+            assert out == exp, (enc, n)
+            assert (iv_g, pos_g) == (iv_o, pos_o), (enc, n)
+
+
 def test_golden_cfb_cases_stream_batch(engine, golden):
     """The same cases as ONE device stream batch: each case is a stream segment with its
     own key, carried (iv, pos) in and out (fpnn_aes_stream_encrypt/decrypt)."""
