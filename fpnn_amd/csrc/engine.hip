@@ -396,8 +396,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // Few chains (fewer than the lanes of a full chip) or ragged lengths: one quad per
     // chain (K2c); otherwise one lane per chain with 8-block chunks (K2).
     const uint64_t full_chip = (uint64_t)e->num_cus * kThreads;
-    const bool coop = e->variant.coop == 1 || (e->variant.coop == -1 && (b->count < full_chip || b->len != nullptr));
-    if (coop) {
+    if (b->count < full_chip || b->len != nullptr) {
         const uint64_t lanes = 4 * b->count;
         int threads = 64;
         while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
@@ -413,21 +412,20 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.perm = e->d_perm;
         }
         EventPair *ev;
-        // ragged and more chains than quads: a work queue balances them (with fewer
-        // chains every quad holds at most one and the grid stride is cheaper)
-        const bool queue = b->len && (e->variant.queue == 2 || (e->variant.queue == 1 && lanes > full_chip));
-        if (queue && (rc = grow(e, e->d_next, e->cap_next, 2))) return rc;
-        if (queue && e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
-        const bool hybrid = queue && e->variant.hybrid && b->count > 1;
+        // ragged with more chains than quads: K2h (short chains one per lane, the longest
+        // on quads, both from work queues); with fewer every quad holds at most one chain
+        // and K2c's grid stride is cheaper
+        const bool hybrid = b->len && b->count > 1 && (lanes > full_chip || e->variant.hyb_force);
+        if (hybrid && (rc = grow(e, e->d_next, e->cap_next, 2))) return rc;
         if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
         if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
+            k.flags |= F_ALIGN_CHUNKS;
             HybridArgs h;
             h.ctr = e->d_next;
             h.buckets = e->d_buckets;
             h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
             h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
-            h.qflags = (uint32_t)e->variant.hyb_qflags;
             h.sink = e->d_sink;
             if ((b->flags & FPNN_AES_F_WIRE_PREFIX) && !e->variant.hyb_wire_lanes) {
                 // wire frames (htole32(len) || C): every chain on quads -- the lane session's
@@ -435,26 +433,25 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
                 h.long_bucket = 127;
                 h.quad_waves = 16;
             }
-            HIP_TRY(launch_encrypt_hybrid(k, h, b->keys->nrounds, km, stream, e->variant.fence, e->num_cus, e->stream));
-        } else if (queue)
-            HIP_TRY(launch_encrypt_queue(k, b->keys->nrounds, km, stream, grid, threads, e->d_next, e->stream));
-        else
+            HIP_TRY(launch_encrypt_hybrid(k, h, b->keys->nrounds, km, stream, e->num_cus, e->stream));
+        } else {
             HIP_TRY(launch_encrypt_coop(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
+        }
         return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
     }
     // One lane per chain.  Workgroup size: the smallest power of two (>= one wave) that
     // still spreads the chains over every CU -- with few chains (C3: 4096 streams) a
     // 1024-thread workgroup would pack them onto a handful of CUs whose LDS they then
     // saturate, while the rest of the chip idles.
-    const uint64_t slots = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
+    const uint64_t slots = (uint64_t)e->num_cus;
     int threads = 64;
     while (threads < kThreads && (uint64_t)threads * slots < b->count) threads *= 2;
     const uint64_t want = (b->count + threads - 1) / threads;
     const int grid = (int)(want < slots ? (want ? want : 1) : slots);
-    if (e->variant.enc_align) k.flags |= F_ALIGN_CHUNKS;
+    k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, e->variant, layout, km, stream, grid, threads, e->stream));
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
     return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
 }
 
@@ -491,12 +488,12 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         const uint64_t nb = ((uint64_t)b->uniform_len + 15) >> 4;
         const uint64_t total = nb * b->count;
         if (nb > 0 && total < (1ull << 32) && nb > 1) {
-            layout = (b->uniform_len & 15) == 0 && e->variant.dec_full ? LAYOUT_FULL : LAYOUT_UNIFORM;
+            layout = (b->uniform_len & 15) == 0 ? LAYOUT_FULL : LAYOUT_UNIFORM;
             k.total_blocks = total;
             k.nb_uniform = (uint32_t)nb;
             k.magic = magic_for((uint32_t)nb);
         }
-    } else if (!stream && km == KEY_LANE && !b->in_off && !b->out_off && !b->len && e->variant.dec_dense &&
+    } else if (!stream && km == KEY_LANE && !b->in_off && !b->out_off && !b->len &&
                b->uniform_len >= 32 && b->uniform_len % 16 == 0 && b->stride == b->uniform_len) {
         // dense whole-block packets, one key slot each: K1d with a wave-uniform key per
         // step when packets are whole 64-block chunks (C5), K1k with per-lane keys
@@ -539,9 +536,8 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // in place (in == out, identical offsets: fpnn_aes.h) the predecessor blocks of the
         // waves' first chunks are saved by a plan launch before any wave writes; otherwise
         // every wave finds its own at the start of the decrypt kernel (one launch fewer)
-        const bool plan_launch = inplace || e->variant.k1r_plan;
-        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, e->d_sink, e->variant.fence,
-                                      plan_launch, grid, e->stream));
+        HIP_TRY(launch_decrypt_ragged(k, b->keys->nrounds, km, stream, e->d_plan, e->d_sink, inplace, grid,
+                                      e->stream));
         return timing_end(e, ev, FPNN_AES_K_DECRYPT);
     }
     EventPair *ev = nullptr;
@@ -552,10 +548,10 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         k.boundary = e->d_boundary;
     }
     const uint64_t want = (nchunks + 63) / 64;  // 16 waves per workgroup x up to 4 chunks per wave step
-    const uint64_t cap = (uint64_t)e->num_cus * blocks_per_cu(e->variant, km);
+    const uint64_t cap = (uint64_t)e->num_cus;
     const int grid = (int)(want < cap ? (want ? want : 1) : cap);
     if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
-    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, e->variant, layout, km, inplace, grid, e->stream));
+    HIP_TRY(launch_decrypt_blocks(k, b->keys->nrounds, layout, km, inplace, grid, e->stream));
     return timing_end(e, ev, FPNN_AES_K_DECRYPT);
 }
 
@@ -632,23 +628,11 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     fpnn_aes_engine *e = new fpnn_aes_engine();
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
-    if (const char *v = getenv("FPNN_AES_TABLES")) e->variant.tables = atoi(v) == 2 ? 2 : 4;
-    if (const char *v = getenv("FPNN_AES_QUEUE")) e->variant.queue = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
-    if (const char *v = getenv("FPNN_AES_HYBRID")) e->variant.hybrid = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_FENCE")) e->variant.fence = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K1R_PLAN")) e->variant.k1r_plan = atoi(v) != 0;
+    // K2h split (tests set these so that small batches exercise each session)
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_HYB_QFLAGS")) e->variant.hyb_qflags = atoi(v);
-    if (const char *v = getenv("FPNN_AES_COOP")) e->variant.coop = atoi(v) < 0 ? -1 : (atoi(v) ? 1 : 0);
-    if (const char *v = getenv("FPNN_AES_DEC_FULL")) e->variant.dec_full = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_DEC_DENSE")) e->variant.dec_dense = atoi(v) < 0 ? 0 : atoi(v) > 2 ? 2 : atoi(v);
-    if (const char *v = getenv("FPNN_AES_ENC_ALIGN")) e->variant.enc_align = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_ENC_CHUNK")) {
-        const int c = atoi(v);
-        e->variant.enc_chunk = (c == 1 || c == 4) ? c : 8;
-    }
+    if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
     {  // stream-ordered scratch allocation; the pool keeps freed memory for reuse
         int pools = 0;
         const char *v = getenv("FPNN_AES_POOLS");
@@ -1093,26 +1077,6 @@ void devkey_from_schedule(DevKey *hk, const fpnn_aes_schedule *ctx) {
 
 bool valid_rounds(int nr) { return nr == 10 || nr == 12 || nr == 14; }
 
-// Synchronous per-call forms (the drop-in Encryptor / rijndael.h / calcKey calls) wait for
-// the engine stream with the blocking hipStreamSynchronize.  FPNN_AES_SYNC_SPIN=1 polls
-// hipStreamQuery for up to 2 ms first: measured slower (1 KiB per-call decrypt 43-50 vs
-// 32-33 us, encrypt 79 vs 73 us; tools/gpu_r03v.sh), so it is an A/B switch only.
-hipError_t sync_spin(hipStream_t st) {
-    static const bool on = [] {
-        const char *v = getenv("FPNN_AES_SYNC_SPIN");
-        return v && atoi(v) != 0;
-    }();
-    if (on) {
-        const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-            const hipError_t q = hipStreamQuery(st);
-            if (q != hipErrorNotReady) return q;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-        }
-    }
-    return hipStreamSynchronize(st);
-}
-
 // K0 for calls of up to kSmallMaxBytes (FPNN_AES_SMALL=0 routes them through the batch
 // kernels, the A/B baseline).
 bool small_enabled() {
@@ -1207,7 +1171,7 @@ int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const
     e->last_kernel[FPNN_AES_K_ENCRYPT] = last_launched();
     HIP_TRY(hipMemcpyAsync(h_iv, a.iv, 32, hipMemcpyDeviceToHost, e->stream));
     if (out_copy) HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + ipad, a.out, out_copy, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(sync_spin(e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     if (out_copy) memcpy(out, e->h_stage + hdr + ipad, out_copy);
     if (ivec && mode != MODE_CBC_DEC) memcpy(ivec, h_iv, 16);
     if (p_num) *p_num = *h_pos;
@@ -1298,7 +1262,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h_iv, d_iv, 32, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + pay, e->d_stage + hdr + pay, len, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(sync_spin(e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     memcpy(out, e->h_stage + hdr + pay, len);
     memcpy(ivec, h_iv, 16);
     *p_num = *h_pos;
@@ -1826,13 +1790,6 @@ int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
 // written by the host threads during step t), so the move stream never waits for a copy.
 // Events hand each chunk between the two streams.  The host threads only write
 // descriptors.
-// FPNN_AES_MAP_PREP_FIRST=1: the mapped pipelines prepare chunk t + 1's descriptors before
-// queueing the cipher of chunk t - 1 (the round-2 order; A/B only)
-bool map_prep_first() {
-    const char *v = getenv("FPNN_AES_MAP_PREP_FIRST");
-    return v && atoi(v) != 0;
-}
-
 int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                     const fpnn_aes_keyset *keys, uint32_t flags, const MapView &v, uint32_t *done) {
     const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
@@ -1850,7 +1807,6 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
         if (int rc = mslot_reserve(m, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
-    const bool prep_first = map_prep_first();
     // the move stream starts after work already queued on the engine stream
     HIP_TRY(hipEventRecord(e->ms[0].ciphered, e->stream));
     HIP_TRY(hipStreamWaitEvent(ms, e->ms[0].ciphered, 0));
@@ -2036,11 +1992,6 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
         // t - 3, was scattered by step t - 1's launch, which the cipher waited for); the
         // cipher is queued before the host prepares chunk t + 1's descriptors
         bool next = false, prepared = false;
-        if (prep_first) {
-            next = prepare(t + 1, rc);
-            if (rc) break;
-            prepared = true;
-        }
         if (cipher_t1) {
             const Chunk &c = ch[k1];
             MapSlot &m = e->ms[k1];
@@ -2139,7 +2090,6 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         if (int rc = mslot_reserve(m, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
-    const bool prep_first = map_prep_first();
     // ---- the streams' (iv, pos), compact, on the device (engine stream) ----
     if (int rc = sstate_reserve(e, nseg * 20)) return rc;
     uint8_t *h_state = e->h_sstate, *d_state = e->d_sstate;
@@ -2322,11 +2272,6 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         // the cipher of chunk t - 1 is queued before the host prepares chunk t + 1 (the
         // engine stream is not left empty while the host works)
         bool more = false, prepared = false;
-        if (prep_first) {
-            more = prepare(t + 1, rc);
-            if (rc) break;
-            prepared = true;
-        }
         if (cipher_t1) {
             const Chunk &c = ch[k1];
             MapSlot &m = e->ms[k1];
@@ -2763,7 +2708,7 @@ int fpnn_ecdh_calc_key_host(fpnn_aes_engine *e, const char *curve, const uint8_t
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh upload"); break; }
         if ((rc = fpnn_ecdh_calc_keys(e, cv, private_key, d, 1, keylen, d + 64, d + 96, d + 112))) break;
         err = hipMemcpyAsync(res, d + 64, sizeof res, hipMemcpyDeviceToHost, e->stream);
-        if (err == hipSuccess) err = sync_spin(e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
     if (rc) return rc;
@@ -2788,7 +2733,7 @@ int fpnn_ecdh_public_key_host(fpnn_aes_engine *e, int curve, const uint8_t *priv
         if ((rc = fpnn_ecdh_public_keys(e, curve, d, 1, d + 32, d + 96))) break;
         err = hipMemcpyAsync(res, d + 32, 64, hipMemcpyDeviceToHost, e->stream);
         if (err == hipSuccess) err = hipMemcpyAsync(res + 64, d + 96, 1, hipMemcpyDeviceToHost, e->stream);
-        if (err == hipSuccess) err = sync_spin(e->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "ecdh download"); break; }
     } while (0);
     if (rc) return rc;

@@ -370,13 +370,13 @@ __global__ __launch_bounds__(256) void k_boundary_save(KBatch b, uint4 *boundary
 // (package mode, one key), 1 for stream / per-packet-key variants (they would spill).
 constexpr int dec_u(bool stream, int km) { return (!stream && km == KEY_UNIFORM) ? 4 : 1; }
 
-template <int NR, bool INPLACE, int NT>
-static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, bool fence, int grid, hipStream_t st) {
-#define FPNN_DEC(L, NTX) \
-    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, KEY_UNIFORM, false, INPLACE, NTX, 4, 1>), dim3(grid), \
+template <int NR, bool INPLACE>
+static void dec_launch(const KBatch &b, Layout layout, KeyMode km, bool dense, int grid, hipStream_t st) {
+#define FPNN_DEC(L) \
+    hipLaunchKernelGGL((k_cfb_decrypt_blocks<NR, L, KEY_UNIFORM, false, INPLACE, 4, 4, 1>), dim3(grid), \
                        dim3(kThreads), 0, st, b)
-#define FPNN_DENSE(AL, U, PF, KEYED) \
-    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, AL, U, 1, PF, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
+#define FPNN_DENSE(AL, U, KEYED) \
+    hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, 4, AL, U, 1, true, KEYED>), dim3(grid), dim3(kThreads), 0, st, b)
     const bool aligned = b.nb_uniform % 64 == 0;
     set_launched(layout == LAYOUT_FULL && km == KEY_LANE && !aligned ? "cfb_decrypt_lanekey"
                  : layout == LAYOUT_FULL && (km == KEY_LANE || dense) ? "cfb_decrypt_dense"
@@ -385,45 +385,36 @@ static void dec_launch(const KBatch &b, Layout layout, KeyMode km, int dense, bo
         hipLaunchKernelGGL((k_cfb_decrypt_lanekey<NR, INPLACE, 4>), dim3(grid), dim3(kThreads), 0, st, b);
     } else if (layout == LAYOUT_FULL && km == KEY_LANE) {  // dense, chunk-aligned, one key per packet
         const uint32_t nbc = b.nb_uniform / 64;
-        if (nbc % 4 == 0) FPNN_DENSE(true, 4, true, true);
-        else if (nbc % 2 == 0) FPNN_DENSE(true, 2, true, true);
-        else FPNN_DENSE(true, 1, true, true);
-    } else if (layout == LAYOUT_FULL && dense == 2) {
-        if (aligned && fence && NT == 4)  // the C2 decrypt with fenced rounds (Variant::fence)
-            hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, NT, true, 4, 1, true, false, true>), dim3(grid),
+        if (nbc % 4 == 0) FPNN_DENSE(true, 4, true);
+        else if (nbc % 2 == 0) FPNN_DENSE(true, 2, true);
+        else FPNN_DENSE(true, 1, true);
+    } else if (layout == LAYOUT_FULL && dense) {  // K1d with the next step prefetched
+        if (aligned)  // the C2 decrypt: fenced rounds
+            hipLaunchKernelGGL((k_cfb_decrypt_dense<NR, INPLACE, 4, true, 4, 1, true, false, true>), dim3(grid),
                                dim3(kThreads), 0, st, b);
-        else if (aligned) FPNN_DENSE(true, 4, true, false);
-        else FPNN_DENSE(false, 4, true, false);
-    } else if (layout == LAYOUT_FULL && dense) {
-        if (aligned) FPNN_DENSE(true, 4, false, false); else FPNN_DENSE(false, 4, false, false);
+        else FPNN_DENSE(false, 4, false);
     } else if (layout == LAYOUT_FULL) {
-        FPNN_DEC(LAYOUT_FULL, NT);
+        FPNN_DEC(LAYOUT_FULL);
     } else {  // LAYOUT_UNIFORM package batch with a partial last block per packet
-        FPNN_DEC(LAYOUT_UNIFORM, NT);
+        FPNN_DEC(LAYOUT_UNIFORM);
     }
 #undef FPNN_DENSE
 #undef FPNN_DEC
 }
 
 template <int NR>
-static void dec_nr(const KBatch &b, const Variant &v, Layout layout, KeyMode km, bool inplace, int grid,
-                   hipStream_t st) {
-    const int dense = b.stride == 16ull * b.nb_uniform ? v.dec_dense : 0;
-    if (v.tables == 2 && km == KEY_UNIFORM) {
-        if (inplace) dec_launch<NR, true, 2>(b, layout, km, dense, v.fence, grid, st);
-        else dec_launch<NR, false, 2>(b, layout, km, dense, v.fence, grid, st);
-    } else {
-        if (inplace) dec_launch<NR, true, 4>(b, layout, km, dense, v.fence, grid, st);
-        else dec_launch<NR, false, 4>(b, layout, km, dense, v.fence, grid, st);
-    }
+static void dec_nr(const KBatch &b, Layout layout, KeyMode km, bool inplace, int grid, hipStream_t st) {
+    const bool dense = b.stride == 16ull * b.nb_uniform;
+    if (inplace) dec_launch<NR, true>(b, layout, km, dense, grid, st);
+    else dec_launch<NR, false>(b, layout, km, dense, grid, st);
 }
 
-hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool inplace, int grid, hipStream_t st) {
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
+                                 hipStream_t st) {
     switch (nrounds) {
-        case 10: dec_nr<10>(b, v, layout, km, inplace, grid, st); break;
-        case 12: dec_nr<12>(b, v, layout, km, inplace, grid, st); break;
-        case 14: dec_nr<14>(b, v, layout, km, inplace, grid, st); break;
+        case 10: dec_nr<10>(b, layout, km, inplace, grid, st); break;
+        case 12: dec_nr<12>(b, layout, km, inplace, grid, st); break;
+        case 14: dec_nr<14>(b, layout, km, inplace, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -41,36 +41,15 @@ __device__ __forceinline__ Fe<NW> reduce_once(const uint32_t *t, uint32_t top, c
     return r;
 }
 
-// (hi:lo) += x * y with the carry out of the 64-bit accumulate into hi: one v_mad_u64_u32
-// (its carry-out operand) and one v_addc per product.  Written out because the compiler
-// otherwise rebuilds the carry with a 64-bit compare and select (4-5 instructions).
-__device__ __forceinline__ void mac(uint64_t &lo, uint32_t &hi, uint32_t x, uint32_t y) {
-    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-        : "+v"(lo), "+v"(hi)
-        : "v"(x), "v"(y)
-        : "vcc");
-}
-// the same with a wave-uniform second factor (the modulus limbs, SGPRs)
-__device__ __forceinline__ void mac_s(uint64_t &lo, uint32_t &hi, uint32_t x, uint32_t ys) {
-    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
-        : "+v"(lo), "+v"(hi)
-        : "v"(x), "s"(ys)
-        : "vcc");
-}
-
-// Montgomery product a*b/R mod p (a, b < p), product scanning with the reduction
-// interleaved column by column (Koc, Acar, Kaliski: "FIPS"): every one of the 2*NW^2
-// partial products goes into one 96-bit column accumulator, two VALU instructions each.
-// (Splitting the a*b and m*p products over two accumulators for more ILP measured 12 %
-// slower: the kernel is VALU-issue-bound, not latency-bound.)
 // secp256k1 (p = 2^256 - 2^32 - 977) in normal form: the 512-bit product t = H*2^256 + L
 // by product scanning (NW^2 partial products, half the Montgomery product's 2*NW^2), then
 // t = L + H*(2^32 + 977) (mod p) folded twice and one conditional subtraction.  The host
 // passes R = 1 (r1 = r2 = 1) for this form, so the Montgomery-form conversions around the
 // ladder become identities and every field value is the same residue as micro-ecc's.
-// Field kinds: Montgomery form with the generic product (any curve), or normal form with
-// a special-prime reduction of the full 512-bit product (R = 1 on the host side).
-enum : int { FK_MONT = 0, FK_K1 = 1, FK_P256 = 2, FK_P224 = 3, FK_P192 = 4 };
+// Field kinds: normal form with a special-prime reduction of the full 2*NW-limb product
+// per curve (R = 1 on the host side).  (Rounds 1-2 also built a generic Montgomery-form
+// product for any curve; it was the A/B baseline and is gone since round 4.)
+enum : int { FK_K1 = 1, FK_P256 = 2, FK_P224 = 3, FK_P192 = 4 };
 
 // t (512 bits) mod p: t = L + H*(2^32 + 977) as three carry chains over the limbs --
 // L + lo(H_i * 977), then + H << 32, then + hi(H_i * 977) << 32 -- leaving a top
@@ -280,7 +259,6 @@ __device__ __forceinline__ Fe<NW> p224_fold(const uint32_t (&t)[14], const EccCo
 
 template <int NW, int FK>
 __device__ __forceinline__ Fe<NW> fold_nf(const uint32_t (&t)[2 * NW], const EccConst &c) {
-    static_assert(FK != FK_MONT, "normal form only");
     if constexpr (FK == FK_K1) {
         static_assert(NW == 8, "secp256k1 has 8 limbs");
         return k1_fold<NW>(t, c);
@@ -296,74 +274,32 @@ __device__ __forceinline__ Fe<NW> fold_nf(const uint32_t (&t)[2 * NW], const Ecc
     }
 }
 
-template <int NW, int FK = FK_MONT>
+template <int NW, int FK>
 __device__ __forceinline__ Fe<NW> fmul(const Fe<NW> &a, const Fe<NW> &b, const EccConst &c) {
-    if constexpr (FK != FK_MONT) {
-        uint32_t t[2 * NW];
-        prodN<NW>(a.v, b.v, t);
-        return fold_nf<NW, FK>(t, c);
-    } else {
-        uint32_t m[NW], r[NW];
-        uint64_t lo = 0;
-        uint32_t hi = 0;
-#pragma unroll
-        for (int i = 0; i < NW; i++) {
-#pragma unroll
-            for (int j = 0; j < i; j++) {
-                mac(lo, hi, a.v[j], b.v[i - j]);
-                mac_s(lo, hi, m[j], c.p[i - j]);
-            }
-            mac(lo, hi, a.v[i], b.v[0]);
-            m[i] = (uint32_t)lo * c.n0inv;
-            mac_s(lo, hi, m[i], c.p[0]);  // the column's low word becomes 0
-            lo = (lo >> 32) | ((uint64_t)hi << 32);
-            hi = 0;
-        }
-#pragma unroll
-        for (int i = NW; i < 2 * NW; i++) {
-#pragma unroll
-            for (int j = i - NW + 1; j < NW; j++) {
-                mac(lo, hi, a.v[j], b.v[i - j]);
-                mac_s(lo, hi, m[j], c.p[i - j]);
-            }
-            r[i - NW] = (uint32_t)lo;
-            lo = (lo >> 32) | ((uint64_t)hi << 32);
-            hi = 0;
-        }
-        return reduce_once<NW>(r, (uint32_t)lo, c);  // < 2p
-    }
+    uint32_t t[2 * NW];
+    prodN<NW>(a.v, b.v, t);
+    return fold_nf<NW, FK>(t, c);
 }
 
-template <int NW, int FK = FK_MONT>
+template <int NW, int FK>
 __device__ __forceinline__ Fe<NW> fsqr(const Fe<NW> &a, const EccConst &c) {
-    if constexpr (FK != FK_MONT) {
-        uint32_t t[2 * NW];
-        sqrN<NW>(a.v, t);
-        return fold_nf<NW, FK>(t, c);
-    } else {
-        return fmul<NW, FK>(a, a, c);
-    }
+    uint32_t t[2 * NW];
+    sqrN<NW>(a.v, t);
+    return fold_nf<NW, FK>(t, c);
 }
 
 // r1 = a1 * b1 (a1^2 if SQ1), r2 = a2 * b2 (a2^2 if SQ2) -- two independent field products
 // computed together (prod_dual); every operand is read before either result is written, so
-// r1 / r2 may alias any input.  The Montgomery form (the A/B baseline) runs them one by one.
+// r1 / r2 may alias any input.
 template <int NW, int FK, bool SQ1, bool SQ2>
 __device__ __forceinline__ void fdual(Fe<NW> &r1, const Fe<NW> &a1, const Fe<NW> &b1, Fe<NW> &r2, const Fe<NW> &a2,
                                       const Fe<NW> &b2, const EccConst &c) {
-    if constexpr (FK != FK_MONT) {
-        uint32_t t1[2 * NW], t2[2 * NW];
-        prod_dual<NW, SQ1, SQ2>(a1.v, SQ1 ? a1.v : b1.v, t1, a2.v, SQ2 ? a2.v : b2.v, t2);
-        if (SQ1) sqr_finish<NW>(a1.v, t1);
-        if (SQ2) sqr_finish<NW>(a2.v, t2);
-        r1 = fold_nf<NW, FK>(t1, c);
-        r2 = fold_nf<NW, FK>(t2, c);
-    } else {
-        const Fe<NW> x = SQ1 ? fsqr<NW, FK>(a1, c) : fmul<NW, FK>(a1, b1, c);
-        const Fe<NW> y = SQ2 ? fsqr<NW, FK>(a2, c) : fmul<NW, FK>(a2, b2, c);
-        r1 = x;
-        r2 = y;
-    }
+    uint32_t t1[2 * NW], t2[2 * NW];
+    prod_dual<NW, SQ1, SQ2>(a1.v, SQ1 ? a1.v : b1.v, t1, a2.v, SQ2 ? a2.v : b2.v, t2);
+    if (SQ1) sqr_finish<NW>(a1.v, t1);
+    if (SQ2) sqr_finish<NW>(a2.v, t2);
+    r1 = fold_nf<NW, FK>(t1, c);
+    r2 = fold_nf<NW, FK>(t2, c);
 }
 
 template <int NW>
@@ -476,15 +412,6 @@ __device__ Fe<NW> finv(const Fe<NW> &a, const EccConst &c) {
             return fmul<NW, FK>(fsqr_n<NW, FK>(t, 2, c), a, c);
         }
     }
-    Fe<NW> r = fconst<NW>(c.r1);
-    for (int w = NW - 1; w >= 0; w--) {
-        const uint32_t e = c.pm2[w];
-        for (int b = 31; b >= 0; b--) {
-            r = fsqr<NW, FK>(r, c);
-            if ((e >> b) & 1u) r = fmul<NW, FK>(r, a, c);
-        }
-    }
-    return r;
 }
 
 // double_jacobian (curve-specific.inc:50-95 a = -3; :1110-1141 secp256k1, a = 0), z != 0
@@ -876,42 +803,14 @@ void hex_limbs(const char *h, uint32_t out[8]) {
     }
 }
 
-// r = 2r mod p over nw limbs (r < p)
-void dbl_mod(uint32_t *r, const uint32_t *p, int nw) {
-    uint32_t t[9], carry = 0;
-    for (int j = 0; j < nw; j++) {
-        const uint64_t s = ((uint64_t)r[j] << 1) | carry;
-        t[j] = (uint32_t)s;
-        carry = (uint32_t)(s >> 32);
-    }
-    uint32_t d[8], borrow = 0;
-    for (int j = 0; j < nw; j++) {
-        const uint64_t s = (uint64_t)t[j] - p[j] - borrow;
-        d[j] = (uint32_t)s;
-        borrow = (uint32_t)(s >> 63);
-    }
-    const bool use_d = carry || !borrow;
-    for (int j = 0; j < nw; j++) r[j] = use_d ? d[j] : t[j];
-}
-
 void be_to_limbs(const uint8_t *be, int nbytes, uint32_t *out, int nlimbs) {
     memset(out, 0, nlimbs * sizeof(uint32_t));
     for (int i = 0; i < nbytes; i++) out[i / 4] |= (uint32_t)be[nbytes - 1 - i] << (8 * (i % 4));
 }
 
-template <int NW, bool AM3, int FK = FK_MONT>
+template <int NW, bool AM3, int FK>
 void launch_nw(const EccConst &c, const EcdhJob &j, hipStream_t st) {
     hipLaunchKernelGGL((k_ecdh<NW, AM3, FK>), dim3((j.count + 255) / 256), dim3(256), 0, st, c, j);
-}
-
-// Every curve in normal form with its special-prime reduction (secp256k1, secp256r1,
-// secp224r1, secp192r1); FPNN_ECDH_MONT=1 selects the generic Montgomery kernels (A/B)
-bool special_form(int curve) {
-    static const bool mont = [] {
-        const char *v = getenv("FPNN_ECDH_MONT");
-        return v && atoi(v) != 0;
-    }();
-    return !mont;  // every supported curve has a special-form kernel
 }
 
 }  // namespace
@@ -941,16 +840,11 @@ bool ecc_fill_const(int curve, EccConst &c) {
     uint32_t inv = 1;  // p^-1 mod 2^32 by Newton iteration
     for (int i = 0; i < 5; i++) inv *= 2u - c.p[0] * inv;
     c.n0inv = 0u - inv;
-    uint32_t r[8] = {1};
-    for (int i = 0; i < 32 * nw; i++) dbl_mod(r, c.p, nw);  // R mod p
-    memcpy(c.r1, r, sizeof r);
-    for (int i = 0; i < 32 * nw; i++) dbl_mod(r, c.p, nw);  // R^2 mod p
-    memcpy(c.r2, r, sizeof r);
-    if (special_form(curve)) {  // normal form: R = 1
-        memset(c.r1, 0, sizeof c.r1);
-        memset(c.r2, 0, sizeof c.r2);
-        c.r1[0] = c.r2[0] = 1;
-    }
+    // every kernel works in normal form (special-prime reduction): R = 1, so the Montgomery
+    // conversions around the ladder are identities
+    memset(c.r1, 0, sizeof c.r1);
+    memset(c.r2, 0, sizeof c.r2);
+    c.r1[0] = c.r2[0] = 1;
     return true;
 }
 
@@ -980,31 +874,13 @@ void ecc_set_uniform_point(EccConst &c, const uint8_t *pub_be) {
 
 hipError_t launch_ecdh(const EccConst &c, const EcdhJob &j, int curve, hipStream_t st) {
     if (j.count == 0) return hipSuccess;
+    // every curve in normal form with its special-prime reduction (round 2/3; the generic
+    // Montgomery-form kernel was the A/B baseline and is no longer built)
     switch (curve) {
-        case ECC_SECP256K1:
-            if (special_form(curve))
-                launch_nw<8, false, FK_K1>(c, j, st);
-            else
-                launch_nw<8, false>(c, j, st);
-            break;
-        case ECC_SECP256R1:
-            if (special_form(curve))
-                launch_nw<8, true, FK_P256>(c, j, st);
-            else
-                launch_nw<8, true>(c, j, st);
-            break;
-        case ECC_SECP224R1:
-            if (special_form(curve))
-                launch_nw<7, true, FK_P224>(c, j, st);
-            else
-                launch_nw<7, true>(c, j, st);
-            break;
-        case ECC_SECP192R1:
-            if (special_form(curve))
-                launch_nw<6, true, FK_P192>(c, j, st);
-            else
-                launch_nw<6, true>(c, j, st);
-            break;
+        case ECC_SECP256K1: launch_nw<8, false, FK_K1>(c, j, st); break;
+        case ECC_SECP256R1: launch_nw<8, true, FK_P256>(c, j, st); break;
+        case ECC_SECP224R1: launch_nw<7, true, FK_P224>(c, j, st); break;
+        case ECC_SECP192R1: launch_nw<6, true, FK_P192>(c, j, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -63,10 +63,6 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of m
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-#ifndef FPNN_K2H_VKEYS
-#define FPNN_K2H_VKEYS 0
-#endif
-
 template <int NR, int KM, bool STREAM, int NT, int CH, bool SHIFT, bool FENCE, bool LANES = true>
 __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cfb_encrypt_hybrid(KBatch b, HybridArgs h) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
@@ -86,15 +82,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     const bool wm = SHIFT && __builtin_amdgcn_readfirstlane(h.buckets[kWireFlagWord]) == 0u;
 
     RoundKeys<NR> rku;
-    if (KM == KEY_UNIFORM) {
-        rku = load_round_keys<NR>(b.keys);
-        // the last FPNN_K2H_VKEYS round-key words in VGPRs (every lane the same word): the
-        // sessions' scalar state then leaves fewer SGPRs to spill into VGPR lanes
-#pragma unroll
-        // (not for wire frames' lane session, an A/B-only path: it would spill VGPRs)
-        for (int i = 4 * (NR + 1) - FPNN_K2H_VKEYS; i < 4 * (NR + 1); i++)
-            if (i >= 0 && !(SHIFT && LANES)) asm volatile("v_mov_b32 %0, %1" : "=v"(rku.k[i]) : "s"(rku.k[i]));
-    }
+    if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
 
     // ---------------- quad session: K2q's cipher over perm[0, n_long) ----------------
     // Steps of 8 blocks; the next step's input words are loaded during this step's rounds.
@@ -193,7 +181,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 d = 0;
                 lo0 = 0;
                 const int bnd = (int)((128u - ((uint32_t)(uintptr_t)oo & 127u)) & 127u) - wlo;  // line end - word
-                jt = (h.qflags & 1u) || bnd + wlo == 0 ? 8u : bnd <= 0 ? 0u : (uint32_t)(bnd + 15) >> 4;
+                jt = bnd + wlo == 0 ? 8u : bnd <= 0 ? 0u : (uint32_t)(bnd + 15) >> 4;
                 hv = false;
             } else if (SHIFT) {
                 d = (uint32_t)(uintptr_t)oo & 15u;
@@ -207,7 +195,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 praw = pw;
                 lo0 = d > pv ? d - pv : 0u;
                 const uint32_t m = (8u - (((uint32_t)((uintptr_t)(oo - d) >> 4)) & 7u)) & 7u;
-                jt = (h.qflags & 1u) || m == 0 ? 8u : m;
+                jt = m == 0 ? 8u : m;
                 hv = false;
             }
         };
@@ -278,14 +266,13 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             // this step: 8 blocks, or up to the next line boundary where input and output
             // share their line offset; the next step is loaded during this one's rounds
             uint32_t lim = 8u;
-            if (!SHIFT && !(h.qflags & 1u)) {
+            if (!SHIFT) {
                 const uint32_t xo = (uint32_t)(uintptr_t)o & 127u, xi = (uint32_t)(uintptr_t)p & 127u;
                 if (xo == xi && !(xo & 15u)) lim = 8u - (xo >> 4);
             }
             const uint32_t kk = active ? (nfull < lim ? nfull : lim) : 0u;
             const uint32_t rest = active ? nfull - kk : 0u;
-            const uint32_t kk2 = (h.qflags & 2u) ? 0u : rest < 8u ? rest : 8u;
-            if (h.qflags & 2u) fresh = true;
+            const uint32_t kk2 = rest < 8u ? rest : 8u;
             // Memory ops of the steady state are unconditional (lanes with nothing to load
             // read the key table, lanes with nothing to store write the wave's sink slot),
             // so the waitcnt pass counts them exactly: the rounds wait only for this step's
@@ -548,10 +535,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     if (__atomic_load_n(&h.ctr[0], __ATOMIC_RELAXED) + static_q < n_long) quad_session(false);
 }
 
-template <int NR, bool F>
-static void hybrid_nrf(const KBatch &b, const HybridArgs &h, KeyMode km, bool stream, int grid, hipStream_t st) {
+template <int NR>
+static void hybrid_nr(const KBatch &b, const HybridArgs &h, KeyMode km, bool stream, int grid, hipStream_t st) {
 #define FPNN_HYB(K, STR, CH, SH, LN) \
-    hipLaunchKernelGGL((k_cfb_encrypt_hybrid<NR, K, STR, 4, CH, SH, F || SH, LN>), dim3(grid), dim3(kThreads), 0, st, b, h)
+    hipLaunchKernelGGL((k_cfb_encrypt_hybrid<NR, K, STR, 4, CH, SH, true, LN>), dim3(grid), dim3(kThreads), 0, st, b, h)
     // the funnel-shifted whole-slot stores only where outputs sit off the block grid by
     // construction (the wire prefix); other ragged outputs are stored as they fall
     const bool shift = !stream && (b.flags & F_WIRE_PREFIX);
@@ -570,22 +557,15 @@ static void hybrid_nrf(const KBatch &b, const HybridArgs &h, KeyMode km, bool st
 #undef FPNN_HYB
 }
 
-template <int NR>
-static void hybrid_nr(const KBatch &b, const HybridArgs &h, KeyMode km, bool stream, bool fence, int grid,
-                      hipStream_t st) {
-    if (fence) hybrid_nrf<NR, true>(b, h, km, stream, grid, st);
-    else hybrid_nrf<NR, false>(b, h, km, stream, grid, st);
-}
-
-hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, bool fence,
-                                 int grid, hipStream_t st) {
+hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, int grid,
+                                 hipStream_t st) {
     hipError_t err = hipMemsetAsync(h.ctr, 0, 2 * sizeof(uint32_t), st);
     if (err != hipSuccess) return err;
     set_launched("cfb_encrypt_hybrid");
     switch (nrounds) {
-        case 10: hybrid_nr<10>(b, h, km, stream, fence, grid, st); break;
-        case 12: hybrid_nr<12>(b, h, km, stream, fence, grid, st); break;
-        case 14: hybrid_nr<14>(b, h, km, stream, fence, grid, st); break;
+        case 10: hybrid_nr<10>(b, h, km, stream, grid, st); break;
+        case 12: hybrid_nr<12>(b, h, km, stream, grid, st); break;
+        case 14: hybrid_nr<14>(b, h, km, stream, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -435,15 +435,16 @@ static void ragged_nrf(const KBatch &b, KeyMode km, bool stream, const RaggedPla
 }
 
 template <int NR>
-static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, bool fence,
-                      int grid, hipStream_t st) {
-    // fenced AES-192/256 per-slot passes run out of SGPRs for their round keys (spills)
-    if (fence && (NR == 10 || km == KEY_UNIFORM)) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
+static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, int grid,
+                      hipStream_t st) {
+    // fenced rounds, except AES-192/256 per-slot passes: those run out of SGPRs for their
+    // round keys (spills)
+    if (NR == 10 || km == KEY_UNIFORM) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
     else ragged_nrf<NR, false>(b, km, stream, plan, sink, grid, st);
 }
 
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
-                                 bool fence, bool plan_launch, int grid, hipStream_t st) {
+                                 bool plan_launch, int grid, hipStream_t st) {
     const uint64_t nwaves = (uint64_t)grid * (kThreads / 64);
     const unsigned pgrid = (unsigned)((nwaves * 64 + 255) / 256);
     if (!plan_launch)
@@ -454,9 +455,9 @@ hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool 
         hipLaunchKernelGGL((k_ragged_plan<false>), dim3(pgrid), dim3(256), 0, st, b, nwaves, plan);
     set_launched("cfb_decrypt_ragged");
     switch (nrounds) {
-        case 10: ragged_nr<10>(b, km, stream, plan, sink, fence, grid, st); break;
-        case 12: ragged_nr<12>(b, km, stream, plan, sink, fence, grid, st); break;
-        case 14: ragged_nr<14>(b, km, stream, plan, sink, fence, grid, st); break;
+        case 10: ragged_nr<10>(b, km, stream, plan, sink, grid, st); break;
+        case 12: ragged_nr<12>(b, km, stream, plan, sink, grid, st); break;
+        case 14: ragged_nr<14>(b, km, stream, plan, sink, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -47,16 +47,19 @@ __device__ __forceinline__ void fill_tables_regs(uint4 *lds4, const uint32_t *__
 template <int NR, bool ENCRYPT>
 __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
-    __shared__ uint4 buf[kSmallMaxBytes / 16 + 1];
+    __shared__ uint4 buf[kSmallMaxBytes / 16 + 2];  // head block + body + one spare (prefetch)
     __shared__ uint32_t fhead[4], fout[4];  // feedback register after the head / after the call
     const uint32_t t = threadIdx.x;
-    fill_tables_regs<4>(lds4, a.t0le, ENCRYPT ? 4 : 32);
     // the call's bytes: the body starts at io + kSmallBodyAt (16-aligned), the head's
     // bytes (pos != 0: the rest of the current keystream block) sit right before it
     const uint32_t rem = a.len - a.head, r = rem & 15u;
     const uint32_t nb = (rem + 15) >> 4;  // body blocks, the last one partial when r != 0
     uint4 *io = reinterpret_cast<uint4 *>(a.io + kSmallBodyAt - 16);
-    for (uint32_t i = t; i <= nb; i += kSmallThreads) buf[i] = io[i];  // buf[0]: the head bytes at its end
+    // first PCIe read in flight before the table fill (both wait on memory, not on each other)
+    const uint4 first = t <= nb ? io[t] : make_uint4(0, 0, 0, 0);
+    fill_tables_regs<4>(lds4, a.t0le, ENCRYPT ? 4 : 32);
+    if (t <= nb) buf[t] = first;  // buf[0]: the head bytes at its end
+    for (uint32_t i = t + kSmallThreads; i <= nb; i += kSmallThreads) buf[i] = io[i];
     __syncthreads();
     if (t == 0) {  // head: ivec bytes [pos, pos + head) are keystream already (base/rijndael.c:1180-1195)
         uint8_t *fb = reinterpret_cast<uint8_t *>(fhead);
@@ -80,9 +83,12 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
             for (int k = 0; k <= NR; k++) rkq[k] = a.rk[4 * k + t];
             uint32_t fq = word_of(f0, (int)t);
             uint32_t *bw = reinterpret_cast<uint32_t *>(buf + 1);
+            uint32_t pw = nb ? bw[t] : 0u;  // P_i, loaded one block ahead of its use
             for (uint32_t i = 0; i < nb; i++) {
+                const uint32_t p = pw;
+                pw = bw[4 * (i + 1) + t];  // (buf has one spare block past the body)
                 const uint32_t k = aes_encrypt_column<NR, 4>(fq, rkq, T);
-                const uint32_t c = k ^ bw[4 * i + t];
+                const uint32_t c = k ^ p;
                 bw[4 * i + t] = c;
                 if (i + 1 < nb || r == 0) {
                     fq = c;

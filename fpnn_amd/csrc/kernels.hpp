@@ -53,32 +53,21 @@ struct KBatch {
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
-// Kernel build variant chosen per engine (defaults tuned on MI355X; overridable with
-// FPNN_AES_TABLES / FPNN_AES_ENC_CHUNK for A/B measurements).
+// Per-engine dispatch settings.  Round 4 removed the measured-and-rejected kernel
+// variants (2-table LDS image, 1/4-block encrypt chunks, unfenced rounds, K2q, K1 on dense
+// batches, the separate K1r plan launch for out-of-place batches); what is left are the
+// K2h split parameters, settable per engine so that small test batches exercise each of
+// its sessions (tests/conftest.py).
 struct Variant {
-    int tables = 4;     // LDS T-table layout: 2 (T0,T2; two workgroups/CU) or 4 (T0..T3; one)
-    int enc_chunk = 8;     // encrypt chain: blocks per chunk (1, 4 or 8; 8 = one 128-B line per lane)
-    int enc_align = 1;     // K2: run a chain's blocks before its first 128-B line boundary singly
-    int coop = -1;         // encrypt: -1 auto, 0 never, 1 always use the 4-lane K2c
-    int queue = 1;         // encrypt, ragged batches: K2q work queue -- 0 never, 1 when chains > quads, 2 always
-    int hybrid = 1;        // ragged batches that take the queue: K2h (lanes + quads) instead of K2q
     // K2h: chains of at least hyb_long blocks (bucket-rounded) go to quads; hyb_quad_waves
-    // of a workgroup's 16 waves start on them.  Round-3 sweep on C4 (tools/gpu_r03w.sh,
-    // gpu_r03x.sh; profiles/r03/sweep_c4_r03x.json): 1024 / 12 at 790-799 GiB/s against
-    // 738 for round 2's 512 / 8 on the same box.
+    // of a workgroup's 16 waves start on them.  Round-3 sweep on C4 (profiles/r03/
+    // sweep_c4_r03x.json): 1024 / 12 at 790-799 GiB/s against 738 for 512 / 8.
     int hyb_long = 1024;
     int hyb_quad_waves = 12;
-    int hyb_wire_lanes = 0;  // K2h: wire-prefix batches also use the lane session (else all quads)
-    int hyb_qflags = 0;      // K2h quad-session A/B flags (HybridArgs::qflags)
-    int dec_full = 1;      // decrypt: whole-block fast path (LAYOUT_FULL) when it applies
-    int dec_dense = 2;     // decrypt, LAYOUT_FULL with stride == length: 0 = K1, 1 = K1d, 2 = K1d + prefetch
-    int fence = 1;         // K2 / K1d (C2 shape), K1r, K2h: issue each round's 16 lookups before folding
-    // K1r per-wave plan: 0 = in the decrypt kernel itself when in != out (no other wave
-    // can overwrite a predecessor block then), 1 = always the separate k_ragged_plan launch
-    int k1r_plan = 0;
+    int hyb_wire_lanes = 0;  // wire-prefix batches also use the lane session (else all quads)
+    int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
 };
 
-int blocks_per_cu(const Variant &v, KeyMode km);
 // Base name ("cfb_decrypt_dense", ...) of the main kernel the last launch_* call on this
 // thread queued (the variant the dispatch actually chose; instrumentation and bench labels).
 const char *last_launched();
@@ -112,15 +101,11 @@ struct KScan {
 };
 
 hipError_t launch_scan_frames(const KScan &s, bool stream, int num_cus, hipStream_t st);
-hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool stream, int grid, int threads, hipStream_t st);
+hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
+                                 int threads, hipStream_t st);
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st);
-// K2q: K2c with a work queue (a quad takes the next chain as soon as it is done);
-// next = one device word of scratch (zeroed here, on the stream).
-hipError_t launch_encrypt_queue(const KBatch &b, int nrounds, KeyMode km, bool stream, int grid, int threads,
-                                uint32_t *next, hipStream_t st);
 // K2h (k_hybrid.hip): ragged batches with more chains than quads.  Chains of perm[]
 // in length buckets <= long_bucket run on quads (K2c's cipher), the rest one per lane
 // (K2's); quad_waves waves per workgroup start on the long ones.  ctr: 2 device words
@@ -136,18 +121,17 @@ struct HybridArgs {
     uint32_t long_bucket;
     uint32_t quad_waves;
     uint4 *sink;      // 2 x uint4 per wave (grid * kThreads / 64 waves): stores with nothing to store
-    uint32_t qflags;  // A/B of the quad session: 1 = 8-block steps (not line-aligned), 2 = no prefetch
 };
-hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, bool fence,
-                                 int grid, hipStream_t st);
+hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, int grid,
+                                 hipStream_t st);
 // length bucket of a block count (descending: bucket 0 = longest), as launch_length_order
 uint32_t length_bucket_of(uint64_t nblocks);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
 // (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
 // K1 / K1d / K1k for uniform and dense layouts (every segment's block count known on the host).
-hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, const Variant &v, Layout layout, KeyMode km,
-                                 bool inplace, int grid, hipStream_t st);
+hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
+                                 hipStream_t st);
 // K1r (k_ragged.hip): ragged decrypt with no host round trip.  b.bstart[0..count] from
 // launch_block_map_scan (bstart[count] = total blocks, device only); plan: one entry per
 // wave of the grid (grid * kThreads / 64), filled by the plan kernel queued first.
@@ -160,7 +144,7 @@ struct RaggedPlan {
 // ones from stride / uniform_len; out_off may be in_off).
 // sink: 2 x uint4 per wave of the grid, written by lanes with nothing to store, never read.
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,
-                                 bool fence, bool plan_launch, int grid, hipStream_t st);
+                                 bool plan_launch, int grid, hipStream_t st);
 hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_len, uint64_t *in_off, uint32_t *len,
                               hipStream_t st);
 // In-place K1 / K1d: save the ciphertext block before every 64-block chunk.

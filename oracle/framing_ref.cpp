@@ -89,7 +89,14 @@ int run(R &r, int rfd, int wfd, const uint8_t *wire, uint64_t n, uint32_t piece,
             FPQuestPtr q;
             FPAnswerPtr a;
             bool http = false;
-            const bool f = r.fetch(q, a, http);
+            bool f;
+            try {  // the reference Encryptor cannot throw here; the drop-in reports GPU failures this way
+                f = r.fetch(q, a, http);
+            } catch (const std::exception &ex) {
+                fprintf(stderr, "fetch threw: %s\n", ex.what());
+                fprintf(out, "{\"end\": \"fetch_exception\", \"curr\": %d, \"total\": %d}\n", r.curr(), r.total());
+                return 4;
+            }
             std::string raw;
             const char *kind = "none";
             if (f && q) {

@@ -38,6 +38,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -124,7 +125,19 @@ double now() {
 
 }  // namespace
 
+static int run(int argc, char **argv);
+
 int main(int argc, char **argv) {
+    try {  // the reference Encryptor cannot throw; the drop-in reports GPU failures this way
+        return run(argc, argv);
+    } catch (const std::exception &ex) {
+        fprintf(stderr, "io_echo: %s\n", ex.what());
+        fflush(stderr);
+        _exit(9);
+    }
+}
+
+static int run(int argc, char **argv) {
     if (argc < 5) {
         fprintf(stderr, "usage: %s mode keylen quests payload [window]\n", argv[0]);
         return 2;

@@ -69,16 +69,6 @@ def _env_engine(env):
                 os.environ[k] = v
 
 
-@pytest.fixture(scope="session")
-def queue_engine():
-    """An engine that always uses the K2q work-queue encrypt for ragged batches
-    (by default ragged batches with more chains than lane quads take K2h)."""
-    eng = _env_engine({"FPNN_AES_QUEUE": "2", "FPNN_AES_HYBRID": "0"})
-    yield eng
-    eng.sync()
-    eng.close()
-
-
 # K2h (k_hybrid.hip) on every ragged batch, with the long-chain threshold and the number
 # of waves that start on quads set so that small test batches exercise each session:
 #   hybrid_engine       chains of >= 64 blocks on quads, 3 quad waves per workgroup
@@ -93,7 +83,7 @@ HYBRID_ENGINES = {
 
 
 def _hybrid(name):
-    env = {"FPNN_AES_QUEUE": "2", "FPNN_AES_HYBRID": "1"}
+    env = {"FPNN_AES_HYB_FORCE": "1"}
     env.update(HYBRID_ENGINES[name])
     return _env_engine(env)
 

@@ -61,7 +61,7 @@ def test_c1_echo_reference_io_plumbing_on_dropin(idx):
     g = _c1()["echo"][idx]
     out = subprocess.run([exe, "1" if g["mode"] == "stream" else "0", str(g["keylen"]), str(g["quests"]),
                           str(g["payload"]), str(g["window"])], capture_output=True, text=True, timeout=600)
-    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.returncode == 0, (out.returncode, out.stderr[-2000:])
     d = json.loads(out.stdout.strip().splitlines()[-1])
     print(json.dumps(d))
     assert d["answers_ok"] and d["served"] == g["quests"]

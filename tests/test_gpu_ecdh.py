@@ -175,17 +175,3 @@ def test_cpp_keyexchange_dropin(tmp_path, golden):
             assert (int(ok), key.replace("-", ""), iv.replace("-", "")) == (s["ok"], s["key"], s["iv"]), s
         assert out[k] == "roundtrip 1", (cv["curve"], out[k])
         k += 1
-
-
-@pytest.mark.skipif(os.environ.get("FPNN_ECDH_MONT") == "1", reason="this is the Montgomery-form child run")
-def test_montgomery_form_kernels_too():
-    """FPNN_ECDH_MONT=1 selects the generic Montgomery-form kernel for every curve -- the
-    A/B baseline of secp256k1's / secp256r1's special-prime forms (k_ecdh.hip FK_K1 /
-    FK_P256).  The same fixture and oracle checks run against it in a child process (the
-    switch is read once per process)."""
-    env = dict(os.environ, FPNN_ECDH_MONT="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        os.path.abspath(__file__), "-k", "server_batch or client_side or random_peers"],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout and "failed" not in r.stdout

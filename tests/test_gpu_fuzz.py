@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 
-ENGINES = ["engine", "engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine", "hybrid_quad_engine"]
+ENGINES = ["engine", "engine", "hybrid_engine", "hybrid_lane_engine", "hybrid_quad_engine"]
 SHAPES = ["uniform", "dense", "dense_partial", "keyed_dense", "keyed_lane", "contiguous", "gapped", "ragged_keys"]
 
 

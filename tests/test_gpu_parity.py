@@ -155,7 +155,7 @@ def test_golden_cfb_cases_stream_batch(engine, golden):
                 assert int(poso[i]) == c["pos_out"]
 
 
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+@pytest.mark.parametrize("eng_kind", ["engine", "hybrid_engine", "hybrid_lane_engine",
                                       "hybrid_quad_engine"])
 def test_golden_package_cases(request, golden, eng_kind):
     engine = request.getfixturevalue(eng_kind)
@@ -238,7 +238,7 @@ def make_ragged(rng, n, max_len, align_gap=True):
 @pytest.mark.parametrize("keylen", [16, 24, 32])
 @pytest.mark.parametrize("nkeys", [1, 7])
 @pytest.mark.parametrize("inplace", [False, True])
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+@pytest.mark.parametrize("eng_kind", ["engine", "hybrid_engine", "hybrid_lane_engine",
                                       "hybrid_quad_engine"])
 def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind):
     engine = request.getfixturevalue(eng_kind)
@@ -427,7 +427,7 @@ def test_dense_keyed_layout(engine, oracle, length, inplace):
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
-@pytest.mark.parametrize("eng_kind", ["engine", "queue_engine", "hybrid_engine", "hybrid_lane_engine",
+@pytest.mark.parametrize("eng_kind", ["engine", "hybrid_engine", "hybrid_lane_engine",
                                       "hybrid_quad_engine"])
 def test_random_stream_batches(request, oracle, keylen, eng_kind):
     """Many streams, several successive calls each with random lengths; outputs and the
@@ -1200,14 +1200,14 @@ def test_host_frames_over_two_engines(engine, oracle):
 
 @pytest.mark.parametrize("layout", ["same_offsets", "inplace", "shifted_out", "stream"])
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_queue_line_aligned_steps(queue_engine, oracle, layout, keylen):
-    """K2q's line-aligned steps (k_encrypt.hip): a chain whose input and output sit at the
+def test_quad_line_aligned_steps(hybrid_quad_engine, oracle, layout, keylen):
+    """K2h's quad session, line-aligned steps (k_hybrid.hip): a chain whose input and output sit at the
     same 16-B multiple inside a 128-B line takes a short first step to the line boundary.
     Ragged batches with 16-B multiple offsets at every line position and lengths from one
     block to many 8-block steps (some with a partial last block); 'shifted_out' (output
     16 B off the input) keeps the unaligned steps; 'stream' starts at random CFB
     positions, so the aligned step begins after the head bytes."""
-    engine = queue_engine
+    engine = hybrid_quad_engine
     rng = np.random.default_rng(77 + 3 * keylen + ["same_offsets", "inplace", "shifted_out", "stream"].index(layout))
     n = 1200
     lens = (rng.integers(0, 200, n) * 16 + rng.choice([0, 0, 0, 5, 11], n)).astype(np.int64)

@@ -12,7 +12,7 @@ equal the first variant's, byte for byte.
   R1A  the same with 16-byte aligned bodies (1040-byte frame pitch)
   C2R  C2's 1M x 1 KiB packets as a ragged batch (offset / length arrays)
 With --decrypt the package configs also decrypt the output back (timed, round trip checked).
-Usage: python tools/ab_encrypt.py --config C4 --variants "FPNN_AES_HYBRID=0;FPNN_AES_HYBRID=1"
+Usage: python tools/ab_encrypt.py --config C4 --variants "FPNN_AES_HYB_LONG=512;FPNN_AES_HYB_LONG=1024"
 """
 import argparse
 import hashlib
@@ -47,7 +47,7 @@ def make_engine(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C4")
-    ap.add_argument("--variants", default="FPNN_AES_HYBRID=0;FPNN_AES_HYBRID=1")
+    ap.add_argument("--variants", default="FPNN_AES_HYB_LONG=512;FPNN_AES_HYB_LONG=1024")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--decrypt", action="store_true", help="also time decrypting the output back (package batches)")
