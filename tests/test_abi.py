@@ -243,3 +243,15 @@ def test_thread_engine_device_plan():
     assert _plan({"FPNN_AES_DEVICE": "2"}, 3, 4) == ([2, 2, 2], 16)
     assert _plan({"FPNN_AES_DEVICE": "7"}, 2, 4) == ([-1, -1], 1)
     assert _plan({"FPNN_AES_MAX_ENGINES": "3"}, 4, 8)[1] == 3
+
+
+def test_cpp_threads_program_compiles(tmp_path):
+    """tests/cpp/threads.cpp (the engine-pool test of tests/test_gpu_threads.py) builds
+    against the headers with -Wall -Werror."""
+    import fpnn_amd
+    exe = os.path.join(str(tmp_path), "threads")
+    libdir = os.path.dirname(fpnn_amd.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "threads.cpp"), "-o", exe, "-L", libdir, "-lfpnn_aes",
+                    f"-Wl,-rpath,{libdir}"], check=True, capture_output=True, text=True)
+    assert os.access(exe, os.X_OK)
