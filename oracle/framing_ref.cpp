@@ -19,6 +19,8 @@
 //   case.bin: "FRG1" u32 mode (0 package, 1 stream) u32 keylen key[keylen] iv[16]
 //             i32 max_len u32 piece u64 wire_len wire[wire_len]   (little endian)
 #include <errno.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -122,7 +124,20 @@ int run(R &r, int rfd, int wfd, const uint8_t *wire, uint64_t n, uint32_t piece,
 
 }  // namespace
 
+// a crash prints its stack to stderr (the drop-in build runs on a GPU box without a debugger)
+static void on_fatal(int sig) {
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    fprintf(stderr, "fatal signal %d, stack:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char **argv) {
+    signal(SIGABRT, on_fatal);
+    signal(SIGSEGV, on_fatal);
+    signal(SIGBUS, on_fatal);
     if (argc != 3) {
         fprintf(stderr, "usage: %s case.bin out.jsonl\n", argv[0]);
         return 2;

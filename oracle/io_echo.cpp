@@ -28,6 +28,8 @@
 //   window: quests in flight (1 = strict ping-pong, the per-call latency shape)
 #include <arpa/inet.h>
 #include <errno.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -127,7 +129,20 @@ double now() {
 
 static int run(int argc, char **argv);
 
+// a crash prints its stack to stderr (the drop-in build runs on a GPU box without a debugger)
+static void on_fatal(int sig) {
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    fprintf(stderr, "fatal signal %d, stack:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char **argv) {
+    signal(SIGABRT, on_fatal);
+    signal(SIGSEGV, on_fatal);
+    signal(SIGBUS, on_fatal);
     try {  // the reference Encryptor cannot throw; the drop-in reports GPU failures this way
         return run(argc, argv);
     } catch (const std::exception &ex) {

@@ -53,7 +53,8 @@ def run_receiver(exe, case, piece):
         with open(cin, "wb") as f:
             f.write(b"FRG1" + struct.pack("<II", 0 if case["mode"] == "package" else 1, len(key)) + key + iv
                     + struct.pack("<iIQ", case["max_len"], piece, len(wire)) + wire)
-        r = subprocess.run([exe, cin, cout], timeout=120, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        r = subprocess.run([exe, cin, cout], timeout=120, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                           env=dict(os.environ, LIBC_FATAL_STDERR_="1"))
         assert r.returncode == 0, f"{os.path.basename(exe)} exited {r.returncode}: {r.stderr[-2000:]}"
         with open(cout) as f:
             lines = [json.loads(x) for x in f]
