@@ -26,16 +26,23 @@ import torch  # noqa: E402
 import workloads as W  # noqa: E402
 
 
-def timed(eng, which, fn, reps, rounds=3):
-    """Steady state, as bench.py: after two warm-up calls (clocks ramp; the first calls grow
-    scratch buffers), `rounds` rounds of `reps` calls issued back to back (no host sync
-    between them -- an idle gap lets the clock drop, which individually timed calls of a
-    ~1 ms kernel measure instead of the kernel).  Returns the medians over rounds of (wall s
-    per call, kernel s per launch of the main kernel `which` from HIP events on the engine
-    stream) and the launches per call."""
+def timed(eng, which, fn, reps, rounds=3, warm_s=0.3):
+    """Steady state, as bench.py: warm-up calls for at least warm_s seconds of GPU work (the
+    first calls grow scratch buffers, and the chip needs tens of ms of load to reach its
+    clock: with two warm-up calls C2 read 866 / 952 GiB/s against bench.py's 1 008 / 1 014 in
+    the same session, profiles/r04/timers.json), then `rounds` rounds of `reps` calls issued
+    back to back (no host sync between them -- an idle gap lets the clock drop, which
+    individually timed calls of a ~1 ms kernel measure instead of the kernel).  Returns the
+    medians over rounds of (wall s per call, kernel s per launch of the main kernel `which`
+    from HIP events on the engine stream) and the launches per call."""
     import statistics
-    for _ in range(2):
+    t0 = time.perf_counter()
+    n = 0
+    while n < 2 or time.perf_counter() - t0 < warm_s:
         fn()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     walls, kern, launches = [], [], 0
     for _ in range(max(1, rounds)):
