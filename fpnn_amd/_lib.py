@@ -94,6 +94,11 @@ SIGNATURES = {
     "fpnn_aes_engine_stream": (_vp, [_vp]),
     "fpnn_aes_thread_engine_device": (C.c_int, [C.c_uint32, C.c_int]),
     "fpnn_aes_max_thread_engines": (C.c_int, [C.c_int]),
+    "fpnn_aes_device_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
+    "fpnn_aes_device_free": (C.c_int, [_vp, _vp]),
+    "fpnn_aes_pinned_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
+    "fpnn_aes_pinned_free": (C.c_int, [_vp, _vp]),
+    "fpnn_aes_copy_async": (C.c_int, [_vp, _vp, _vp, C.c_size_t]),
     "fpnn_aes_engine_reserve": (C.c_int, [_vp, C.c_uint64, C.c_uint64]),
     "fpnn_aes_keyset_create": (C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int, C.POINTER(_vp)]),
     "fpnn_aes_keyset_from_schedules": (C.c_int, [_vp, C.c_uint32, C.POINTER(Schedule), _vp, C.POINTER(_vp)]),
@@ -130,6 +135,8 @@ SIGNATURES = {
     "fpnn_ecdh_curve": (C.c_int, [C.c_char_p]),
     "fpnn_ecdh_secret_len": (C.c_int, [C.c_int]),
     "fpnn_ecdh_private_len": (C.c_int, [C.c_int]),
+    "fpnn_ecdh_curve_name": (C.c_char_p, [C.c_int]),
+    "fpnn_ecdh_random_private": (C.c_int, [C.c_int, C.c_char_p]),
     "fpnn_ecdh_calc_keys": (C.c_int, [_vp, C.c_int, C.c_char_p, _vp, C.c_uint32, C.c_int, _vp, _vp, _vp]),
     "fpnn_ecdh_calc_keys_client": (C.c_int, [_vp, C.c_int, _vp, C.c_char_p, C.c_uint32, C.c_int, _vp, _vp, _vp]),
     "fpnn_ecdh_public_keys": (C.c_int, [_vp, C.c_int, _vp, C.c_uint32, _vp, _vp]),

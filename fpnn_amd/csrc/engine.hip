@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/random.h>
 
 #include <algorithm>
 #include <atomic>
@@ -562,17 +563,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
 
 extern "C" {
 
-const char *fpnn_aes_strerror(int status) {
-    switch (status) {
-        case FPNN_AES_OK: return "ok";
-        case FPNN_AES_ERR_KEYLEN: return "key length must be 16, 24 or 32 bytes";
-        case FPNN_AES_ERR_ARG: return "invalid argument";
-        case FPNN_AES_ERR_RANGE: return "batch too large";
-        case FPNN_AES_ERR_HIP: return "HIP runtime error";
-        case FPNN_AES_ERR_NODEV: return "no usable gfx950 device";
-        default: return "unknown status";
-    }
-}
+// (fpnn_aes_strerror lives in the front library, front.cpp: it must work without this one)
 
 const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
 
@@ -2507,6 +2498,46 @@ int fpnn_aes_stream_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_k
     });
 }
 
+int fpnn_aes_device_alloc(fpnn_aes_engine *e, size_t bytes, void **out) {
+    if (!e || !out) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipMalloc(out, bytes ? bytes : 1));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_device_free(fpnn_aes_engine *e, void *p) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    if (!p) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipFree(p));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_pinned_alloc(fpnn_aes_engine *e, size_t bytes, void **out) {
+    if (!e || !out) return FPNN_AES_ERR_ARG;
+    *out = nullptr;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, 0));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_pinned_free(fpnn_aes_engine *e, void *p) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    if (!p) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipHostFree(p));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_copy_async(fpnn_aes_engine *e, void *dst, const void *src, size_t bytes) {
+    if (!e || (bytes && (!dst || !src))) return FPNN_AES_ERR_ARG;
+    if (!bytes) return FPNN_AES_OK;
+    DeviceGuard g(e->device);
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, e->stream));
+    return FPNN_AES_OK;
+}
+
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset) {
     if (!e || (nbytes && !dst)) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
@@ -2591,6 +2622,42 @@ int fpnn_ecdh_secret_len(int curve) {
 
 int fpnn_ecdh_private_len(int curve) {
     return curve >= 0 && curve < ECC_NCURVES ? (ecc_curve_info(curve).num_n_bits + 7) / 8 : -1;
+}
+
+const char *fpnn_ecdh_curve_name(int curve) {
+    return curve >= 0 && curve < ECC_NCURVES ? ecc_curve_info(curve).name : nullptr;
+}
+
+int fpnn_ecdh_random_private(int curve, uint8_t *out) {
+    EccConst c;
+    if (!out || !ecc_fill_const(curve, c)) return 0;
+    const int nw = c.nw, bits = c.num_n_bits;
+    for (int tries = 0; tries < 64; tries++) {
+        uint32_t k[8] = {0};
+        size_t got = 0;
+        while (got < sizeof(uint32_t) * nw) {
+            const ssize_t r = getrandom(reinterpret_cast<uint8_t *>(k) + got, sizeof(uint32_t) * nw - got, 0);
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                return 0;
+            }
+            got += (size_t)r;
+        }
+        if (bits < 32 * nw) k[nw - 1] &= 0xFFFFFFFFu >> (32 * nw - bits);
+        bool zero = true, below = false, decided = false;
+        for (int w = nw - 1; w >= 0; w--) {
+            zero = zero && k[w] == 0;
+            if (!decided && k[w] != c.n[w]) {
+                below = k[w] < c.n[w];
+                decided = true;
+            }
+        }
+        if (zero || !below) continue;
+        const int pb = c.private_bytes;
+        for (int i = 0; i < pb; i++) out[i] = (uint8_t)(k[(pb - 1 - i) / 4] >> (8 * ((pb - 1 - i) % 4)));
+        return 1;
+    }
+    return 0;
 }
 
 int fpnn_ecdh_calc_keys(fpnn_aes_engine *e, int curve, const uint8_t *private_key, const uint8_t *peer_public,

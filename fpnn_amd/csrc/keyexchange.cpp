@@ -1,16 +1,13 @@
 // keyexchange.cpp -- fpnn::ECCKeyExchange / ECCKeysMaker (include/KeyExchange.h) over the
 // GPU ECDH of include/fpnn_ecdh.h.  Mirrors core/KeyExchange.cpp:49-187 check for check;
 // the scalar multiplications and hashes run in k_ecdh.hip.
-#include <errno.h>
 #include <string.h>
-#include <sys/random.h>
 
 #include <string>
 
 #include "../../include/Encryptor.h"
 #include "../../include/KeyExchange.h"
 #include "../../include/fpnn_ecdh.h"
-#include "ecc.hpp"
 #include "thread_engine.hpp"
 
 namespace {
@@ -33,41 +30,7 @@ void throw_if_error(int rc, const char *what) {
     }
 }
 
-const char *curve_name(int curve) { return fpnn_aes::ecc_curve_info(curve).name; }
-
-// uECC_generate_random_int (core/micro-ecc/uECC.c:980-1002): 0 < k < n, drawn with the
-// top word masked to n's bit length; big-endian private_len bytes out.
-bool random_below_n(int curve, uint8_t *out) {
-    fpnn_aes::EccConst c;
-    if (!fpnn_aes::ecc_fill_const(curve, c)) return false;
-    const int nw = c.nw, bits = c.num_n_bits;
-    for (int tries = 0; tries < 64; tries++) {
-        uint32_t k[8] = {0};
-        size_t got = 0;
-        while (got < sizeof(uint32_t) * nw) {
-            const ssize_t r = getrandom(reinterpret_cast<uint8_t *>(k) + got, sizeof(uint32_t) * nw - got, 0);
-            if (r < 0) {
-                if (errno == EINTR) continue;
-                return false;
-            }
-            got += (size_t)r;
-        }
-        if (bits < 32 * nw) k[nw - 1] &= 0xFFFFFFFFu >> (32 * nw - bits);
-        bool zero = true, below = false, decided = false;
-        for (int w = nw - 1; w >= 0; w--) {
-            zero = zero && k[w] == 0;
-            if (!decided && k[w] != c.n[w]) {
-                below = k[w] < c.n[w];
-                decided = true;
-            }
-        }
-        if (zero || !below) continue;
-        const int pb = c.private_bytes;
-        for (int i = 0; i < pb; i++) out[i] = (uint8_t)(k[(pb - 1 - i) / 4] >> (8 * ((pb - 1 - i) % 4)));
-        return true;
-    }
-    return false;
-}
+const char *curve_name(int curve) { return fpnn_ecdh_curve_name(curve); }
 
 }  // namespace
 
@@ -127,7 +90,7 @@ std::string ECCKeysMaker::publicKey(bool reGen) {
         fpnn_aes_engine *e = lease.engine();
         uint8_t priv[32], pub[64];
         for (int tries = 0; tries < 64; tries++) {
-            if (!random_below_n(_curve, priv)) return std::string();  // "Gen public key & private key failed."
+            if (!fpnn_ecdh_random_private(_curve, priv)) return std::string();  // "Gen public key & private key failed."
             const int r = fpnn_ecdh_public_key_host(e, _curve, priv, pub);
             throw_if_error(r, "publicKey");
             if (r == 1) {

@@ -3,7 +3,6 @@
 // EncryptedStreamReceiver::recvPackage + fetch (core/EncryptedStreamReceiver.cpp:72-163)
 // over fpnn_aes_stream_recv.  Host work: lay out each connection's region (plaintext carry
 // ‖ new ciphertext) in pinned staging, one H2D, the call, one D2H, hand out the messages.
-#include <hip/hip_runtime.h>
 #include <string.h>
 
 #include <algorithm>
@@ -25,10 +24,6 @@ std::string describe(int rc) {
     return s;
 }
 
-void check_hip(hipError_t err, const char *what) {
-    if (err != hipSuccess) throw EncryptorError(std::string("StreamReceiverBatch: ") + what + ": " + hipGetErrorString(err));
-}
-
 void check(int rc, const char *what) {
     if (rc != FPNN_AES_OK) throw EncryptorError(std::string("StreamReceiverBatch: ") + what + ": " + describe(rc));
 }
@@ -38,44 +33,47 @@ size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 }  // namespace
 
 // Device and pinned buffers of one batch, on the engine of the thread that flushes it
-// (grown, kept).  Pool engines are never destroyed (thread_engine.hpp), so the cached
-// stream stays valid when the batch is destroyed or flushed by another thread after the
-// first one has exited.  Plain hipMalloc / hipFree: no dependence on memory-pool support.
+// (grown, kept), through the C-ABI's memory calls (this file is built without HIP).
+// Pool engines are never destroyed (thread_engine.hpp), so the cached engine stays valid
+// when the batch is destroyed or flushed by another thread after the first has exited.
 struct StreamReceiverBatch::Dev {
     fpnn_aes_engine *e = nullptr;
     uint64_t eid = 0;
-    hipStream_t st = nullptr;
     fpnn_aes_keyset *ks[3] = {nullptr, nullptr, nullptr};  // per key length
     uint8_t *d = nullptr, *h = nullptr;  // regions | descriptors | results
     size_t cap_d = 0, cap_h = 0;
 
     void release() {
-        if (st) (void)hipStreamSynchronize(st);  // a pass that threw may have left copies queued
+        if (e) (void)fpnn_aes_engine_sync(e);  // a pass that threw may have left copies queued
         for (fpnn_aes_keyset *&k : ks) {
             if (k) fpnn_aes_keyset_destroy(k);
             k = nullptr;
         }
-        if (d) (void)hipFree(d);
-        if (h) (void)hipHostFree(h);
+        if (d) (void)fpnn_aes_device_free(e, d);
+        if (h) (void)fpnn_aes_pinned_free(e, h);
         d = h = nullptr;
         cap_d = cap_h = 0;
     }
     void reserve(size_t need) {
-        if (need > cap_d || need > cap_h) check_hip(hipStreamSynchronize(st), "hipStreamSynchronize");
+        if (need > cap_d || need > cap_h) check(fpnn_aes_engine_sync(e), "sync");
         if (need > cap_d) {
             size_t n = std::max<size_t>(cap_d * 2, std::max<size_t>(need, 1 << 20));
-            if (d) (void)hipFree(d);
+            if (d) (void)fpnn_aes_device_free(e, d);
             d = nullptr;
             cap_d = 0;
-            check_hip(hipMalloc(reinterpret_cast<void **>(&d), n), "hipMalloc");
+            void *p = nullptr;
+            check(fpnn_aes_device_alloc(e, n, &p), "device buffer");
+            d = static_cast<uint8_t *>(p);
             cap_d = n;
         }
         if (need > cap_h) {
             size_t n = std::max<size_t>(cap_h * 2, std::max<size_t>(need, 1 << 20));
-            if (h) (void)hipHostFree(h);
+            if (h) (void)fpnn_aes_pinned_free(e, h);
             h = nullptr;
             cap_h = 0;
-            check_hip(hipHostMalloc(reinterpret_cast<void **>(&h), n, 0), "hipHostMalloc");
+            void *p = nullptr;
+            check(fpnn_aes_pinned_alloc(e, n, &p), "pinned buffer");
+            h = static_cast<uint8_t *>(p);
             cap_h = n;
         }
     }
@@ -141,7 +139,6 @@ void StreamReceiverBatch::flush() {
         _dev = new Dev();
         _dev->e = e;
         _dev->eid = eid;
-        _dev->st = (hipStream_t)fpnn_aes_engine_stream(e);
     }
     for (Conn &c : _conns) c.msgs.clear();
     // passes until no connection stopped at max_frames; one pass per key length
@@ -202,7 +199,7 @@ void StreamReceiverBatch::pass(const std::vector<int> &ids, int nrounds) {
     fpnn_aes_keyset *&ks = D.ks[(nrounds - 10) / 2];
     if (!ks) check(fpnn_aes_keyset_reserve(D.e, std::max<uint32_t>(n, 256), nrounds, &ks), "key table");
     check(fpnn_aes_keyset_set(ks, 0, n, scheds.data(), nullptr), "key table upload");
-    check_hip(hipMemcpyAsync(D.d, h, o_foff, hipMemcpyHostToDevice, D.st), "upload");
+    check(fpnn_aes_copy_async(D.e, D.d, h, o_foff), "upload");
     fpnn_aes_batch b;
     memset(&b, 0, sizeof b);
     b.in = D.d;
@@ -217,9 +214,9 @@ void StreamReceiverBatch::pass(const std::vector<int> &ids, int nrounds) {
                                reinterpret_cast<uint64_t *>(D.d + o_foff), reinterpret_cast<uint32_t *>(D.d + o_flen),
                                reinterpret_cast<fpnn_aes_frame_scan *>(D.d + o_scan)),
           "stream_recv");
-    check_hip(hipMemcpyAsync(h, D.d, at, hipMemcpyDeviceToHost, D.st), "download");
-    check_hip(hipMemcpyAsync(h + o_pos, D.d + o_pos, total - o_pos, hipMemcpyDeviceToHost, D.st), "download");
-    check_hip(hipStreamSynchronize(D.st), "hipStreamSynchronize");
+    check(fpnn_aes_copy_async(D.e, h, D.d, at), "download");
+    check(fpnn_aes_copy_async(D.e, h + o_pos, D.d + o_pos, total - o_pos), "download");
+    check(fpnn_aes_engine_sync(D.e), "sync");
     for (uint32_t i = 0; i < n; i++) {
         Conn &c = _conns[ids[i]];
         const uint8_t *region = h + seg[i] - c.carry.size();

@@ -15,6 +15,16 @@
  * the engine's HIP stream; calls return after queuing unless they say otherwise.
  * Results are bit-identical to the reference for every key length (16/24/32),
  * payload length (including 0 and non-multiples of 16) and CFB position.
+ *
+ * Library layout: libfpnn_aes.so (what callers link) carries these entry points, the
+ * C++ classes (Encryptor.h, EncryptorBatch.h, StreamReceiverBatch.h, KeyExchange.h) and
+ * no HIP dependency of its own; on first use it loads libfpnn_aes_gpu.so from its own
+ * directory (FPNN_AES_GPU_LIB overrides the path) -- the HIP kernels and the engine --
+ * and forwards every call there.  Loading the HIP runtime late keeps its static TLS
+ * (about 30 KiB, rocprofiler-register) out of every thread's stack: FPNN starts threads
+ * with 16 KiB stacks (base/msec.c:72-74), which the runtime linked at start-up made
+ * pthread_create refuse.  If the GPU library cannot be loaded every call returns
+ * FPNN_AES_ERR_NODEV (fpnn_aes_last_error says why).
  */
 #ifndef FPNN_AES_H
 #define FPNN_AES_H
@@ -277,6 +287,16 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
 int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state,
                          const uint32_t *carry, uint32_t max_len, uint32_t max_frames, uint64_t *frame_off,
                          uint32_t *frame_len, fpnn_aes_frame_scan *scan);
+
+/* ---- memory on an engine's device, for callers built without HIP headers ------------ */
+/* (StreamReceiverBatch uses these: libfpnn_aes.so itself has no HIP dependency, see the
+ * library layout note at the top.)  device_free waits for the device; copy_async queues a
+ * copy of `bytes` between any two of host-pinned / device memory on the engine stream. */
+int fpnn_aes_device_alloc(fpnn_aes_engine *e, size_t bytes, void **out);
+int fpnn_aes_device_free(fpnn_aes_engine *e, void *p);
+int fpnn_aes_pinned_alloc(fpnn_aes_engine *e, size_t bytes, void **out);
+int fpnn_aes_pinned_free(fpnn_aes_engine *e, void *p);
+int fpnn_aes_copy_async(fpnn_aes_engine *e, void *dst, const void *src, size_t bytes);
 
 /* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
 /* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */

@@ -44,6 +44,12 @@ int fpnn_ecdh_curve(const char *name);
 int fpnn_ecdh_secret_len(int curve);
 /* uECC_curve_private_key_size: 32, 32, 28, 24; -1 unknown. */
 int fpnn_ecdh_private_len(int curve);
+/* The reference's configuration name of a curve ("secp256k1", ...); NULL when unknown. */
+const char *fpnn_ecdh_curve_name(int curve);
+/* uECC_generate_random_int (core/micro-ecc/uECC.c:980-1002): a private key 0 < k < n from
+ * the OS random source, big-endian private_len bytes.  1 on success, 0 when no random
+ * bytes could be had. */
+int fpnn_ecdh_random_private(int curve, uint8_t *out);
 
 /* Server side: private_key (host, private_len bytes) against count peer public keys
  * (device, count * 2*secret_len bytes).  keys (device, count*keylen), ivs (device,

@@ -66,8 +66,56 @@ def test_cpp_encryptor_symbols_exported():
 
 def test_kernels_built_for_gfx950():
     import fpnn_amd
-    data = open(fpnn_amd.LIB_PATH, "rb").read()
+    gpu = os.path.join(os.path.dirname(fpnn_amd.LIB_PATH), "libfpnn_aes_gpu.so")
+    data = open(gpu, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle id of the embedded code object
+
+
+def test_front_library_has_no_hip_dependency():
+    """libfpnn_aes.so (what FPNN links) loads the HIP runtime only on first use, through
+    libfpnn_aes_gpu.so: linked at start-up, the runtime's ~30 KiB of static TLS made
+    pthread_create refuse FPNN's 16 KiB-stack clock thread (base/msec.c:72-74) and the
+    reference's receivers aborted on their first message (tests/test_gpu_dropin.py).  So:
+    no HIP library among its dependencies, and a thread with a 16 KiB stack starts in a
+    process that has it loaded and initialised."""
+    import fpnn_amd
+    deps = subprocess.run(["readelf", "-d", fpnn_amd.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "NEEDED" in deps and not any(x in deps for x in ("amdhip", "hsa-runtime", "rocprof")), deps
+    tls = subprocess.run(["readelf", "-lW", fpnn_amd.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    for line in tls.splitlines():
+        if line.split()[:1] == ["TLS"]:
+            assert int(line.split()[5], 16) <= 256, line
+
+
+def test_small_stack_thread_after_first_call(tmp_path):
+    """A C program linked with libfpnn_aes.so makes a library call (which loads the GPU
+    library and the HIP runtime) and then starts a thread with a 16 KiB stack, as FPNN's
+    base/msec.c does; pthread_create must succeed (no GPU needed: the call may fail)."""
+    import fpnn_amd
+    src = tmp_path / "stack.c"
+    src.write_text(r"""
+#include <pthread.h>
+#include <stdio.h>
+#include "fpnn_aes.h"
+static void *run(void *a) { return a; }
+int main(void) {
+    int n = 0;
+    fpnn_aes_device_count(&n);
+    pthread_attr_t attr; pthread_t t;
+    pthread_attr_init(&attr);
+    pthread_attr_setstacksize(&attr, 16 * 1024);
+    int rc = pthread_create(&t, &attr, run, 0);
+    if (rc == 0) pthread_join(t, 0);
+    printf("%d\n", rc);
+    return rc;
+}
+""")
+    exe = str(tmp_path / "stack")
+    libdir = os.path.dirname(fpnn_amd.LIB_PATH)
+    subprocess.run(["gcc", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", exe, "-L", libdir, "-lfpnn_aes",
+                    f"-Wl,-rpath,{libdir}", "-pthread"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "0", (out.stdout, out.stderr[-500:])
 
 
 def test_version_string():

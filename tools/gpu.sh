@@ -78,6 +78,10 @@ for step in "$@"; do
     prof:ECDH) pmc_passes prof_ECDH 'k_ecdh' python3 tools/bench_ecdh.py --curves secp256k1 --no-cpu --reps 3 ;;
     prof:*) c=${step#prof:}; pmc_passes "prof_$c" 'cfb_' python3 tools/bench_configs.py --configs "$c" --no-host --reps 3 ;;
     ecdh) run ecdh 300 python -u tools/bench_ecdh.py ;;
+    diag_dropin)  # the drop-in receiver on one framing case with the HIP runtime's log on
+      AMD_LOG_LEVEL=3 run diag_framing 120 oracle/_ref/framing_dropin tools/probe/case0.bin "$OUT/case0.jsonl"
+      AMD_LOG_LEVEL=3 run diag_echo 120 oracle/_ref/io_echo_dropin 0 32 20 1024 1
+      run diag_echo_nolog 120 oracle/_ref/io_echo_dropin 0 32 2000 1024 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
