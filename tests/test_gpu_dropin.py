@@ -49,8 +49,8 @@ def test_reference_receivers_on_dropin_reproduce_framing_fixtures(case):
     exe = _exe("framing_dropin")
     for piece in (1, 7, 65536):
         ev, end = run_receiver(exe, case, piece)
+        assert (len(ev), end["end"]) == (len(case["frames"]), case["end"]["end"]), (case["name"], piece, end)
         assert ev == case["frames"], (case["name"], piece)
-        assert end["end"] == case["end"]["end"], (case["name"], piece, end)
 
 
 @pytest.mark.parametrize("idx", range(len(_c1()["echo"])))

@@ -124,6 +124,26 @@ def test_small_call_kernel_vs_oracle(engine, oracle, keylen):
             assert (iv_g, pos_g) == (iv_o, pos_o), (enc, n)
 
 
+def test_small_call_receiver_pattern(engine, oracle):
+    """The call sequence of EncryptedStreamReceiver on one connection
+    (core/EncryptedStreamReceiver.cpp:89,124): decrypt the 12-byte header, then the body
+    at position 12 mod 16, message after message, state carried -- 400 messages through
+    K0, each call against the oracle."""
+    import fpnn_amd
+    rng = np.random.default_rng(1212)
+    for keylen in (16, 32):
+        key = rng.bytes(keylen)
+        ctx = fpnn_amd.setup_encrypt(key)
+        iv_g = iv_o = rng.bytes(16)
+        pos_g = pos_o = 0
+        for m in range(400):
+            for n in (12, int(rng.integers(1, 1500))):
+                data = rng.bytes(n)
+                out, iv_g, pos_g = engine.cfb(ctx, False, data, iv_g, pos_g)
+                exp, iv_o, pos_o = oracle.cfb(key, False, data, iv_o, pos_o)
+                assert (out, iv_g, pos_g) == (exp, iv_o, pos_o), (keylen, m, n)
+
+
 def test_golden_cfb_cases_stream_batch(engine, golden):
     """The same cases as ONE device stream batch: each case is a stream segment with its
     own key, carried (iv, pos) in and out (fpnn_aes_stream_encrypt/decrypt)."""
