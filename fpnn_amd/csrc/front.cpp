@@ -13,6 +13,7 @@
 // (tests/test_gpu_dropin.py).  A library loaded later with dlopen keeps its TLS out of the
 // static block.
 #include <dlfcn.h>
+#include <errno.h>
 #include <stdlib.h>
 
 #include <mutex>
@@ -57,9 +58,23 @@ F gpu_symbol(const char *name) {
 
 }  // namespace
 
+// Every entry point leaves errno as it found it.  The reference's cipher never touches
+// errno, and FPNN's receivers rely on that: after a short read() they test errno
+// (core/EncryptedStreamReceiver.cpp:31-55) although a decrypt call ran since the socket
+// call that set it -- the HIP runtime's calls in between would otherwise make a partial
+// body read look like a failed socket and close the connection (found by
+// tests/test_gpu_dropin.py, stream fixtures fed in 7-byte pieces).
+namespace {
+struct ErrnoKeep {
+    int saved = errno;
+    ~ErrnoKeep() { errno = saved; }
+};
+}  // namespace
+
 #define FPNN_FWD(RET, NAME, PARAMS, ARGS, FAIL)                        \
     extern "C" RET NAME PARAMS {                                       \
         using fn_t = RET(*) PARAMS;                                    \
+        ErrnoKeep keep;                                                \
         static const fn_t f = gpu_symbol<fn_t>(#NAME);                 \
         if (!f) return FAIL;                                           \
         return f ARGS;                                                 \
@@ -83,6 +98,7 @@ const char *fpnn_aes_strerror(int status) {
 
 const char *fpnn_aes_last_error(void) {
     using fn_t = const char *(*)(void);
+    ErrnoKeep keep;
     static const fn_t f = gpu_symbol<fn_t>("fpnn_aes_last_error");
     return f ? f() : g_load_error.c_str();
 }

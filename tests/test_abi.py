@@ -90,7 +90,9 @@ def test_front_library_has_no_hip_dependency():
 def test_small_stack_thread_after_first_call(tmp_path):
     """A C program linked with libfpnn_aes.so makes a library call (which loads the GPU
     library and the HIP runtime) and then starts a thread with a 16 KiB stack, as FPNN's
-    base/msec.c does; pthread_create must succeed (no GPU needed: the call may fail)."""
+    base/msec.c does; pthread_create must succeed (no GPU needed: the call may fail).  The
+    calls leave errno unchanged (FPNN's receivers test errno after a short read with a
+    decrypt call in between, core/EncryptedStreamReceiver.cpp:31-55)."""
     import fpnn_amd
     src = tmp_path / "stack.c"
     src.write_text(r"""
@@ -98,9 +100,14 @@ def test_small_stack_thread_after_first_call(tmp_path):
 #include <stdio.h>
 #include "fpnn_aes.h"
 static void *run(void *a) { return a; }
+#include <errno.h>
 int main(void) {
     int n = 0;
+    errno = EAGAIN;  /* every call leaves errno as it found it (front.cpp) */
     fpnn_aes_device_count(&n);
+    fpnn_aes_engine *e = 0;
+    fpnn_aes_engine_create(0, FPNN_AES_OWN_STREAM, &e);
+    if (errno != EAGAIN) { printf("errno %d\n", errno); return 7; }
     pthread_attr_t attr; pthread_t t;
     pthread_attr_init(&attr);
     pthread_attr_setstacksize(&attr, 16 * 1024);
