@@ -38,6 +38,28 @@ def main():
         out["checksums_match"] = r["checksum"] == gpu["checksum"]
         out["per_call_slowdown_vs_reference"] = round(gpu["us_per_encrypt"] / r["us_per_encrypt"], 2)
         out["batched_speedup_vs_reference_per_call"] = round(r["us_per_encrypt"] / gpu["us_per_frame_batched"], 2)
+    # C1 itself: the reference's SendBuffer + encrypted receivers, encrypted echo over loopback
+    # TCP (oracle/io_echo.cpp), on the reference's Encryptor and on the drop-in
+    echo = {}
+    for name in ("io_echo_ref", "io_echo_dropin"):
+        exe = os.path.join(ROOT, "oracle", "_ref", name)
+        if not os.path.exists(exe):
+            continue
+        for mode, kl, win in (("0", "32", "1"), ("0", "32", "64"), ("1", "16", "1")):
+            r = subprocess.run([exe, mode, kl, str(args.frames), str(args.len), win], capture_output=True, text=True,
+                               timeout=600)
+            if r.returncode == 0:
+                d = json.loads(r.stdout.strip().splitlines()[-1])
+                echo.setdefault(f"{d['mode']}_aes{8 * int(kl)}_window{win}", {})[name] = {
+                    k: d[k] for k in ("us_per_echo", "echo_per_s", "answers_ok", "wire_c2s_fnv", "wire_s2c_fnv")}
+            else:
+                echo.setdefault(f"mode{mode}_window{win}", {})[name] = {"rc": r.returncode, "stderr": r.stderr[-300:]}
+    if echo:
+        for v in echo.values():
+            if "io_echo_ref" in v and "io_echo_dropin" in v and "wire_c2s_fnv" in v["io_echo_ref"]:
+                v["wire_matches"] = all(v["io_echo_ref"][k] == v["io_echo_dropin"].get(k)
+                                        for k in ("wire_c2s_fnv", "wire_s2c_fnv"))
+        out["c1_echo"] = echo
     print(json.dumps(out))
 
 
