@@ -234,6 +234,13 @@ struct fpnn_aes_engine {
     uint8_t *h_small = nullptr;
     uint8_t *d_small = nullptr;
     uint32_t small_seq = 0;
+    // K0s: the resident small-call server's mailbox (pinned), its device view, the last
+    // request number and the epoch of the last server launched (0: none yet)
+    SmallMailbox *h_mb = nullptr;
+    SmallMailbox *d_mb = nullptr;
+    uint32_t mb_seq = 0;
+    uint32_t srv_epoch = 0;
+    uint64_t srv_idle_ticks = 0, srv_life_ticks = 0;
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
     uint8_t *d_stage = nullptr;
@@ -680,6 +687,11 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_small) (void)hipHostFree(e->h_small);
+    if (e->h_mb) {  // the server left already (idle) or leaves now; the stream sync above waited
+        __atomic_store_n(&e->h_mb->req.stop, 1u, __ATOMIC_RELEASE);
+        if (e->stream) (void)hipStreamSynchronize(e->stream);
+        (void)hipHostFree(e->h_mb);
+    }
     if (e->h_sstate) (void)hipHostFree(e->h_sstate);
     for (auto &v : e->ev)
         for (auto &p : v) {
@@ -1083,9 +1095,8 @@ bool small_enabled() {
 // says the results are in.  The wait spins on that word; after 20 ms it falls back to the
 // stream sync, which also reports a kernel that failed.
 constexpr uint64_t kSmallStage = kSmallBodyAt + kSmallMaxBytes + 64;
-int cfb_small(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, const uint8_t *in, uint8_t *out,
-              size_t len, uint8_t ivec[16], size_t *p_num) {
-    DeviceGuard g(e->device);
+int cfb_small_launch(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, const uint8_t *in, uint8_t *out,
+                     size_t len, uint8_t ivec[16], size_t *p_num) {
     if (!e->h_small) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_small), kSmallStage, hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&e->d_small), e->h_small, 0));
@@ -1128,6 +1139,89 @@ int cfb_small(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, co
     }
     *p_num = hstate[4];
     return FPNN_AES_OK;
+}
+
+// K0s, the resident server (FPNN_AES_SMALL_SERVER=0: a K0 launch per call instead).  The
+// request goes into the mailbox, its number last (release); if no server of this engine is
+// alive one is launched on the engine stream (it starts after whatever is queued there);
+// the host spins until the server stores the number into resp.done.  A server that left
+// (idle, lifetime) before seeing the request is relaunched; after 20 ms of spinning the
+// stream sync -- which returns once the server has left, and reports a failed kernel --
+// settles it.
+bool server_enabled() {
+    static const bool on = [] {
+        const char *v = getenv("FPNN_AES_SMALL_SERVER");
+        return !v || atoi(v) != 0;
+    }();
+    return on;
+}
+
+int launch_server(fpnn_aes_engine *e) {
+    if (!e->srv_idle_ticks) {
+        int khz = 0;  // device wall clock (wall_clock64), kHz
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, e->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        e->srv_idle_ticks = (uint64_t)khz / 20;   // 50 us without a request
+        e->srv_life_ticks = (uint64_t)khz * 2;    // 2 ms in any case
+    }
+    const uint32_t epoch = ++e->srv_epoch;
+    HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, e->stream));
+    return FPNN_AES_OK;
+}
+
+int cfb_small_server(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, const uint8_t *in, uint8_t *out,
+                     size_t len, uint8_t ivec[16], size_t *p_num) {
+    if (!e->h_mb) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_mb), sizeof(SmallMailbox), hipHostMallocCoherent));
+        memset(e->h_mb, 0, sizeof(SmallMailbox));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&e->d_mb), e->h_mb, 0));
+    }
+    SmallMailbox *mb = e->h_mb;
+    const uint32_t pos = (uint32_t)*p_num;
+    const uint32_t head = pos ? (uint32_t)std::min<size_t>(len, 16 - pos) : 0u;
+    memcpy(mb->io + kSmallBodyAt - head, in, len);
+    mb->req.op = encrypt ? 1u : 0u;
+    mb->req.len = (uint32_t)len;
+    mb->req.head = head;
+    mb->req.pos = pos;
+    mb->req.nrounds = (uint32_t)ctx->nrounds;
+    memcpy(mb->req.iv, ivec, 16);
+    for (int k = 0; k < 4 * (ctx->nrounds + 1); k++) mb->req.rk[k] = bswap32(ctx->rk[k]);
+    const uint32_t seq = ++e->mb_seq;
+    __atomic_store_n(&mb->req.seq, seq, __ATOMIC_RELEASE);
+    const int which = encrypt ? FPNN_AES_K_ENCRYPT : FPNN_AES_K_DECRYPT;
+    e->last_kernel[which] = "cfb_server";
+    // a server is alive unless none was launched or the last one has stored its epoch
+    if (e->srv_epoch == 0 || __atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch)
+        if (int rc = launch_server(e)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0; __atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq; spins++) {
+        __builtin_ia32_pause();
+        if (__atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch &&
+            __atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq) {
+            if (int rc = launch_server(e)) return rc;  // it left before seeing this request
+            continue;
+        }
+        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+            HIP_TRY(hipStreamSynchronize(e->stream));
+            if (__atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq) {
+                g_last_error = "small-call server left without serving the request";
+                return FPNN_AES_ERR_HIP;
+            }
+            break;
+        }
+    }
+    memcpy(out, mb->io + kSmallBodyAt - head, len);
+    memcpy(ivec, mb->resp.state, 16);
+    *p_num = mb->resp.state[4];
+    return FPNN_AES_OK;
+}
+
+int cfb_small(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encrypt, const uint8_t *in, uint8_t *out,
+              size_t len, uint8_t ivec[16], size_t *p_num) {
+    DeviceGuard g(e->device);
+    return server_enabled() ? cfb_small_server(e, ctx, encrypt, in, out, len, ivec, p_num)
+                            : cfb_small_launch(e, ctx, encrypt, in, out, len, ivec, p_num);
 }
 
 // One synchronous rijndael.h call in the non-CFB modes (k_modes.hip).  Staging:

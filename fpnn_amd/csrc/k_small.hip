@@ -1,4 +1,4 @@
-// k_small.hip -- K0, the small single-call CFB kernel behind the synchronous drop-in
+// k_small.hip -- the small single-call CFB kernels behind the synchronous drop-in
 // (PackageEncryptor / StreamEncryptor per call, rijndael_cfb_encrypt; core/Encryptor.cpp:10-70,
 // base/rijndael.c:1171-1201) for calls of up to kSmallMaxBytes.
 //
@@ -6,15 +6,17 @@
 // kernels pay for throughput machinery a single frame never uses: K2c fills the 128 KiB
 // replicated LDS image with 64 threads (128 dependent rounds of a global load each), K1r
 // launches a block map, a descriptor pass and a 256-workgroup grid for 64 blocks, and the
-// call moves its bytes with three DMA copies and waits with the blocking stream sync.  K0
-// is one launch of one 256-thread workgroup:
-//   * the table image is filled from registers: thread x loads T0[x] once and writes its
-//     entry's copies (encrypt: copies 0..3 only, the chain's quad reads nothing else);
-//   * the call's bytes are read from and written back to the engine's pinned staging
-//     directly over PCIe (one coalesced burst each way through an LDS buffer);
-//   * completion is a sequence number the kernel stores to pinned memory after its
-//     results (system-scope release); the host spins on it instead of sleeping in
-//     hipStreamSynchronize.
+// call moved its bytes with three DMA copies and waited in the blocking stream sync.
+//   K0  k_cfb_single : one launch of one 256-thread workgroup per call.  The table image is
+//       filled from registers (thread x loads T0[x] once); the bytes are read from and
+//       written back to the engine's pinned staging directly over PCIe; completion is a
+//       sequence number the kernel stores to pinned memory after its results
+//       (system-scope release), on which the host spins.
+//   K0s k_cfb_server : the same call body in a workgroup that stays resident while calls
+//       keep coming: it polls a mailbox in pinned host memory, serves each request and
+//       publishes its sequence number; between requests it checks an idle interval, a
+//       lifetime bound and a stop flag, and leaves on any of them.  No launch, no table
+//       fill and no kernel-argument fetch per call; the host relaunches it once it has left.
 // Decrypt: one lane per 16-byte block (block i's keystream is E(C_{i-1})).  Encrypt: the
 // serial chain on one quad (K2c's column round, coop.hpp) -- C_i = P_i ^ E(C_{i-1}).
 #include "coop.hpp"
@@ -26,15 +28,17 @@ namespace {
 
 constexpr int kSmallThreads = 256;
 
-__device__ __forceinline__ void store_seq(uint32_t *p, uint32_t v) {
+__device__ __forceinline__ void store_release(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint32_t load_acquire(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // LDS image: copies [0, ncopies) of every (table, x) entry (the layout of aes_device.hpp)
-template <int NT>
-__device__ __forceinline__ void fill_tables_regs(uint4 *lds4, const uint32_t *__restrict__ t0le, int ncopies) {
+__device__ __forceinline__ void fill_tables_regs(uint4 *lds4, uint32_t v0, int ncopies) {
     const uint32_t x = threadIdx.x;  // kSmallThreads == 256 entries
-    const uint32_t v0 = t0le[x];
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
         const uint32_t v = rotl32(v0, 8u * k);
@@ -44,43 +48,40 @@ __device__ __forceinline__ void fill_tables_regs(uint4 *lds4, const uint32_t *__
     }
 }
 
+struct SmallShared {
+    uint4 buf[kSmallMaxBytes / 16 + 2];  // head block + body + one spare (prefetch)
+    uint32_t fhead[4], fout[4];          // feedback register after the head / after the call
+};
+
+// One call (after buf[0..nb] holds the staging's blocks): head, body, write-back, and the
+// (ivec, pos) result into state[0..4].  Every thread of the workgroup calls it.
 template <int NR, bool ENCRYPT>
-__global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
-    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
-    __shared__ uint4 buf[kSmallMaxBytes / 16 + 2];  // head block + body + one spare (prefetch)
-    __shared__ uint32_t fhead[4], fout[4];  // feedback register after the head / after the call
+__device__ __forceinline__ void small_body(uint32_t len, uint32_t head, uint32_t pos, uint4 iv, const uint32_t *rkp,
+                                           uint4 *io, uint32_t *state, const uint4 *lds4, SmallShared &S) {
     const uint32_t t = threadIdx.x;
-    // the call's bytes: the body starts at io + kSmallBodyAt (16-aligned), the head's
-    // bytes (pos != 0: the rest of the current keystream block) sit right before it
-    const uint32_t rem = a.len - a.head, r = rem & 15u;
+    const uint32_t rem = len - head, r = rem & 15u;
     const uint32_t nb = (rem + 15) >> 4;  // body blocks, the last one partial when r != 0
-    uint4 *io = reinterpret_cast<uint4 *>(a.io + kSmallBodyAt - 16);
-    // first PCIe read in flight before the table fill (both wait on memory, not on each other)
-    const uint4 first = t <= nb ? io[t] : make_uint4(0, 0, 0, 0);
-    fill_tables_regs<4>(lds4, a.t0le, ENCRYPT ? 4 : 32);
-    if (t <= nb) buf[t] = first;  // buf[0]: the head bytes at its end
-    for (uint32_t i = t + kSmallThreads; i <= nb; i += kSmallThreads) buf[i] = io[i];
-    __syncthreads();
+    uint4 *buf = S.buf;
     if (t == 0) {  // head: ivec bytes [pos, pos + head) are keystream already (base/rijndael.c:1180-1195)
-        uint8_t *fb = reinterpret_cast<uint8_t *>(fhead);
-        *reinterpret_cast<uint4 *>(fhead) = a.iv;
-        uint8_t *hb = reinterpret_cast<uint8_t *>(&buf[0]) + 16 - a.head;
-        for (uint32_t j = 0; j < a.head; j++) {
+        uint8_t *fb = reinterpret_cast<uint8_t *>(S.fhead);
+        *reinterpret_cast<uint4 *>(S.fhead) = iv;
+        uint8_t *hb = reinterpret_cast<uint8_t *>(&buf[0]) + 16 - head;
+        for (uint32_t j = 0; j < head; j++) {
             const uint8_t c = hb[j];
-            const uint8_t o = c ^ fb[a.pos + j];
+            const uint8_t o = c ^ fb[pos + j];
             hb[j] = o;
-            fb[a.pos + j] = ENCRYPT ? o : c;  // the feedback is always the ciphertext byte
+            fb[pos + j] = ENCRYPT ? o : c;  // the feedback is always the ciphertext byte
         }
-        *reinterpret_cast<uint4 *>(fout) = *reinterpret_cast<const uint4 *>(fhead);  // nb == 0
+        *reinterpret_cast<uint4 *>(S.fout) = *reinterpret_cast<const uint4 *>(S.fhead);  // nb == 0
     }
     __syncthreads();
-    const uint4 f0 = *reinterpret_cast<const uint4 *>(fhead);
+    const uint4 f0 = *reinterpret_cast<const uint4 *>(S.fhead);
     if (ENCRYPT) {
         if (t < 4) {  // the chain on one quad: lane q owns column q (coop.hpp)
             const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
             uint32_t rkq[NR + 1];
 #pragma unroll
-            for (int k = 0; k <= NR; k++) rkq[k] = a.rk[4 * k + t];
+            for (int k = 0; k <= NR; k++) rkq[k] = rkp[4 * k + t];
             uint32_t fq = word_of(f0, (int)t);
             uint32_t *bw = reinterpret_cast<uint32_t *>(buf + 1);
             uint32_t pw = nb ? bw[t] : 0u;  // P_i, loaded one block ahead of its use
@@ -98,34 +99,130 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
                     fq = (c & m) | (k & ~m);
                 }
             }
-            if (nb) fout[t] = fq;
+            if (nb) S.fout[t] = fq;
         }
         __syncthreads();
         for (uint32_t i = t; i <= nb; i += kSmallThreads) io[i] = buf[i];
     } else {  // one lane per block; plaintext straight back to the staging
         const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
-        const RoundKeys<NR> rk = *reinterpret_cast<const RoundKeys<NR> *>(a.rk);
+        const RoundKeys<NR> rk = *reinterpret_cast<const RoundKeys<NR> *>(rkp);
         for (uint32_t i = t; i < nb; i += kSmallThreads) {
             const uint4 k = aes_encrypt_block<NR, 4>(i ? buf[i] : f0, rk, T);  // buf[i] = C_{i-1}
             const uint4 c = buf[i + 1];
             io[i + 1] = c ^ k;
             if (i + 1 == nb)  // ivec after the call: the last C block, or C bytes [0, r) + K
-                *reinterpret_cast<uint4 *>(fout) = r ? select_bytes(byte_mask(0, (int)r), c, k) : c;
+                *reinterpret_cast<uint4 *>(S.fout) = r ? select_bytes(byte_mask(0, (int)r), c, k) : c;
         }
         __syncthreads();
         if (t == 0) io[0] = buf[0];
     }
     if (t == 0) {
-        uint32_t *st = a.state;
-        st[0] = fout[0];
-        st[1] = fout[1];
-        st[2] = fout[2];
-        st[3] = fout[3];
-        st[4] = nb ? r : (a.pos + a.head) & 15u;
+        state[0] = S.fout[0];
+        state[1] = S.fout[1];
+        state[2] = S.fout[2];
+        state[3] = S.fout[3];
+        state[4] = nb ? r : (pos + head) & 15u;
     }
+}
+
+template <int NR, bool ENCRYPT>
+__global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    __shared__ SmallShared S;
+    const uint32_t t = threadIdx.x;
+    // the call's bytes: the body starts at io + kSmallBodyAt (16-aligned), the head's
+    // bytes (pos != 0: the rest of the current keystream block) sit right before it
+    const uint32_t nb = (a.len - a.head + 15) >> 4;
+    uint4 *io = reinterpret_cast<uint4 *>(a.io + kSmallBodyAt - 16);
+    // first PCIe read in flight before the table fill (both wait on memory, not on each other)
+    const uint4 first = t <= nb ? io[t] : make_uint4(0, 0, 0, 0);
+    fill_tables_regs(lds4, a.t0le[t], ENCRYPT ? 4 : 32);  // encrypt: the chain's quad reads copies 0..3
+    if (t <= nb) S.buf[t] = first;  // buf[0]: the head bytes at its end
+    for (uint32_t i = t + kSmallThreads; i <= nb; i += kSmallThreads) S.buf[i] = io[i];
+    __syncthreads();
+    small_body<NR, ENCRYPT>(a.len, a.head, a.pos, a.iv, a.rk, io, a.state, lds4, S);
     __threadfence_system();
     __syncthreads();
-    if (t == 0) store_seq(a.state + 5, a.seq);
+    if (t == 0) store_release(a.state + 5, a.seq);
+}
+
+// K0s.  Mailbox (pinned host memory, kernels.hpp SmallMailbox): the host writes a request
+// (fields, then its sequence number with a release store), the server serves every new
+// sequence number in order and stores it into resp.done after the results.
+__global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *mb, const uint32_t *t0le,
+                                                                 uint32_t epoch, uint64_t idle_ticks,
+                                                                 uint64_t life_ticks) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    __shared__ SmallShared S;
+    __shared__ SmallReq rq;
+    __shared__ uint32_t ctl[2][4];  // [iteration parity][action, sequence number, body blocks]
+    const uint32_t t = threadIdx.x;
+    fill_tables_regs(lds4, t0le[t], 32);
+    uint32_t done = 0;
+    uint64_t t_start = 0, t_idle = 0;
+    if (t == 0) {
+        done = load_acquire(&mb->resp.done);
+        t_start = t_idle = wall_clock64();
+    }
+    __syncthreads();
+    uint4 *io = reinterpret_cast<uint4 *>(mb->io + kSmallBodyAt - 16);
+    for (uint32_t it = 0;; it++) {
+        if (t == 0) {  // 0 = nothing yet, 1 = serve, 2 = leave
+            const uint32_t s = load_acquire(&mb->req.seq);
+            const uint64_t now = wall_clock64();
+            uint32_t action = 0;
+            uint32_t nb = 0;
+            if (s != done) {
+                action = 1;
+                nb = (mb->req.len - mb->req.head + 15) >> 4;  // (after the acquire of seq)
+                nb = nb < kSmallMaxBytes / 16 ? nb : kSmallMaxBytes / 16;  // the host never asks for more
+            } else if (__hip_atomic_load(&mb->req.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                       now - t_idle > idle_ticks || now - t_start > life_ticks) {
+                action = 2;
+            }
+            ctl[it & 1][0] = action;
+            ctl[it & 1][1] = s;
+            ctl[it & 1][2] = nb;
+        }
+        __syncthreads();
+        const uint32_t action = ctl[it & 1][0], s = ctl[it & 1][1], nb = ctl[it & 1][2];
+        if (action == 2) break;
+        if (action == 0) {
+            __builtin_amdgcn_s_sleep(4);
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this wave sees the host's request
+        // request header and the call's bytes into LDS
+        if (t < sizeof(SmallReq) / 16)
+            reinterpret_cast<uint4 *>(&rq)[t] = reinterpret_cast<const uint4 *>(&mb->req)[t];
+        for (uint32_t i = t; i <= nb; i += kSmallThreads) S.buf[i] = io[i];
+        __syncthreads();
+        const uint4 iv = make_uint4(rq.iv[0], rq.iv[1], rq.iv[2], rq.iv[3]);
+        uint32_t *st = mb->resp.state;
+        const bool enc = rq.op & 1u;
+        switch (rq.nrounds) {
+            case 10:
+                if (enc) small_body<10, true>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                else small_body<10, false>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                break;
+            case 12:
+                if (enc) small_body<12, true>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                else small_body<12, false>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                break;
+            default:
+                if (enc) small_body<14, true>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                else small_body<14, false>(rq.len, rq.head, rq.pos, iv, rq.rk, io, st, lds4, S);
+                break;
+        }
+        __threadfence_system();
+        __syncthreads();
+        if (t == 0) {
+            store_release(&mb->resp.done, s);
+            done = s;
+            t_idle = wall_clock64();
+        }
+    }
+    if (t == 0) store_release(&mb->resp.exited, epoch);
 }
 
 }  // namespace
@@ -144,6 +241,13 @@ hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipS
         default: return hipErrorInvalidValue;
     }
 #undef FPNN_K0
+    return hipGetLastError();
+}
+
+hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
+                             uint64_t life_ticks, hipStream_t st) {
+    set_launched("cfb_server");
+    hipLaunchKernelGGL(k_cfb_server, dim3(1), dim3(kSmallThreads), 0, st, mb, t0le, epoch, idle_ticks, life_ticks);
     return hipGetLastError();
 }
 

@@ -191,6 +191,27 @@ struct SmallArgs {
     uint32_t *state;
 };
 hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipStream_t st);
+// K0s (k_small.hip): the resident form of K0 behind a mailbox in pinned host memory.  The
+// host fills req (seq last, release), the server serves each new seq and stores it into
+// resp.done after the results (io in place, resp.state = ivec + pos); it leaves after
+// idle_ticks without a request, after life_ticks in any case, or when req.stop is set,
+// storing its epoch into resp.exited.  Ticks of the device wall clock (wall_clock64).
+struct alignas(16) SmallReq {
+    uint32_t seq, op, len, head, pos, nrounds, stop, pad;  // op bit 0: encrypt
+    uint32_t iv[4];
+    uint32_t rk[60];  // block byte order
+};
+struct alignas(64) SmallResp {
+    uint32_t done, exited, pad[2];
+    uint32_t state[8];  // ivec (4 words), pos
+};
+struct SmallMailbox {
+    SmallReq req;
+    SmallResp resp;
+    alignas(64) uint8_t io[kSmallBodyAt + kSmallMaxBytes + 64];
+};
+hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
+                             uint64_t life_ticks, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
 // Host-mapped frame moves: a job copies n segments, segment i from address sbase + soff[i]
