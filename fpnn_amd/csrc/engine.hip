@@ -2145,7 +2145,9 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     // ---- streams in array order (stable counting sort by slot, as host_pipeline) ----
     // (Round 3 measured a parallel sort plus parallel piece building -- per-range
     // histograms, two pool passes per chunk -- at 22-25 GiB/s against this serial form's
-    // 27-29 on the same box: tools/gpu_r03t.sh.)
+    // 27-29 on the same box.)
+    HostStats hst;
+    const double t_call = hst.on ? HostStats::now() : 0;
     std::vector<uint32_t> order(n);
     {
         std::vector<uint32_t> cnt((size_t)keys->count + 1, 0);
@@ -2153,23 +2155,44 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
         for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
     }
+    // The frames themselves in that order (gathered on the host pool): the serial quota
+    // walk below then reads them sequentially -- in arrival order a stream's frames lie
+    // one stream-count apart, a cache and TLB miss each.  Opt-in (FPNN_AES_MAP_SORTED=1)
+    // until it is measured on the box; the default walks frames[order[i]].
+    static const bool sorted_copy = [] {
+        const char *x = getenv("FPNN_AES_MAP_SORTED");
+        return x && atoi(x) != 0;
+    }();
+    std::vector<fpnn_aes_host_frame> sfv;
+    const fpnn_aes_host_frame *sf = frames;  // sf[k] = frames[order[k]] (via ord)
+    const uint32_t *ord = order.data();
+    if (sorted_copy) {
+        sfv.resize(n);
+        const unsigned parts = n >= 16384 ? pool_of(e)->parts() : 1u;
+        pool_of(e)->run(parts, [&](unsigned p) {
+            const uint32_t a0 = (uint32_t)((uint64_t)n * p / parts), b0 = (uint32_t)((uint64_t)n * (p + 1) / parts);
+            for (uint32_t k = a0; k < b0; k++) sfv[k] = frames[order[k]];
+        });
+        sf = sfv.data();
+        ord = nullptr;
+    }
+    auto frame_at = [&](uint32_t k) -> const fpnn_aes_host_frame & { return ord ? sf[ord[k]] : sf[k]; };
     struct SSeg {
         uint32_t slot, first, nframes;
         uint64_t bytes;
     };
     std::vector<SSeg> segs;
     for (uint32_t i = 0; i < n;) {
-        const uint32_t slot = frames[order[i]].key_slot;
+        const uint32_t slot = frame_at(i).key_slot;
         uint32_t j = i;
         uint64_t bytes = 0;
-        while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
+        while (j < n && frame_at(j).key_slot == slot) bytes += frame_at(j++).len;
         if (bytes) segs.push_back({slot, i, j - i, bytes});
         i = j;
     }
     if (segs.empty()) return FPNN_AES_OK;
     const uint64_t nseg = segs.size();
-    HostStats hst;
-    const double t_call = hst.on ? HostStats::now() : 0;
+    const double t_sorted = hst.on ? HostStats::now() : 0;
     DeviceGuard g(e->device);
     for (auto &m : e->ms)
         if (int rc = mslot_reserve(m, 0, 0)) return rc;
@@ -2254,8 +2277,8 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             const uint64_t take = std::min(rem[s], quota);
             uint64_t took = 0;
             while (took < take) {
-                const uint32_t fidx = order[sg.first + fi[s]];
-                const fpnn_aes_host_frame &f = frames[fidx];
+                const uint32_t fidx = sg.first + fi[s];  // sorted position
+                const fpnn_aes_host_frame &f = frame_at(fidx);
                 const uint32_t part = (uint32_t)std::min<uint64_t>(f.len - fo[s], take - took);
                 if (part) pieces.push_back({fidx, fo[s], part});
                 took += part;
@@ -2302,7 +2325,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             long rs = -1, rd = -1;
             for (uint32_t q = a0; q < b0; q++) {
                 const Piece &pc = pieces[q];
-                const fpnn_aes_host_frame &f = frames[pc.frame];
+                const fpnn_aes_host_frame &f = frame_at(pc.frame);
                 const uintptr_t xs = (uintptr_t)f.src + pc.off, xd = (uintptr_t)f.dst + pc.off;
                 if (rs < 0 || xs < v.lo[rs] || xs + pc.len > v.hi[rs]) rs = v.find((const void *)xs, pc.len);
                 if (rd < 0 || xd < v.lo[rd] || xd + pc.len > v.hi[rd]) rd = v.find((const void *)xd, pc.len);
@@ -2399,10 +2422,10 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     }
     e->host_path = "host_mapped";
     if (hst.on)
-        fprintf(stderr, "[fpnn_aes host] mapped stream %s: %u frames, %llu streams, %.2f ms total, descriptors %.2f, "
-                "slot waits %.2f, final drain %.2f ms\n", encrypt ? "encrypt" : "decrypt", n,
-                (unsigned long long)nseg, 1e3 * (HostStats::now() - t_call), 1e3 * hst.gather, 1e3 * hst.wait,
-                1e3 * (HostStats::now() - td));
+        fprintf(stderr, "[fpnn_aes host] mapped stream %s: %u frames, %llu streams, %.2f ms total, sort %.2f, "
+                "descriptors %.2f, slot waits %.2f, final drain %.2f ms%s\n", encrypt ? "encrypt" : "decrypt", n,
+                (unsigned long long)nseg, 1e3 * (HostStats::now() - t_call), 1e3 * (t_sorted - t_call),
+                1e3 * hst.gather, 1e3 * hst.wait, 1e3 * (HostStats::now() - td), sorted_copy ? " (sorted copy)" : "");
     return rc;
 }
 

@@ -6,7 +6,9 @@
 timing run exactly as on an 8-GPU node, over gloo.  Each rank encrypts its own contiguous
 shard of the global C4 / C5 batch and checks the ciphertext against the reference's
 digest for that shard (tests/golden/digests.json "shards", made through oracle/_ref by
-oracle/gen_golden.py); the line must report every rank checked and matching.
+oracle/gen_golden.py); the line must report every rank checked and matching.  World 8 is
+the driver's 8-GPU layout rehearsed on one card (8 rank processes, within the box's limit
+of 16 processes on the GPU).
 """
 import json
 import os
@@ -27,7 +29,7 @@ def _env():
     return env
 
 
-@pytest.mark.parametrize("workload,world", [("C4", 2), ("C5", 2), ("C4", 4), ("C5", 4)])
+@pytest.mark.parametrize("workload,world", [("C4", 2), ("C5", 2), ("C4", 4), ("C5", 4), ("C4", 8), ("C5", 8)])
 def test_sharded_config_every_rank_matches_reference(workload, world):
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--workload", workload,
            "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]

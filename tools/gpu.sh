@@ -15,6 +15,8 @@
 #   configs          tools/bench_configs.py --no-host, every device config (steady-state medians)
 #   configs:<list>   the same for a comma list, e.g. configs:C4,R1
 #   host             tools/bench_configs.py --configs C2,S1 with the host / PCIe legs
+#   s1ab             S1 (stream host frames) with the host-stats breakdown, walk vs sorted
+#                    copy (FPNN_AES_MAP_SORTED), alternating twice on one box
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
@@ -70,6 +72,10 @@ for step in "$@"; do
     configs) run configs 700 python -u tools/bench_configs.py --reps 3 --no-host ;;
     configs:*) run "configs_${step#configs:}" 600 python -u tools/bench_configs.py --reps 3 --no-host --configs "${step#configs:}" ;;
     host) run host 600 python -u tools/bench_configs.py --reps 3 --configs C2,S1 ;;
+    s1ab) for i in 1 2; do
+        FPNN_AES_HOST_STATS=1 FPNN_AES_MAP_SORTED=0 run "s1_walk$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
+        FPNN_AES_HOST_STATS=1 FPNN_AES_MAP_SORTED=1 run "s1_sorted$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
+      done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
     percall) run percall 300 python -u tools/bench_percall.py ;;
     percall_trace) percall_exe
