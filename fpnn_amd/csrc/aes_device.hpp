@@ -430,6 +430,11 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// Lane l receives lane (l-1)'s value, lane 0 lane 63's: DPP wave_ror:1.
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, true);
+}
+
 // Same with 0 into lane 0 (bound_ctrl: no "old" register to materialise).
 __device__ __forceinline__ uint32_t wave_shr1_zero(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);

@@ -227,7 +227,8 @@ struct fpnn_aes_engine {
     uint64_t cap_sstate = 0;
     uint8_t *h_sstate = nullptr;  // its pinned twin
     uint64_t cap_hsstate = 0;
-    bool pools = false;            // stream-ordered allocation (hipMallocAsync) for grow()
+    bool pools = false;            // stream-ordered allocation from `pool` for grow()
+    hipMemPool_t mpool = nullptr;  // the engine's own memory pool (keeps freed scratch for reuse)
     std::vector<void *> deferred;  // grown-out scratch awaiting an idle stream (no pools)
     // K0 (k_small.hip): pinned staging of the small synchronous calls, its device view,
     // and the sequence number the kernel stores when a call is done
@@ -296,8 +297,8 @@ struct DeviceGuard {
 // Scratch growth on the call path never frees synchronously: hipFree waits for the whole
 // device, so one thread's first large call would stall every other engine's queued work.
 // With stream-ordered pools the old buffer is released by hipFreeAsync behind the work
-// already queued on this engine's stream; without them it is kept until engine_sync /
-// engine_destroy.
+// already queued on this engine's stream; without them it is kept until the stream is
+// next idle (engine_sync, the end of a synchronous host call, engine_destroy).
 template <class T>
 int grow(fpnn_aes_engine *e, T *&ptr, uint64_t &cap, uint64_t need) {
     if (need <= cap) return FPNN_AES_OK;
@@ -305,7 +306,7 @@ int grow(fpnn_aes_engine *e, T *&ptr, uint64_t &cap, uint64_t need) {
     while (n < need) n *= 2;
     T *np = nullptr;
     if (e->pools)
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&np), n * sizeof(T), e->stream));
+        HIP_TRY(hipMallocFromPoolAsync(reinterpret_cast<void **>(&np), n * sizeof(T), e->mpool, e->stream));
     else
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&np), n * sizeof(T)));
     if (ptr) {
@@ -539,6 +540,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             if (!k.len) k.len = e->d_desc_len;
         }
         if (!k.out_off) k.out_off = k.in_off;
+        k.runs = (uint32_t)e->variant.k1r_runs;
         EventPair *ev = nullptr;
         if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
         // in place (in == out, identical offsets: fpnn_aes.h) the predecessor blocks of the
@@ -631,16 +633,27 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
-    {  // stream-ordered scratch allocation; the pool keeps freed memory for reuse
+    if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
+    {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed
+       // memory for reuse (release threshold: never) without changing the device's
+       // default pool, which other code in the process allocates from
         int pools = 0;
         const char *v = getenv("FPNN_AES_POOLS");
         if ((!v || atoi(v) != 0) &&
             hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device) == hipSuccess && pools) {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            hipMemPoolProps props;
+            memset(&props, 0, sizeof props);
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = device;
+            if (hipMemPoolCreate(&e->mpool, &props) == hipSuccess) {
                 uint64_t keep = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+                (void)hipMemPoolSetAttribute(e->mpool, hipMemPoolAttrReleaseThreshold, &keep);
                 e->pools = true;
+            } else {
+                (void)hipGetLastError();
+                e->mpool = nullptr;
             }
         }
     }
@@ -683,6 +696,10 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         release_scratch(e, p);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_deferred(e);
+    if (e->mpool) {  // (its blocks were freed above, behind the stream)
+        (void)hipStreamSynchronize(e->stream);
+        (void)hipMemPoolDestroy(e->mpool);
+    }
     (void)hipFree(e->d_total);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -1257,6 +1274,7 @@ int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const
     HIP_TRY(hipMemcpyAsync(h_iv, a.iv, 32, hipMemcpyDeviceToHost, e->stream));
     if (out_copy) HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + ipad, a.out, out_copy, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    free_deferred(e);  // the stream is idle: grown-out scratch can go
     if (out_copy) memcpy(out, e->h_stage + hdr + ipad, out_copy);
     if (ivec && mode != MODE_CBC_DEC) memcpy(ivec, h_iv, 16);
     if (p_num) *p_num = *h_pos;
@@ -1348,6 +1366,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     HIP_TRY(hipMemcpyAsync(h_iv, d_iv, 32, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + pay, e->d_stage + hdr + pay, len, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    free_deferred(e);  // the stream is idle: grown-out scratch can go
     memcpy(out, e->h_stage + hdr + pay, len);
     memcpy(ivec, h_iv, 16);
     *p_num = *h_pos;
@@ -1472,6 +1491,51 @@ int sstate_reserve(fpnn_aes_engine *e, uint64_t bytes) {
     return FPNN_AES_OK;
 }
 
+// Stream-mode host frames grouped by stream: order[] lists the frame indices by key slot,
+// each stream's frames in array order (a stable sort), and segs the streams that carry
+// bytes, in slot order ({slot, first, nframes, bytes}: frames order[first .. +nframes)).
+// A serial counting sort whose first pass also sums each slot's bytes, so the segments
+// come from the histogram, not from a walk of frames[order[i]] (one cache miss per frame
+// in arrival order).  A parallel form on the host pool (per-part histograms, prefix over
+// slot ranges, per-part placement) measured 5-8 ms per 1M frames on the GPU box against
+// this form's 3 (S1, gpurun_out r04k / r04l): four pool passes over a 16-CPU share cost
+// more than they split.  Sparse slot ranges take std::stable_sort.
+struct StreamSeg {
+    uint32_t slot, first, nframes;
+    uint64_t bytes;
+};
+
+void group_streams(const fpnn_aes_host_frame *frames, uint32_t n, uint32_t nkeys, std::vector<uint32_t> &order,
+                   std::vector<StreamSeg> &segs) {
+    order.resize(n);
+    segs.clear();
+    if ((uint64_t)nkeys > 4ull * n + 1024) {  // sparse
+        for (uint32_t i = 0; i < n; i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [frames](uint32_t x, uint32_t y) { return frames[x].key_slot < frames[y].key_slot; });
+        for (uint32_t i = 0; i < n;) {
+            const uint32_t slot = frames[order[i]].key_slot;
+            uint32_t j = i;
+            uint64_t bytes = 0;
+            while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
+            if (bytes) segs.push_back({slot, i, j - i, bytes});  // empty streams keep their state
+            i = j;
+        }
+        return;
+    }
+    std::vector<uint32_t> cnt((size_t)nkeys + 1, 0);
+    std::vector<uint64_t> byt(nkeys, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        cnt[frames[i].key_slot + 1]++;
+        byt[frames[i].key_slot] += frames[i].len;
+    }
+    for (uint32_t k = 0; k < nkeys; k++) {
+        if (byt[k]) segs.push_back({k, cnt[k], cnt[k + 1], byt[k]});
+        cnt[k + 1] += cnt[k];
+    }
+    for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
+}
+
 // Host-frame pipeline shared by the package and stream entry points.
 //   package: one segment per frame (key slot frames[i].key_slot, fresh chain).
 //   stream : one segment per distinct stream slot = the concatenation of that
@@ -1489,35 +1553,8 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
     const uint64_t kChunk = 32ull << 20;  // input bytes per pipeline chunk
     // ---- segments in staging order -------------------------------------------------
     std::vector<uint32_t> order;  // frame indices
-    struct Seg {
-        uint32_t slot, first, nframes;  // frames order[first .. first+nframes)
-        uint64_t bytes;
-    };
-    std::vector<Seg> segs;  // stream mode only (package chunks walk `frames` directly)
-    if (stream) {
-        // stable counting sort by stream slot (slots are < keys->count)
-        std::vector<uint32_t> cnt;
-        const bool dense = (uint64_t)keys->count <= 4ull * n + 1024;
-        order.resize(n);
-        if (dense) {
-            cnt.assign((size_t)keys->count + 1, 0);
-            for (uint32_t i = 0; i < n; i++) cnt[frames[i].key_slot + 1]++;
-            for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
-            for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
-        } else {
-            for (uint32_t i = 0; i < n; i++) order[i] = i;
-            std::stable_sort(order.begin(), order.end(),
-                             [frames](uint32_t x, uint32_t y) { return frames[x].key_slot < frames[y].key_slot; });
-        }
-        for (uint32_t i = 0; i < n;) {
-            const uint32_t slot = frames[order[i]].key_slot;
-            uint32_t j = i;
-            uint64_t bytes = 0;
-            while (j < n && frames[order[j]].key_slot == slot) bytes += frames[order[j++]].len;
-            if (bytes) segs.push_back({slot, i, j - i, bytes});  // empty streams keep their state
-            i = j;
-        }
-    }
+    std::vector<StreamSeg> segs;  // stream mode only (package chunks walk `frames` directly)
+    if (stream) group_streams(frames, n, keys->count, order, segs);
     if (stream && segs.empty()) return FPNN_AES_OK;
     e->host_path = "host_staged";
     const uint64_t nseg = stream ? segs.size() : n;
@@ -1673,7 +1710,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             while (sr.rem[t] == 0) t = t + 1 < nseg ? t + 1 : 0;  // left_total > 0: terminates
             state0 = t;
             for (; t < nseg && in_b < sr.chunk; t++) {
-                const Seg &sg = segs[t];
+                const StreamSeg &sg = segs[t];
                 const uint64_t take = std::min(sr.rem[t], sr.quota);
                 uint64_t took = 0;
                 while (took < take) {
@@ -2114,6 +2151,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
     const double td = hst.on ? HostStats::now() : 0;
     HIP_TRY(hipStreamSynchronize(ms));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    free_deferred(e);  // the stream is idle: grown-out scratch can go
     for (auto &m : e->ms) m.busy = false;
     for (auto &c : ch) c.cnt = 0;
     *done = si;
@@ -2142,54 +2180,12 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         return (x && atoi(x) > 0 ? (uint64_t)atoi(x) : 32ull) << 20;
     }();
     constexpr int kSlots = (int)(sizeof(e->ms) / sizeof(e->ms[0]));
-    // ---- streams in array order (stable counting sort by slot, as host_pipeline) ----
-    // (Round 3 measured a parallel sort plus parallel piece building -- per-range
-    // histograms, two pool passes per chunk -- at 22-25 GiB/s against this serial form's
-    // 27-29 on the same box.)
+    // ---- streams in array order (group_streams) ----
     HostStats hst;
     const double t_call = hst.on ? HostStats::now() : 0;
-    std::vector<uint32_t> order(n);
-    {
-        std::vector<uint32_t> cnt((size_t)keys->count + 1, 0);
-        for (uint32_t i = 0; i < n; i++) cnt[frames[i].key_slot + 1]++;
-        for (uint32_t k = 0; k < keys->count; k++) cnt[k + 1] += cnt[k];
-        for (uint32_t i = 0; i < n; i++) order[cnt[frames[i].key_slot]++] = i;
-    }
-    // The frames themselves in that order (gathered on the host pool): the serial quota
-    // walk below then reads them sequentially -- in arrival order a stream's frames lie
-    // one stream-count apart, a cache and TLB miss each.  Opt-in (FPNN_AES_MAP_SORTED=1)
-    // until it is measured on the box; the default walks frames[order[i]].
-    static const bool sorted_copy = [] {
-        const char *x = getenv("FPNN_AES_MAP_SORTED");
-        return x && atoi(x) != 0;
-    }();
-    std::vector<fpnn_aes_host_frame> sfv;
-    const fpnn_aes_host_frame *sf = frames;  // sf[k] = frames[order[k]] (via ord)
-    const uint32_t *ord = order.data();
-    if (sorted_copy) {
-        sfv.resize(n);
-        const unsigned parts = n >= 16384 ? pool_of(e)->parts() : 1u;
-        pool_of(e)->run(parts, [&](unsigned p) {
-            const uint32_t a0 = (uint32_t)((uint64_t)n * p / parts), b0 = (uint32_t)((uint64_t)n * (p + 1) / parts);
-            for (uint32_t k = a0; k < b0; k++) sfv[k] = frames[order[k]];
-        });
-        sf = sfv.data();
-        ord = nullptr;
-    }
-    auto frame_at = [&](uint32_t k) -> const fpnn_aes_host_frame & { return ord ? sf[ord[k]] : sf[k]; };
-    struct SSeg {
-        uint32_t slot, first, nframes;
-        uint64_t bytes;
-    };
-    std::vector<SSeg> segs;
-    for (uint32_t i = 0; i < n;) {
-        const uint32_t slot = frame_at(i).key_slot;
-        uint32_t j = i;
-        uint64_t bytes = 0;
-        while (j < n && frame_at(j).key_slot == slot) bytes += frame_at(j++).len;
-        if (bytes) segs.push_back({slot, i, j - i, bytes});
-        i = j;
-    }
+    std::vector<uint32_t> order;
+    std::vector<StreamSeg> segs;
+    group_streams(frames, n, keys->count, order, segs);
     if (segs.empty()) return FPNN_AES_OK;
     const uint64_t nseg = segs.size();
     const double t_sorted = hst.on ? HostStats::now() : 0;
@@ -2273,12 +2269,12 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
         c.state0 = s;
         uint64_t in_b = 0;
         for (; s < nseg && in_b < chunk; s++) {
-            const SSeg &sg = segs[s];
+            const StreamSeg &sg = segs[s];
             const uint64_t take = std::min(rem[s], quota);
             uint64_t took = 0;
             while (took < take) {
-                const uint32_t fidx = sg.first + fi[s];  // sorted position
-                const fpnn_aes_host_frame &f = frame_at(fidx);
+                const uint32_t fidx = order[sg.first + fi[s]];
+                const fpnn_aes_host_frame &f = frames[fidx];
                 const uint32_t part = (uint32_t)std::min<uint64_t>(f.len - fo[s], take - took);
                 if (part) pieces.push_back({fidx, fo[s], part});
                 took += part;
@@ -2325,7 +2321,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
             long rs = -1, rd = -1;
             for (uint32_t q = a0; q < b0; q++) {
                 const Piece &pc = pieces[q];
-                const fpnn_aes_host_frame &f = frame_at(pc.frame);
+                const fpnn_aes_host_frame &f = frames[pc.frame];
                 const uintptr_t xs = (uintptr_t)f.src + pc.off, xd = (uintptr_t)f.dst + pc.off;
                 if (rs < 0 || xs < v.lo[rs] || xs + pc.len > v.hi[rs]) rs = v.find((const void *)xs, pc.len);
                 if (rd < 0 || xd < v.lo[rd] || xd + pc.len > v.hi[rd]) rd = v.find((const void *)xd, pc.len);
@@ -2410,6 +2406,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     const double td = hst.on ? HostStats::now() : 0;
     HIP_TRY(hipStreamSynchronize(ms));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    free_deferred(e);  // the stream is idle: grown-out scratch can go
     for (auto &m : e->ms) m.busy = false;
     for (auto &c : ch) c.np = 0;
     if (!rc) {
@@ -2423,9 +2420,9 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     e->host_path = "host_mapped";
     if (hst.on)
         fprintf(stderr, "[fpnn_aes host] mapped stream %s: %u frames, %llu streams, %.2f ms total, sort %.2f, "
-                "descriptors %.2f, slot waits %.2f, final drain %.2f ms%s\n", encrypt ? "encrypt" : "decrypt", n,
+                "descriptors %.2f, slot waits %.2f, final drain %.2f ms\n", encrypt ? "encrypt" : "decrypt", n,
                 (unsigned long long)nseg, 1e3 * (HostStats::now() - t_call), 1e3 * (t_sorted - t_call),
-                1e3 * hst.gather, 1e3 * hst.wait, 1e3 * (HostStats::now() - td), sorted_copy ? " (sorted copy)" : "");
+                1e3 * hst.gather, 1e3 * hst.wait, 1e3 * (HostStats::now() - td));
     return rc;
 }
 

@@ -376,29 +376,113 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         return readlane63(X.x);
     };
 
+    // --- interior runs -------------------------------------------------------------
+    // A chunk that lies inside one segment (Dx.uni: its descriptors are in last_*) and
+    // whose blocks -- and the following chunks' -- are whole interior blocks of it (every
+    // block 16 bytes of the segment, none its first block (the IV) or, in stream mode, its
+    // last (the state export)) needs none of the general path's per-lane work: addresses
+    // are a wave-uniform base + 16 * lane, there are no edges, one key serves them all.
+    // run_at(Dx) decides that for chunk c (fetched, not yet deciphered) and sets the run's
+    // length and bases; run(x) deciphers chunks [c, c + run_m) in a loop of its own, from
+    // chunk c's ciphertext x (already in registers), the next chunk's in flight during each
+    // chunk's rounds: the cipher's own VALU cost plus ~14 instructions per chunk against
+    // the general path's ~125 (C4: 2.03 VALU per LDS instruction in round 3).  Long
+    // segments (C4's Zipf tail, R1's bodies beyond their first chunk) spend most of their
+    // chunks there.  FPNN_AES_K1R_RUNS=0 (KBatch::runs) keeps every chunk on the general
+    // path, for same-box A/B.
+    // Built for one-key AES-192/256 package batches only: with the run's code the per-key,
+    // stream and AES-128 kernels spill the general path's registers to scratch (framed C3,
+    // AES-128 per key, measured 881 against 957 GiB/s without it).
+    constexpr bool kRuns = KM == KEY_UNIFORM && NR >= 12 && !STREAM;
+    uint64_t c = c0;  // the chunk the pipeline deciphers next
+    // run parameters (wave-uniform), set by run_at; run() re-asserts their uniformity
+    // (readfirstlane) so its loop runs on scalar registers
+    uint64_t run_m = 0;
+    const uint8_t *run_ip = nullptr;
+    uint8_t *run_op = nullptr;
+    auto run_at = [&](const RDesc &Dx) -> bool {
+        if (!kRuns || !b.runs || !Dx.uni) return false;
+        const uint32_t n0 = STREAM ? last_n0 : 0u;
+        const uint64_t bi_hi = STREAM ? (uint64_t)seg_blocks(last_len, n0) - 1 : (uint64_t)(last_len >> 4);
+        uint64_t cend = (last_bs + bi_hi) >> 6;  // chunks below cend end inside the interior
+        if (cend > c1) cend = c1;
+        if ((c << 6) <= last_bs || cend <= c) return false;
+        run_m = cend - c;
+        const uint64_t lo = 16 * ((c << 6) - last_bs) - n0;  // the run's first byte in the segment
+        run_ip = b.in + last_io + lo;
+        run_op = b.out + last_oo + lo;
+        return true;
+    };
+    auto run = [&](uint4 x) {  // x = the run's first chunk, already loaded
+        const uint32_t lofs = lane * 16u;
+        const uint64_t m = readfirst64(run_m);  // (uniform again after the merge)
+        const uint8_t *ip = reinterpret_cast<const uint8_t *>(readfirst64((uint64_t)(uintptr_t)run_ip));
+        uint8_t *op = reinterpret_cast<uint8_t *>(readfirst64((uint64_t)(uintptr_t)run_op));
+        // C_{i-1}: lane 0 takes lane 63 of the chunk before (wave_ror:1 of it, lane 0 of
+        // `prev`), the other lanes their left neighbour (wave_shr:1 over prev)
+        uint4 prev = fill;
+        for (uint64_t j = 0; j < m; j++) {
+            const uint64_t jn = j + 1 < m ? j + 1 : j;
+            const uint4 xn = load16(ip + 1024 * jn + lofs);
+            const uint4 kin = make_uint4(wave_shr1(x.x, prev.x), wave_shr1(x.y, prev.y), wave_shr1(x.z, prev.z),
+                                         wave_shr1(x.w, prev.w));
+            const uint4 ks = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
+            store16(op + 1024 * j + lofs, x ^ ks);
+            prev = make_uint4(wave_ror1(x.x), wave_ror1(x.y), wave_ror1(x.z), wave_ror1(x.w));
+            x = xn;
+        }
+        fill = make_uint4(__builtin_amdgcn_readlane(prev.x, 0), __builtin_amdgcn_readlane(prev.y, 0),
+                          __builtin_amdgcn_readlane(prev.z, 0), __builtin_amdgcn_readlane(prev.w, 0));
+        c += m;
+    };
+
     // Pipeline.  The vector-memory counter retires in issue order, so a wait for a load
-    // also waits for everything issued before it.  Each half of the loop body issues the
-    // next chunk's ciphertext load and the descriptor loads of the chunk after it, THEN
-    // enciphers the current chunk: the current chunk's ciphertext was issued one cipher
-    // earlier, and the back edge follows a cipher, so the loop header (where the compiler
-    // rotates its registers and must wait for their loads) only waits for loads issued
-    // one cipher ago.  Indices past the wave's range are clamped to its last chunk
-    // (re-read, never stored).
+    // also waits for everything issued before it.  Each step issues the next chunk's
+    // ciphertext load and the descriptor loads of the chunk after it, THEN enciphers the
+    // current chunk: the current chunk's ciphertext was issued one cipher earlier, and the
+    // back edge follows a cipher, so the loop header (where the compiler rotates its
+    // registers and must wait for their loads) only waits for loads issued one cipher ago.
+    // Indices past the wave's range are clamped to its last chunk (re-read, never stored).
     const uint64_t clast = c1 - 1;
     auto cl = [&](uint64_t x) { return x < clast ? x : clast; };
     RDesc D1, D0 = locate(c0);
     RChunk X1, X0 = fetch(D0, c0);
     D1 = locate(cl(c0 + 1));
-    uint64_t c = c0;  // X0 = chunk c, D1 = descriptors of chunk c + 1
-    while (true) {
-        X1 = fetch(D1, cl(c + 1));
-        D0 = locate(cl(c + 2));
-        fill = process(X0, fill);
-        if (++c >= c1) return;
-        X0 = fetch(D0, cl(c + 1));
-        D1 = locate(cl(c + 2));
-        fill = process(X1, fill);
-        if (++c >= c1) return;
+    if constexpr (kRuns) {
+        // unrolled by two like the loop below; a run is entered from the first half only
+        // (one copy of its loop: a copy per half spills the general path's registers), so
+        // it may start one chunk late.  The pipeline restarts after it (the descriptor
+        // loads issued for the run's second chunk are dropped).
+        while (true) {
+            X1 = fetch(D1, cl(c + 1));
+            D0 = locate(cl(c + 2));
+            fill = process(X0, fill);
+            if (++c >= c1) return;
+            if (run_at(D1)) {
+                run(X1.x);
+                if (c >= c1) return;
+                D0 = locate(c);
+                X0 = fetch(D0, c);
+                D1 = locate(cl(c + 1));
+                continue;
+            }
+            X0 = fetch(D0, cl(c + 1));
+            D1 = locate(cl(c + 2));
+            fill = process(X1, fill);
+            if (++c >= c1) return;
+        }
+    } else {
+        // unrolled by two (no register rotation)
+        while (true) {
+            X1 = fetch(D1, cl(c + 1));
+            D0 = locate(cl(c + 2));
+            fill = process(X0, fill);
+            if (++c >= c1) return;
+            X0 = fetch(D0, cl(c + 1));
+            D1 = locate(cl(c + 2));
+            fill = process(X1, fill);
+            if (++c >= c1) return;
+        }
     }
 }
 
@@ -421,26 +505,20 @@ hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_
     return hipGetLastError();
 }
 
-template <int NR, bool F>
-static void ragged_nrf(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, int grid,
-                       hipStream_t st) {
-#define FPNN_RAGGED(S, K) \
-    hipLaunchKernelGGL((k_cfb_decrypt_ragged<NR, S, K, F>), dim3(grid), dim3(kThreads), 0, st, b, plan, sink)
-    if (stream) {
-        if (km == KEY_LANE) FPNN_RAGGED(true, KEY_LANE); else FPNN_RAGGED(true, KEY_UNIFORM);
-    } else {
-        if (km == KEY_LANE) FPNN_RAGGED(false, KEY_LANE); else FPNN_RAGGED(false, KEY_UNIFORM);
-    }
-#undef FPNN_RAGGED
-}
-
+// Fenced rounds everywhere except the AES-192/256 per-slot passes, which run out of SGPRs
+// for their round keys when fenced (spills).  Only the launched variants are instantiated.
 template <int NR>
 static void ragged_nr(const KBatch &b, KeyMode km, bool stream, const RaggedPlan *plan, uint4 *sink, int grid,
                       hipStream_t st) {
-    // fenced rounds, except AES-192/256 per-slot passes: those run out of SGPRs for their
-    // round keys (spills)
-    if (NR == 10 || km == KEY_UNIFORM) ragged_nrf<NR, true>(b, km, stream, plan, sink, grid, st);
-    else ragged_nrf<NR, false>(b, km, stream, plan, sink, grid, st);
+    constexpr bool kLaneFence = NR == 10;
+#define FPNN_RAGGED(S, K, F) \
+    hipLaunchKernelGGL((k_cfb_decrypt_ragged<NR, S, K, F>), dim3(grid), dim3(kThreads), 0, st, b, plan, sink)
+    if (stream) {
+        if (km == KEY_LANE) FPNN_RAGGED(true, KEY_LANE, kLaneFence); else FPNN_RAGGED(true, KEY_UNIFORM, true);
+    } else {
+        if (km == KEY_LANE) FPNN_RAGGED(false, KEY_LANE, kLaneFence); else FPNN_RAGGED(false, KEY_UNIFORM, true);
+    }
+#undef FPNN_RAGGED
 }
 
 hipError_t launch_decrypt_ragged(const KBatch &b, int nrounds, KeyMode km, bool stream, RaggedPlan *plan, uint4 *sink,

@@ -31,7 +31,7 @@ struct KBatch {
     // block map (decrypt)
     uint64_t total_blocks;   // uniform layout: exact; general: copy of *total_ptr
     uint32_t nb_uniform;     // uniform layout: blocks per segment
-    uint32_t pad0;
+    uint32_t runs;           // K1r: interior runs on (Variant::k1r_runs)
     uint64_t magic;          // ceil(2^64 / nb_uniform)
     const uint64_t *bstart;  // general: first virtual block of each segment (count + 1)
     const uint4 *boundary;   // in-place: Cx block preceding each 64-block chunk
@@ -66,6 +66,9 @@ struct Variant {
     int hyb_quad_waves = 12;
     int hyb_wire_lanes = 0;  // wire-prefix batches also use the lane session (else all quads)
     int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
+    // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
+    // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
+    int k1r_runs = 1;
 };
 
 // Base name ("cfb_decrypt_dense", ...) of the main kernel the last launch_* call on this

@@ -253,3 +253,58 @@ def test_offsets_beyond_2gib(engine, oracle, stream):
         assert np.array_equal(to_host(ivd), iv_exp) and np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
     del big
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("runs", ["0", "1"])
+@pytest.mark.parametrize("stream", [False, True])
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_interior_runs_after_key_switch(oracle, runs, stream, keylen):
+    """K1r's interior runs (FPNN_AES_K1R_RUNS, k_ragged.hip) on per-key batches whose
+    chunks end on another slot's pass: triples (short slot A, short slot B, long slot A),
+    so the chunk before a long segment's run holds A, B, A and the general path's last
+    key pass is B's.  Lengths off the block grid, gaps between segments, and in stream
+    mode random carried (ivec, pos); with runs off every chunk takes the general path."""
+    from conftest import _env_engine
+    eng = _env_engine({"FPNN_AES_K1R_RUNS": runs})
+    try:
+        rng = np.random.default_rng(4100 + 10 * keylen + 2 * stream + int(runs))
+        ntri, nkeys = 120, 8
+        lens, slots = [], []
+        for t in range(ntri):
+            a, b = (2 * t) % nkeys, (2 * t + 1) % nkeys
+            lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(2000, 9000))]
+            slots += [a, b, a]
+        lens = np.array(lens, np.int64)
+        slots = np.array(slots, np.int32)
+        n = len(lens)
+        gaps = rng.integers(0, 20, n)
+        offs = (np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])]) + 7).astype(np.int64)
+        total = int(offs[-1] + lens[-1]) + 64
+        inp = rng.integers(0, 256, total, dtype=np.uint8)
+        keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+        ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+        ks = keyset(eng, keys, keylen, ivs)
+        exp = inp.copy()
+        kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)), key_slot=to_dev(slots))
+        dst = to_dev(inp)
+        if stream:
+            iv0 = rng.integers(0, 256, 16 * n, dtype=np.uint8)
+            pos0 = rng.integers(0, 16, n).astype(np.uint32)
+            iv_h, pos_h = iv0.copy(), pos0.copy()
+            oracle.stream_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                                lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys,
+                                keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
+            iv_d, pos_d = to_dev(iv0), to_dev(pos0.astype(np.int32))
+            eng.stream_decrypt(to_dev(inp), dst, n, ks, iv_d, pos_d, **kw)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(iv_d), iv_h)
+            assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h)
+        else:
+            oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                                 key_slot=slots.astype(np.uint32), keys=keys, keylen=keylen, ivs=ivs, threads=8)
+            eng.package_decrypt(to_dev(inp), dst, n, ks, **kw)
+            torch.cuda.synchronize()
+        assert np.array_equal(to_host(dst), exp)
+    finally:
+        eng.sync()
+        eng.close()

@@ -15,11 +15,12 @@
 #   configs          tools/bench_configs.py --no-host, every device config (steady-state medians)
 #   configs:<list>   the same for a comma list, e.g. configs:C4,R1
 #   host             tools/bench_configs.py --configs C2,S1 with the host / PCIe legs
-#   s1ab             S1 (stream host frames) with the host-stats breakdown, walk vs sorted
-#                    copy (FPNN_AES_MAP_SORTED), alternating twice on one box
+#   s1               S1 (stream host frames) twice with the host-stats breakdown
+#   ab:<VAR>:<list>  same-box A/B of a dispatch knob: the configs with VAR=0, VAR=1, twice
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
+#   trace:<cfg>      rocprofv3 kernel trace (no counters) of one bench_configs config
 #   prof:<cfg>       rocprofv3 trace + 4 PMC passes of one bench_configs config (or ECDH)
 #   ecdh             tools/bench_ecdh.py
 set -o pipefail
@@ -72,15 +73,23 @@ for step in "$@"; do
     configs) run configs 700 python -u tools/bench_configs.py --reps 3 --no-host ;;
     configs:*) run "configs_${step#configs:}" 600 python -u tools/bench_configs.py --reps 3 --no-host --configs "${step#configs:}" ;;
     host) run host 600 python -u tools/bench_configs.py --reps 3 --configs C2,S1 ;;
-    s1ab) for i in 1 2; do
-        FPNN_AES_HOST_STATS=1 FPNN_AES_MAP_SORTED=0 run "s1_walk$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
-        FPNN_AES_HOST_STATS=1 FPNN_AES_MAP_SORTED=1 run "s1_sorted$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
+    s1) for i in 1 2; do
+        FPNN_AES_HOST_STATS=1 run "s1_$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
       done ;;
+    ab:*) spec=${step#ab:}; var=${spec%%:*}; cfgs=${spec#*:}
+      for i in 1 2; do for v in 0 1; do
+        env "$var=$v" timeout -k 10 300 python -u tools/bench_configs.py --reps 3 --no-host --configs "$cfgs" \
+          > "$OUT/ab_${var}_${v}_$i.log" 2>&1 || { echo "ab $var=$v failed"; tail -5 "$OUT/ab_${var}_${v}_$i.log"; exit 3; }
+        echo "   $var=$v #$i: $(grep -h '^{"configs"' "$OUT/ab_${var}_${v}_$i.log" | cut -c1-700)"
+      done; done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
     percall) run percall 300 python -u tools/bench_percall.py ;;
     percall_trace) percall_exe
       run percall_trace 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv \
         -d "$OUT/percall_prof" -o run -- "$OUT/percall_gpu" 1000 1024 ;;
+    trace:*) c=${step#trace:}; mkdir -p "$OUT/trace_$c"
+      run "trace_$c/trace" 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+        -d "$OUT/trace_$c/trace" -o run -- python3 tools/bench_configs.py --configs "$c" --reps 1 ;;
     prof:ECDH) pmc_passes prof_ECDH 'k_ecdh' python3 tools/bench_ecdh.py --curves secp256k1 --no-cpu --reps 3 ;;
     prof:*) c=${step#prof:}; pmc_passes "prof_$c" 'cfb_' python3 tools/bench_configs.py --configs "$c" --no-host --reps 3 ;;
     ecdh) run ecdh 300 python -u tools/bench_ecdh.py ;;
