@@ -36,6 +36,19 @@ __device__ __forceinline__ uint32_t load_acquire(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The first 16 bytes of the request (seq, op, len, head) in ONE system-coherent vector
+// load (sc0 sc1: past both GPU caches to host memory), so a poll that sees a new sequence
+// number has the call's header in the same PCIe round trip.  The host writes op, len and
+// head before it release-stores seq, all in this one 16-byte block of one cache line
+// (x86 stores become visible in program order, and the line is read whole), so a new seq
+// comes with its own header.  The acquire fence that follows orders the body's loads.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t load_sys16(const void *p) {
+    u32x4_t v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
 // LDS image: copies [0, ncopies) of every (table, x) entry (the layout of aes_device.hpp)
 __device__ __forceinline__ void fill_tables_regs(uint4 *lds4, uint32_t v0, int ncopies) {
     const uint32_t x = threadIdx.x;  // kSmallThreads == 256 entries
@@ -168,13 +181,15 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
     uint4 *io = reinterpret_cast<uint4 *>(mb->io + kSmallBodyAt - 16);
     for (uint32_t it = 0;; it++) {
         if (t == 0) {  // 0 = nothing yet, 1 = serve, 2 = leave
-            const uint32_t s = load_acquire(&mb->req.seq);
+            const u32x4_t h = load_sys16(&mb->req);  // seq, op, len, head
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            const uint32_t s = h.x;
             const uint64_t now = wall_clock64();
             uint32_t action = 0;
             uint32_t nb = 0;
             if (s != done) {
                 action = 1;
-                nb = (mb->req.len - mb->req.head + 15) >> 4;  // (after the acquire of seq)
+                nb = (h.z - h.w + 15) >> 4;
                 nb = nb < kSmallMaxBytes / 16 ? nb : kSmallMaxBytes / 16;  // the host never asks for more
             } else if (__hip_atomic_load(&mb->req.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
                        now - t_idle > idle_ticks || now - t_start > life_ticks) {
