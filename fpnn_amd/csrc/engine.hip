@@ -577,9 +577,10 @@ extern "C" {
 const char *fpnn_aes_last_error(void) { return g_last_error.c_str(); }
 
 const char *fpnn_aes_version(void) {
-    return "fpnn_aes 0.1 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
-           "decrypt: K1d dense/keyed, K1k lane keys, K1r ragged (no host sync), K1 uniform, one lane per block; "
-           "encrypt: K2 lane per chain, K2c quad per chain, K2h lanes + quads for ragged batches; "
+    return "fpnn_aes 0.4 (gfx950; T-tables 32-way replicated in LDS; v_perm addressing; "
+           "decrypt: K1d dense/keyed, K1k lane keys, K1r ragged (no host sync; interior runs), K1 uniform, "
+           "one lane per block; encrypt: K2 lane per chain, K2c quad per chain, K2h lanes + quads for ragged "
+           "batches; single calls <= 16 KiB: K0s resident server (K0 per launch); "
            "ECDH: one lane per derivation, special-prime folds as carry chains)";
 }
 
