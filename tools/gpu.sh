@@ -66,8 +66,8 @@ for step in "$@"; do
     tests_fast) run tests_fast 600 python -u -m pytest tests -q -m "gpu and not slow" -x --timeout 120 --timeout-method thread ;;
     tests:*) run "tests_k" 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread -k "${step#tests:}" ;;
     bench) run bench 300 python -u bench.py ;;
-    bench_trace) mkdir -p "$OUT/bench_prof"
-      run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_prof/trace" -o run -- \
+    bench_trace) mkdir -p "$OUT/bench_trace"  # (bench_pmc's own trace pass goes to bench_prof/trace)
+      run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_trace" -o run -- \
         python3 bench.py --no-cpu-baseline ;;
     bench_pmc) pmc_passes bench_prof 'cfb_' python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
     configs) run configs 700 python -u tools/bench_configs.py --reps 3 --no-host ;;
