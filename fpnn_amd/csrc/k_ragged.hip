@@ -390,10 +390,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     // segments (C4's Zipf tail, R1's bodies beyond their first chunk) spend most of their
     // chunks there.  FPNN_AES_K1R_RUNS=0 (KBatch::runs) keeps every chunk on the general
     // path, for same-box A/B.
-    // Built for one-key AES-192/256 package batches only: with the run's code the per-key,
-    // stream and AES-128 kernels spill the general path's registers to scratch (framed C3,
-    // AES-128 per key, measured 881 against 957 GiB/s without it).
-    constexpr bool kRuns = KM == KEY_UNIFORM && NR >= 12 && !STREAM;
+    // Built for one-key AES-256 package batches only: with the run's code the per-key,
+    // stream, AES-128 and AES-192 kernels spill the general path's registers to scratch
+    // (framed C3, AES-128 per key, measured 881 against 957 GiB/s without it).
+    constexpr bool kRuns = KM == KEY_UNIFORM && NR == 14 && !STREAM;
     uint64_t c = c0;  // the chunk the pipeline deciphers next
     // run parameters (wave-uniform), set by run_at; run() re-asserts their uniformity
     // (readfirstlane) so its loop runs on scalar registers

@@ -255,19 +255,20 @@ def test_offsets_beyond_2gib(engine, oracle, stream):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("runs", ["0", "1"])
+@pytest.mark.parametrize("env", [{"FPNN_AES_K1R_RUNS": "0"}, {"FPNN_AES_K1R_RUNS": "1"}], ids=["runs0", "runs1"])
 @pytest.mark.parametrize("stream", [False, True])
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_interior_runs_after_key_switch(oracle, runs, stream, keylen):
+def test_interior_runs_after_key_switch(oracle, env, stream, keylen):
     """K1r's interior runs (FPNN_AES_K1R_RUNS, k_ragged.hip) on per-key batches whose
     chunks end on another slot's pass: triples (short slot A, short slot B, long slot A),
     so the chunk before a long segment's run holds A, B, A and the general path's last
     key pass is B's.  Lengths off the block grid, gaps between segments, and in stream
-    mode random carried (ivec, pos); with runs off every chunk takes the general path."""
+    mode random carried (ivec, pos), two calls in a row; with runs off every chunk takes
+    the general path."""
     from conftest import _env_engine
-    eng = _env_engine({"FPNN_AES_K1R_RUNS": runs})
+    eng = _env_engine(env)
     try:
-        rng = np.random.default_rng(4100 + 10 * keylen + 2 * stream + int(runs))
+        rng = np.random.default_rng(4100 + 10 * keylen + 2 * stream + len(str(env)))
         ntri, nkeys = 120, 8
         lens, slots = [], []
         for t in range(ntri):
@@ -296,6 +297,16 @@ def test_interior_runs_after_key_switch(oracle, runs, stream, keylen):
                                 keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
             iv_d, pos_d = to_dev(iv0), to_dev(pos0.astype(np.int32))
             eng.stream_decrypt(to_dev(inp), dst, n, ks, iv_d, pos_d, **kw)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp)
+            # a second call continues every stream from the state the first one left
+            inp2 = rng.integers(0, 256, total, dtype=np.uint8)
+            exp = inp2.copy()
+            oracle.stream_batch(False, inp2, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                                lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys,
+                                keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
+            dst = to_dev(inp2)
+            eng.stream_decrypt(to_dev(inp2), dst, n, ks, iv_d, pos_d, **kw)
             torch.cuda.synchronize()
             assert np.array_equal(to_host(iv_d), iv_h)
             assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h)

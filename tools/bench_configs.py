@@ -496,6 +496,31 @@ def main():
                               "GPU gathers/scatters over PCIe; mapped encrypt output checked equal to the staged one")
         del src, dst
         print(json.dumps({"S1": out["S1"]}), flush=True)
+    if "SB" in todo:
+        # Small receive batches (one IO cycle of a server): 256 package frames of 64 .. 2047
+        # bytes (AES-256, one key) per call, 2 000 calls back to back -- the shape where a
+        # call's fixed launches cost more than its decrypt (K1r's fused block map).
+        key, iv = W.single_key(W.C2)
+        ks = fpnn_amd.KeySet(eng, key, len(key), iv)
+        rng = np.random.default_rng(2024)
+        P = 256
+        blen = rng.integers(64, 2048, P).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(blen[:-1])]).astype(np.int64)
+        total = int(blen.sum())
+        a = torch.empty(total, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, 11)
+        ct, back = torch.empty_like(a), torch.empty_like(a)
+        kw = dict(in_off=torch.from_numpy(offs).cuda(), lens=torch.from_numpy(blen.astype(np.int32)).cuda())
+        eng.package_encrypt(a, ct, P, ks, **kw)
+        wd, kd, launches = timed(eng, D, lambda: eng.package_decrypt(ct, back, P, ks, **kw), 2000, rounds=3)
+        torch.cuda.synchronize()
+        assert torch.equal(back, a), "SB round trip"
+        out["SB"] = {"frames_per_call": P, "bytes_per_call": total, "us_per_call_wall": round(wd * 1e6, 2),
+                     "us_per_call_kernel": round(kd * 1e6, 2), "launches_per_call": launches,
+                     "note": "small package receive batches (256 ragged frames, 64..2047 B, AES-256), "
+                             "back to back; K1r with its block map fused unless FPNN_AES_K1R_FUSED=0"}
+        del a, ct, back
+        print(json.dumps({"SB": out["SB"]}), flush=True)
     if "R1R" in todo:
         # R1 with realistic body lengths: CFB does not pad, so FPNN package bodies have any
         # length -- here uniform 1 .. 2047 bytes (mean ~1 KiB), 64 frames per connection
