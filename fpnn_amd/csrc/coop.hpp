@@ -46,6 +46,26 @@ __device__ __forceinline__ uint32_t aes_encrypt_column(uint32_t sq, const uint32
     return xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(rkq[NR], m2), quad_from<3>(m3));
 }
 
+// The same rounds for a serial CFB chain with the chain's two XORs folded into the round
+// keys: sw = C_{i-1} ^ rk[0] (the whitened state, already), fin = rk[NR] ^ P_i ^ rk[0];
+// returns C_i ^ rk[0], the next block's whitened state -- the ciphertext C_i = result ^
+// rk[0] and the keystream E(C_{i-1}) = C_i ^ P_i are side computations off the chain.  Two
+// dependent VALU ops fewer per block than aes_encrypt_column + (k ^ P) + (C ^ rk[0]).
+template <int NR, int NT>
+__device__ __forceinline__ uint32_t aes_chain_column(uint32_t sw, const uint32_t *rkq, uint32_t fin,
+                                                     const Tables4<NT> &T) {
+    uint32_t s0 = sw;
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t t0 = T.template t<0>(s0), t1 = T.template t<1>(s0), t2 = T.template t<2>(s0),
+                       t3 = T.template t<3>(s0);
+        s0 = xor3(xor_quad_from<1>(t0, t1), xor_quad_from<2>(rkq[r], t2), quad_from<3>(t3));
+    }
+    const uint32_t m0 = T.template sraw<0>(s0) & 0x000000ffu, m1 = T.template sraw<1>(s0) & 0x0000ff00u,
+                   m2 = T.template sraw<2>(s0) & 0x00ff0000u, m3 = T.template sraw<3>(s0) & 0xff000000u;
+    return xor3(xor_quad_from<1>(m0, m1), xor_quad_from<2>(fin, m2), quad_from<3>(m3));
+}
+
 typedef uint32_t __attribute__((aligned(1))) uint32_u;
 
 // bytes [lo, hi) of this lane's word (word covers block bytes [4q, 4q+4))

@@ -198,6 +198,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
             uint32_t a[CH];
 #pragma unroll
             for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo);
+            // the chain carries C ^ rk[0] (aes_chain_column: its two XORs folded into the keys)
+            const uint32_t rkx = rkq[NR] ^ rkq[0];
+            uint32_t sw = iv ^ rkq[0];
             for (; i + CH <= nfull; i += CH) {
                 const bool more = i + 2 * CH <= nfull;
                 uint32_t nx[CH], c[CH];
@@ -205,9 +208,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
                 for (int j = 0; j < CH; j++) nx[j] = more ? *reinterpret_cast<const uint32_u *>(p + 16 * (CH + j) + wlo) : 0u;
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
-                    iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];
-                    c[j] = iv;
+                    sw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
+                    c[j] = sw ^ rkq[0];
                 }
+                iv = c[CH - 1];
 #pragma unroll
                 for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
 #pragma unroll

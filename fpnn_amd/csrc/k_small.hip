@@ -96,17 +96,23 @@ __device__ __forceinline__ void small_body(uint32_t len, uint32_t head, uint32_t
 #pragma unroll
             for (int k = 0; k <= NR; k++) rkq[k] = rkp[4 * k + t];
             uint32_t fq = word_of(f0, (int)t);
-            uint32_t *bw = reinterpret_cast<uint32_t *>(buf + 1);
+            const uint32_t *bw = reinterpret_cast<const uint32_t *>(buf + 1);
+            uint32_t *ow = reinterpret_cast<uint32_t *>(io + 1);  // the body's words in the staging
             uint32_t pw = nb ? bw[t] : 0u;  // P_i, loaded one block ahead of its use
+            // the chain carries C ^ rk[0] (aes_chain_column: both XORs folded into the keys)
+            uint32_t sw = fq ^ rkq[0];
+            const uint32_t rkx = rkq[NR] ^ rkq[0];
             for (uint32_t i = 0; i < nb; i++) {
                 const uint32_t p = pw;
                 pw = bw[4 * (i + 1) + t];  // (buf has one spare block past the body)
-                const uint32_t k = aes_encrypt_column<NR, 4>(fq, rkq, T);
-                const uint32_t c = k ^ p;
-                bw[4 * i + t] = c;
+                const uint32_t nsw = aes_chain_column<NR, 4>(sw, rkq, rkx ^ p, T);
+                const uint32_t c = nsw ^ rkq[0];
+                ow[4 * i + t] = c;  // straight out (posted writes during the chain)
+                sw = nsw;
                 if (i + 1 < nb || r == 0) {
                     fq = c;
                 } else {  // partial last block: ivec = C bytes [0, r) + keystream bytes [r, 16)
+                    const uint32_t k = c ^ p;
                     const int lo = (int)r - 4 * (int)t;
                     const uint32_t m = lo >= 4 ? 0xffffffffu : lo <= 0 ? 0u : (0xffffffffu >> (8 * (4 - lo)));
                     fq = (c & m) | (k & ~m);
@@ -115,7 +121,7 @@ __device__ __forceinline__ void small_body(uint32_t len, uint32_t head, uint32_t
             if (nb) S.fout[t] = fq;
         }
         __syncthreads();
-        for (uint32_t i = t; i <= nb; i += kSmallThreads) io[i] = buf[i];
+        if (t == 0) io[0] = buf[0];  // the head's block
     } else {  // one lane per block; plaintext straight back to the staging
         const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
         const RoundKeys<NR> rk = *reinterpret_cast<const RoundKeys<NR> *>(rkp);
