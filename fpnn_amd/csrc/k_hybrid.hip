@@ -292,11 +292,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const bool head = SHIFT && lo0 != 0 && kk != 0;  // the chain's first slot: from byte lo0 on
             auto body = [&](auto fun_c) {
                 constexpr bool FUN = decltype(fun_c)::value;
+                // the chain carries C ^ rk[0] (aes_chain_column: its XORs folded into the keys)
+                const uint32_t rkx = rkq[NR] ^ rkq[0];
+                uint32_t sw = iv ^ rkq[0];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    const uint32_t c = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                    const uint32_t nsw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
+                    const uint32_t c = nsw ^ rkq[0];  // C_i = P_i ^ E(C_{i-1})
                     const bool use = j < (int)kk;
-                    iv = use ? c : iv;
+                    sw = use ? nsw : sw;
                     if (FUN) {  // slot j = the last d bytes of block j - 1 ‖ the first 16 - d of block j
                         // word q of the slot = bytes of block words q - e and q - e + 1
                         // (cl, ch), from the previous block where those indices wrap (fl, fh)
@@ -310,6 +314,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                         a[j] = c;
                     }
                 }
+                iv = sw ^ rkq[0];
                 if (SHIFT) {
                     // one output line: the last step's held words [jt, 8), then this step's
                     // [0, jt) (4-aligned dwords); then this step's [jt, kk) are held
