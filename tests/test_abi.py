@@ -71,6 +71,24 @@ def test_kernels_built_for_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle id of the embedded code object
 
 
+@pytest.mark.slow
+def test_ragged_decrypt_kernels_do_not_spill_vgprs():
+    """Every K1r instantiation keeps its registers out of scratch: a scratch reload inside
+    the chunk loop waits on vmcnt(0), which drains the prefetch pipeline (a fused-map
+    variant that spilled 3 VGPRs ran framed C3 at 407 instead of 955 GiB/s).
+    The compiler's resource remarks for k_ragged.hip (tools/kres.sh), gfx950."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc in this environment")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(["bash", os.path.join(root, "tools", "kres.sh"), "k_ragged.hip"], capture_output=True,
+                         text=True, timeout=600)
+    lines = [ln for ln in out.stdout.splitlines() if "k_cfb_decrypt_ragged<" in ln]
+    assert len(lines) >= 12, out.stdout[-2000:] + out.stderr[-2000:]
+    spills = [ln for ln in lines if not re.search(r"vgpr_spill=0\b", ln)]
+    assert not spills, spills
+
+
 def test_front_library_has_no_hip_dependency():
     """libfpnn_aes.so (what FPNN links) loads the HIP runtime only on first use, through
     libfpnn_aes_gpu.so: linked at start-up, the runtime's ~30 KiB of static TLS made
