@@ -48,7 +48,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 150 C2 steps = 0.3 s of load before the timed steps: the chip needs tens of ms of work
+    # to reach its clock (profiles/r04/timers.json: 5 warm-up steps read 3-4 % low)
+    ap.add_argument("--warmup", type=int, default=150)
     ap.add_argument("--packets", type=int, default=W.C2["packets"])
     ap.add_argument("--length", type=int, default=W.C2["length"])
     ap.add_argument("--cpu-seconds", type=float, default=1.5,
