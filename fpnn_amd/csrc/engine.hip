@@ -1636,7 +1636,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         std::vector<CSeg> cs;
         uint64_t state0 = si;  // stream: state index of the chunk's first segment
         uint64_t in_b = 0;
-        uint32_t cnt = 0;
+        uint32_t cnt = 0, uni_len = 0;  // uni_len: stream chunk whose segments all take this many bytes
         uint64_t out_b = 0, in_pad = 0, out_pad = 0, arr = 0, out_at = 0;
         if (!stream) {
             // whole frames [si, j) with <= kChunk input bytes (at least one frame)
@@ -1745,10 +1745,12 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             uint64_t *out_off = in_off + cnt;
             uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
             uint32_t *slots = lens + cnt;
+            uni_len = cnt ? (uint32_t)cs[0].len : 0u;
             for (uint32_t t = 0; t < cnt; t++) {
                 in_off[t] = out_off[t] = cs[t].at;
                 lens[t] = (uint32_t)cs[t].len;
                 slots[t] = cs[t].slot;
+                if (lens[t] != uni_len) uni_len = 0;
             }
             gather.clear();
             s.scatter.clear();
@@ -1781,6 +1783,14 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
         b.out_off = pre ? b.in_off + cnt : nullptr;
         b.len = reinterpret_cast<const uint32_t *>(s.d + in_pad + 16ull * cnt);
         b.key_slot = keys->count > 1 ? b.len + cnt : nullptr;
+        if (stream && encrypt && uni_len) {
+            // every stream takes the same quota (segments back to back): a uniform batch,
+            // so the encrypt skips the ragged length ordering (mapped_stream_pipeline)
+            b.in_off = nullptr;
+            b.len = nullptr;
+            b.stride = uni_len;
+            b.uniform_len = uni_len;
+        }
         b.keys = keys;
         b.flags = pre ? FPNN_AES_F_WIRE_PREFIX : 0;
         uint8_t *ivp = stream ? d_state + 16 * state0 : nullptr;
