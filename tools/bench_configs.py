@@ -499,7 +499,7 @@ def main():
     if "SB" in todo:
         # Small receive batches (one IO cycle of a server): 256 package frames of 64 .. 2047
         # bytes (AES-256, one key) per call, 2 000 calls back to back -- the shape where a
-        # call's fixed launches cost more than its decrypt (K1r's fused block map).
+        # call's fixed launches (block map + K1r) cost more than its decrypt.
         key, iv = W.single_key(W.C2)
         ks = fpnn_amd.KeySet(eng, key, len(key), iv)
         rng = np.random.default_rng(2024)
@@ -518,7 +518,7 @@ def main():
         out["SB"] = {"frames_per_call": P, "bytes_per_call": total, "us_per_call_wall": round(wd * 1e6, 2),
                      "us_per_call_kernel": round(kd * 1e6, 2), "launches_per_call": launches,
                      "note": "small package receive batches (256 ragged frames, 64..2047 B, AES-256), "
-                             "back to back; K1r with its block map fused unless FPNN_AES_K1R_FUSED=0"}
+                             "back to back: one-workgroup block map + K1r per call (launches_per_call counts K1r)"}
         del a, ct, back
         print(json.dumps({"SB": out["SB"]}), flush=True)
     if "R1R" in todo:
