@@ -34,7 +34,9 @@ def timed(eng, which, fn, reps, rounds=3, warm_s=0.3):
     back to back (no host sync between them -- an idle gap lets the clock drop, which
     individually timed calls of a ~1 ms kernel measure instead of the kernel).  Returns the
     medians over rounds of (wall s per call, kernel s per launch of the main kernel `which`
-    from HIP events on the engine stream) and the launches per call."""
+    from HIP events on the engine stream) and the launches per call.  Each round times the
+    wall first with the engine's event timing off (its two event records per launch are
+    not part of a call), then the same calls again with it on for the kernel time."""
     import statistics
     t0 = time.perf_counter()
     n = 0
@@ -46,13 +48,16 @@ def timed(eng, which, fn, reps, rounds=3, warm_s=0.3):
     torch.cuda.synchronize()
     walls, kern, launches = [], [], 0
     for _ in range(max(1, rounds)):
-        eng.reset_stats()
-        eng.set_timing(True)
-        t0 = time.perf_counter()
+        t0 = time.perf_counter()  # wall: no events in the stream
         for _ in range(max(1, reps)):
             fn()
         torch.cuda.synchronize()
         walls.append((time.perf_counter() - t0) / max(1, reps))
+        eng.reset_stats()
+        eng.set_timing(True)
+        for _ in range(max(1, reps)):
+            fn()
+        torch.cuda.synchronize()
         eng.set_timing(False)
         n, ms = eng.kernel_stats(which)
         kern.append(ms / max(1, n) / 1e3)
