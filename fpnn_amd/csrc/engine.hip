@@ -204,10 +204,9 @@ struct fpnn_aes_engine {
     uint64_t cap_snap_pos = 0;
     uint32_t *d_perm = nullptr;  // ragged encrypt: longest-first order
     uint64_t cap_perm = 0;
-    uint32_t *d_next = nullptr;  // K2q work-queue counter (one word)
-    uint64_t cap_next = 0;
-    uint32_t *d_buckets = nullptr;  // 2 x 128 counters + the wire flag (kLengthOrderWords)
+    uint32_t *d_buckets = nullptr;  // two length-order blocks (kLengthOrderWords each, zeroed when grown)
     uint64_t cap_buckets = 0;
+    uint32_t lo_parity = 0;  // the block the next length ordering uses
     uint64_t *d_fr_off = nullptr;  // package receive: absolute body offset per frame slot
     uint64_t cap_fr_off = 0;
     uint32_t *d_fr_slot = nullptr;  // package receive: key slot per frame slot
@@ -221,6 +220,9 @@ struct fpnn_aes_engine {
     uint32_t *d_desc_len = nullptr;
     uint64_t cap_desc_len = 0;
     uint64_t *d_total = nullptr;  // ragged block total (bstart[count]), device only
+    uint64_t *d_lookback = nullptr;  // one-pass block map: tickets + tile status (zeroed when grown)
+    uint64_t cap_lookback = 0;
+    uint32_t lb_epoch = 0;  // the last launch's status epoch (26 bits, never 0)
     uint8_t *d_ecdh = nullptr;  // ECDH host forms / keyset: peers | keys | ivs | ok (grown, kept)
     uint64_t cap_ecdh = 0;
     uint8_t *d_sstate = nullptr;  // stream host frames: (iv, pos) of the call's streams (grown, kept)
@@ -411,13 +413,20 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
         const uint64_t want = (lanes + threads - 1) / threads;
         const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
+        uint32_t *block = nullptr;  // the call's length-order block (ragged batches)
         if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
             if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
-            if ((rc = grow(e, e->d_buckets, e->cap_buckets, kLengthOrderWords))) return rc;
+            if (2 * kLengthOrderWords > e->cap_buckets) {  // both blocks start zeroed
+                if ((rc = grow(e, e->d_buckets, e->cap_buckets, 2 * kLengthOrderWords))) return rc;
+                HIP_TRY(hipMemsetAsync(e->d_buckets, 0, e->cap_buckets * sizeof(uint32_t), e->stream));
+            }
             if (stream) {  // bucket sizes read pos_state (the encrypt kernel reads it later)
                 k.pos_snap = pos_state;
             }
-            HIP_TRY(launch_length_order(k, stream, e->d_perm, e->d_buckets, e->stream));
+            block = e->d_buckets + kLengthOrderWords * e->lo_parity;
+            HIP_TRY(launch_length_order(k, stream, e->d_perm, block,
+                                        e->d_buckets + kLengthOrderWords * (e->lo_parity ^ 1u), e->stream));
+            e->lo_parity ^= 1u;
             k.perm = e->d_perm;
         }
         EventPair *ev;
@@ -425,14 +434,13 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // on quads, both from work queues); with fewer every quad holds at most one chain
         // and K2c's grid stride is cheaper
         const bool hybrid = b->len && b->count > 1 && (lanes > full_chip || e->variant.hyb_force);
-        if (hybrid && (rc = grow(e, e->d_next, e->cap_next, 2))) return rc;
         if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
         if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
             k.flags |= F_ALIGN_CHUNKS;
             HybridArgs h;
-            h.ctr = e->d_next;
-            h.buckets = e->d_buckets;
+            h.ctr = block + kTicketWords;
+            h.buckets = block;
             h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
             h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
             h.sink = e->d_sink;
@@ -528,7 +536,17 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         if (small_map)
             HIP_TRY(launch_block_map_small(k, stream, iv_state, pos_state, e->d_snap_iv, e->d_snap_pos, e->d_bstart,
                                            e->d_total, e->stream));
-        else
+        else if (e->variant.onepass) {
+            const uint64_t words = block_map_onepass_words(b->count);
+            if (words > e->cap_lookback) {  // the kernel expects zeros on first use
+                if ((rc = grow(e, e->d_lookback, e->cap_lookback, words))) return rc;
+                HIP_TRY(hipMemsetAsync(e->d_lookback, 0, e->cap_lookback * sizeof(uint64_t), e->stream));
+            }
+            e->lb_epoch = (e->lb_epoch + 1) & ((1u << 26) - 1);
+            if (!e->lb_epoch) e->lb_epoch = 1;
+            HIP_TRY(launch_block_map_onepass(k, stream, e->d_bstart, e->d_lookback, e->lb_epoch, e->d_total,
+                                             e->stream));
+        } else
             HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         k.bstart = e->d_bstart;
         if (!k.in_off || !k.len) {  // K1r reads descriptor arrays: materialize the missing ones
@@ -635,6 +653,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed
        // memory for reuse (release threshold: never) without changing the device's
        // default pool, which other code in the process allocates from
@@ -691,9 +710,10 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     (void)hipFree(e->d_tables);
     for (void *p : {(void *)e->d_bstart, (void *)e->d_wgsums, (void *)e->d_boundary, (void *)e->d_snap_iv,
-                    (void *)e->d_snap_pos, (void *)e->d_perm, (void *)e->d_next, (void *)e->d_buckets,
+                    (void *)e->d_snap_pos, (void *)e->d_perm, (void *)e->d_buckets,
                     (void *)e->d_fr_off, (void *)e->d_fr_slot, (void *)e->d_plan, (void *)e->d_sink,
-                    (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh, (void *)e->d_sstate})
+                    (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh, (void *)e->d_sstate,
+                    (void *)e->d_lookback})
         release_scratch(e, p);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     free_deferred(e);
@@ -789,6 +809,10 @@ int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t 
     int rc;
     if ((rc = grow(e, e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
     if ((rc = grow(e, e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
+    if (block_map_onepass_words(max_segments) > e->cap_lookback) {
+        if ((rc = grow(e, e->d_lookback, e->cap_lookback, block_map_onepass_words(max_segments)))) return rc;
+        HIP_TRY(hipMemsetAsync(e->d_lookback, 0, e->cap_lookback * sizeof(uint64_t), e->stream));
+    }
     const uint64_t nchunks = (max_blocks + 63) / 64;
     if ((rc = grow(e, e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
     if ((rc = grow(e, e->d_plan, e->cap_plan, (uint64_t)e->num_cus * (kThreads / 64)))) return rc;

@@ -564,8 +564,6 @@ static void hybrid_nr(const KBatch &b, const HybridArgs &h, KeyMode km, bool str
 
 hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nrounds, KeyMode km, bool stream, int grid,
                                  hipStream_t st) {
-    hipError_t err = hipMemsetAsync(h.ctr, 0, 2 * sizeof(uint32_t), st);
-    if (err != hipSuccess) return err;
     set_launched("cfb_encrypt_hybrid");
     switch (nrounds) {
         case 10: hybrid_nr<10>(b, h, km, stream, grid, st); break;

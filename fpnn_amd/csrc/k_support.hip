@@ -262,6 +262,56 @@ uint32_t length_bucket_of(uint64_t nblocks) {
     return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);
 }
 
+// A wave whose lanes all fall in one bucket (uniform lengths: R1's frames, C2R) adds to
+// it once instead of 64 times: same-address LDS atomics serialise lane by lane.  Returns
+// the lane's slot among the wave's additions to bucket k (base = the counter's old value).
+__device__ __forceinline__ uint32_t bucket_add(uint32_t *h, uint32_t k, bool live) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t act = __builtin_amdgcn_ballot_w64(live);
+    if (!act) return 0;
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)__builtin_ctzll(act));
+    if (__builtin_amdgcn_ballot_w64(live && k == k0) == act) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(act);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&h[k0], (uint32_t)__builtin_popcountll(act));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
+        return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    }
+    return live ? atomicAdd(&h[k], 1u) : 0u;
+}
+
+// Both passes take 16 segments per thread with every load issued before the first use:
+// unconditional loads (lanes past the batch re-read its last segment), so no load sits
+// in a branch of its own with a wait behind it (a loop of load -> atomic per segment
+// waited out one memory latency per segment: R1's 1 M frames cost 19 + 14 µs per call).
+// The host calls these for ragged batches only (b.len set).
+constexpr int kBucketItems = 16;
+constexpr uint64_t kBucketTile = 256ull * kBucketItems;
+
+__device__ __forceinline__ uint32_t bucket_of_blocks(uint64_t nblocks) {  // = length_bucket_of
+    const uint64_t nb = nblocks + 1;
+    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
+    const int lz = 31 - __builtin_clz(x);
+    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
+    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);
+}
+
+// buckets of segments tile0 + 256 i (kBuckets: past the batch)
+template <bool STREAM>
+__device__ __forceinline__ void tile_buckets(const KBatch &b, uint64_t tile0, uint32_t (&kb)[kBucketItems]) {
+    const uint32_t *__restrict__ lens = b.len;
+    uint32_t L[kBucketItems], P[kBucketItems];
+#pragma unroll
+    for (int i = 0; i < kBucketItems; i++) {
+        const uint64_t s = tile0 + 256ull * i, sc = s < b.count ? s : b.count - 1;
+        L[i] = lens[sc];
+        P[i] = STREAM ? b.pos_snap[sc] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kBucketItems; i++)
+        kb[i] = tile0 + 256ull * i < b.count ? bucket_of_blocks(seg_blocks(L[i], P[i])) : (uint32_t)kBuckets;
+}
+
 template <bool STREAM>
 __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts) {
     __shared__ uint32_t h[kBuckets];
@@ -269,11 +319,24 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
     if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
     if (threadIdx.x == 0) off4 = 0;
     __syncthreads();
-    const bool wire = !STREAM && (b.flags & F_WIRE_PREFIX);
-    uint32_t mis = 0;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += (uint64_t)gridDim.x * blockDim.x) {
-        atomicAdd(&h[length_bucket<STREAM>(b, s)], 1u);
-        if (wire) mis |= (uint32_t)(uintptr_t)get_seg<LAYOUT_GENERAL>(b, s).out & 3u;  // K2h's funnel needed
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kBucketTile + threadIdx.x;
+    uint32_t kb[kBucketItems], mis = 0;
+    if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // K2h's funnel is needed when an output is off the 4-byte grid
+        const uint64_t *__restrict__ op = b.out_off ? b.out_off : b.in_off;
+        uint64_t O[kBucketItems];
+#pragma unroll
+        for (int i = 0; i < kBucketItems; i++) {
+            const uint64_t s = tile0 + 256ull * i, sc = s < b.count ? s : b.count - 1;
+            O[i] = op ? op[sc] : sc * b.stride;
+        }
+#pragma unroll
+        for (int i = 0; i < kBucketItems; i++) mis |= (uint32_t)((uintptr_t)b.out + O[i]) & 3u;
+    }
+    tile_buckets<STREAM>(b, tile0, kb);
+#pragma unroll
+    for (int i = 0; i < kBucketItems; i++) {
+        const bool live = kb[i] < (uint32_t)kBuckets;
+        (void)bucket_add(h, live ? kb[i] : 0u, live);
     }
     if (mis) off4 = 1;
     __syncthreads();
@@ -281,7 +344,7 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
     if (threadIdx.x == 0 && off4) atomicOr(&counts[kWireFlagWord], 1u);
 }
 
-__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
+__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor, uint32_t *next) {
     __shared__ uint32_t sh[kBuckets];
     const int t = threadIdx.x;
     sh[t] = counts[t];
@@ -293,44 +356,50 @@ __global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint
         __syncthreads();
     }
     cursor[t] = sh[t] - counts[t];  // exclusive
+    for (int i = t; i < kLengthOrderWords; i += kBuckets) next[i] = 0u;  // the next call's block
 }
 
 template <bool STREAM>
-__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm, uint64_t per_wg) {
+__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm) {
     __shared__ uint32_t cnt[kBuckets], base[kBuckets];
     if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * per_wg;
-    const uint64_t hi = lo + per_wg < b.count ? lo + per_wg : b.count;
-    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) atomicAdd(&cnt[length_bucket<STREAM>(b, s)], 1u);
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kBucketTile + threadIdx.x;
+    uint32_t kb[kBucketItems];
+    tile_buckets<STREAM>(b, tile0, kb);
+#pragma unroll
+    for (int i = 0; i < kBucketItems; i++) {
+        const bool live = kb[i] < (uint32_t)kBuckets;
+        (void)bucket_add(cnt, live ? kb[i] : 0u, live);
+    }
     __syncthreads();
     if (threadIdx.x < kBuckets) {
         base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]) : 0u;
         cnt[threadIdx.x] = 0;
     }
     __syncthreads();
-    for (uint64_t s = lo + threadIdx.x; s < hi; s += blockDim.x) {
-        const uint32_t k = length_bucket<STREAM>(b, s);
-        perm[base[k] + atomicAdd(&cnt[k], 1u)] = (uint32_t)s;
+#pragma unroll
+    for (int i = 0; i < kBucketItems; i++) {
+        const bool live = kb[i] < (uint32_t)kBuckets;
+        const uint32_t k = live ? kb[i] : 0u;
+        const uint32_t slot = bucket_add(cnt, k, live);
+        if (live) perm[base[k] + slot] = (uint32_t)(tile0 + 256ull * i);
     }
 }
 
-hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st) {
-    uint32_t *cursor = counts + kBuckets;
-    hipError_t e = hipMemsetAsync(counts, 0, kLengthOrderWords * sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    const unsigned grid = (unsigned)((b.count + 255) / 256 < 1024 ? (b.count + 255) / 256 : 1024);
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, uint32_t *next,
+                               hipStream_t st) {
+    uint32_t *counts = block, *cursor = block + kBuckets;
+    const unsigned grid = (unsigned)((b.count + kBucketTile - 1) / kBucketTile);
     if (stream)
-        hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
+        hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid), dim3(256), 0, st, b, counts);
     else
-        hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid ? grid : 1), dim3(256), 0, st, b, counts);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor);
-    const uint64_t per_wg = 4096;
-    const unsigned sgrid = (unsigned)((b.count + per_wg - 1) / per_wg);
+        hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid), dim3(256), 0, st, b, counts);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor, next);
     if (stream)
-        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(grid), dim3(256), 0, st, b, cursor, perm);
     else
-        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(sgrid ? sgrid : 1), dim3(256), 0, st, b, cursor, perm, per_wg);
+        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(grid), dim3(256), 0, st, b, cursor, perm);
     return hipGetLastError();
 }
 
@@ -400,6 +469,110 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
             }
         }
     }
+}
+
+// Single-pass block map for batches past the one-workgroup map (decoupled look-back): a
+// workgroup takes a ticket v (tickets follow the order workgroups start in, so every
+// tile it waits for belongs to a running or finished workgroup), scans its 4 096
+// segments, publishes the tile's total, sums its predecessors' published totals back to
+// the nearest inclusive prefix (one wave, 64 tiles per round trip), publishes its own
+// inclusive prefix and writes its bstart entries.  One launch where the three-launch
+// scan took ≈ 19 µs per call at R1's 1 M frames.
+// lb[0] = ticket, lb[1] = finished workgroups (the last one resets both), lb[2 + v] =
+// tile v's status word: epoch (26 bits, never 0; stale words of earlier launches never
+// match) | flag (A = tile total, P = inclusive prefix) | value (36 bits: block totals
+// stay below 2^36, 1 TiB of data).
+constexpr int kOneItems = 16;
+constexpr uint64_t kOneTile = (uint64_t)kScanThreads * kOneItems;
+static_assert(kOneItems * (kScanThreads / 64) == 64, "one wave scans the tile's group totals");
+constexpr uint64_t kLbValue = (1ull << 36) - 1, kLbA = 1ull << 36, kLbP = 2ull << 36, kLbFlags = 3ull << 36;
+constexpr uint32_t kLbMaxSpin = 1u << 22;  // a bound, never reached: no wave spins forever
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool STREAM>
+__global__ __launch_bounds__(kScanThreads) void k_scan_onepass(KBatch b, uint64_t *bstart, uint64_t *lb, uint64_t nwg,
+                                                               uint64_t tag, uint64_t *total_out) {
+    __shared__ uint64_t grp[kOneItems * (kScanThreads / 64)];
+    __shared__ uint64_t ticket;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    if (t == 0) ticket = __hip_atomic_fetch_add(&lb[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint64_t v = ticket, tile0 = v * kOneTile;
+    uint64_t val[kOneItems], ex[kOneItems];
+#pragma unroll
+    for (int k = 0; k < kOneItems; k++) val[k] = nblocks_of<STREAM>(b, tile0 + (uint64_t)k * kScanThreads + t);
+#pragma unroll
+    for (int k = 0; k < kOneItems; k++) {  // segment order (round k, wave, lane), as k_scan_small
+        const uint64_t x = wave_incl_scan64(val[k]);
+        ex[k] = x - val[k];
+        if (lane == 63) grp[k * (kScanThreads / 64) + wv] = x;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t *const st = lb + 2;
+        const uint64_t g = grp[lane];
+        const uint64_t x = wave_incl_scan64(g);
+        const uint64_t agg = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63) << 32);
+        if (lane == 0) lb_store(&st[v], tag | (v == 0 ? kLbP : kLbA) | agg);
+        uint64_t excl = 0;
+        for (uint64_t end = v; end > 0;) {  // tiles [end - 64, end), nearest first in lane 0
+            const int64_t idx = (int64_t)end - 1 - (int64_t)lane;
+            uint64_t w = 0, pm = 0, need = ~0ull;
+            for (uint32_t spin = 0;; spin++) {
+                w = idx >= 0 ? lb_load(&st[idx]) : (tag | kLbP);  // before tile 0: a prefix of 0
+                const bool ok = (w & ~(kLbFlags | kLbValue)) == tag && (w & kLbFlags) != 0;
+                pm = __builtin_amdgcn_ballot_w64(ok && (w & kLbP));
+                need = pm ? ((pm & (0ull - pm)) << 1) - 1 : ~0ull;  // lanes up to the nearest prefix
+                if ((__builtin_amdgcn_ballot_w64(!ok) & need) == 0 || spin == kLbMaxSpin) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const uint64_t part = (need >> lane) & 1ull ? (w & kLbValue) : 0ull;
+            const uint64_t sum = wave_incl_scan64(part);
+            excl += (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)sum, 63) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sum >> 32), 63) << 32);
+            if (pm) break;
+            end = end > 64 ? end - 64 : 0;
+        }
+        if (v > 0 && lane == 0) lb_store(&st[v], tag | kLbP | (excl + agg));
+        grp[lane] = excl + x - g;  // the group's first bstart
+        if (lane == 0 && v == nwg - 1) {
+            bstart[b.count] = excl + agg;
+            *total_out = excl + agg;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kOneItems; k++) {
+        const uint64_t s = tile0 + (uint64_t)k * kScanThreads + t;
+        if (s < b.count) bstart[s] = grp[k * (kScanThreads / 64) + wv] + ex[k];
+    }
+    if (t == 0 && __hip_atomic_fetch_add(&lb[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
+        lb_store(&lb[0], 0);  // every workgroup has its ticket and is past its look-back
+        lb_store(&lb[1], 0);
+    }
+}
+
+uint64_t block_map_onepass_words(uint64_t count) { return 2 + (count + kOneTile - 1) / kOneTile; }
+
+hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint32_t epoch,
+                                    uint64_t *total, hipStream_t st) {
+    const uint64_t nwg = (b.count + kOneTile - 1) / kOneTile;
+    if (!nwg) return hipSuccess;
+    const uint64_t tag = (uint64_t)(epoch & ((1u << 26) - 1)) << 38;
+    if (stream)
+        hipLaunchKernelGGL((k_scan_onepass<true>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, lb, nwg,
+                           tag, total);
+    else
+        hipLaunchKernelGGL((k_scan_onepass<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, lb, nwg,
+                           tag, total);
+    return hipGetLastError();
 }
 
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,

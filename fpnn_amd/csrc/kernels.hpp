@@ -69,6 +69,9 @@ struct Variant {
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;
+    // large ragged block maps in one decoupled look-back launch (0: the three-launch scan;
+    // FPNN_AES_ONEPASS, same-box A/B and tests)
+    int onepass = 1;
 };
 
 // Base name ("cfb_decrypt_dense", ...) of the main kernel the last launch_* call on this
@@ -111,16 +114,20 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
                                int threads, hipStream_t st);
 // K2h (k_hybrid.hip): ragged batches with more chains than quads.  Chains of perm[]
 // in length buckets <= long_bucket run on quads (K2c's cipher), the rest one per lane
-// (K2's); quad_waves waves per workgroup start on the long ones.  ctr: 2 device words
-// (zeroed here, on the stream); buckets: launch_length_order's counts.
-// launch_length_order's counts array: 128 bucket counts, 128 cursors, then (wire-prefix
-// batches) a flag word, nonzero when some frame starts off the 4-byte grid
+// (K2's); quad_waves waves per workgroup start on the long ones.  ctr: the 2 ticket
+// words of the call's length-order block; buckets: its counts.
+// A length-order block (launch_length_order): 128 bucket counts, 128 cursors, then
+// (wire-prefix batches) a flag word, nonzero when some frame starts off the 4-byte grid,
+// then K2h's two ticket counters.  The engine keeps two and alternates: every call's
+// bucket scan zeroes the other one for the next call, so no memset launch is needed
+// (both start zeroed).
 constexpr int kWireFlagWord = 256;
-constexpr int kLengthOrderWords = 257;
+constexpr int kTicketWords = 257;
+constexpr int kLengthOrderWords = 259;
 
 struct HybridArgs {
     uint32_t *ctr;
-    const uint32_t *buckets;  // launch_length_order's counts (kLengthOrderWords)
+    const uint32_t *buckets;  // the call's length-order block
     uint32_t long_bucket;
     uint32_t quad_waves;
     uint4 *sink;      // 2 x uint4 per wave (grid * kThreads / 64 waves): stores with nothing to store
@@ -130,8 +137,10 @@ hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nroun
 // length bucket of a block count (descending: bucket 0 = longest), as launch_length_order
 uint32_t length_bucket_of(uint64_t nblocks);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
-// (quarter-octave buckets).  counts/cursor: 2 x 128 words of scratch.
-hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *counts, hipStream_t st);
+// (quarter-octave buckets).  block: this call's length-order block (zero on entry);
+// next: the other one, zeroed on the way for the next call.
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, uint32_t *next,
+                               hipStream_t st);
 // K1 / K1d / K1k for uniform and dense layouts (every segment's block count known on the host).
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
                                  hipStream_t st);
@@ -156,6 +165,12 @@ hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchun
 // device); wg_sums scratch of ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
+// The same in one launch (decoupled look-back); lb = block_map_onepass_words(count) words,
+// zero when first used, reset by the kernel itself; epoch: nonzero, new for every launch
+// (26 bits).
+uint64_t block_map_onepass_words(uint64_t count);
+hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint32_t epoch,
+                                    uint64_t *total, hipStream_t st);
 // The same for count <= block_map_small_max() in one workgroup; stream batches also
 // copy (iv_state, pos_state) into the snapshot (snap_iv / snap_pos) on the way.
 hipError_t launch_block_map_small(const KBatch &b, bool stream, const uint8_t *iv_state, const uint32_t *pos_state,

@@ -118,13 +118,15 @@ def test_stream_segments_random_positions(engine, oracle, keylen):
         assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 1023, 1024, 1025, 5000, 16383, 16384, 16385])
+@pytest.mark.parametrize("n", [1, 63, 64, 1023, 1024, 1025, 4097, 5000, 16383, 16384, 16385, 262145, 300001])
 def test_block_map_round_boundaries(engine, oracle, n):
     """The single-workgroup block map (k_scan_small, up to 16 384 segments) takes segment
-    k*1024 + t in thread t and scans per wave, then the wave totals: segment counts at and
-    around the 64 / 1024 multiples and the small/large switch (16 385 takes the 3-launch
-    scan), stream mode (the (iv, pos) snapshot comes from the same kernel) and package mode
-    out of place (per-wave plan inside K1r) and in place (plan launch)."""
+    k*1024 + t in thread t and scans per wave, then the wave totals, in groups of four
+    rounds: segment counts at and around the 64 / 1024 / 4096 multiples and the
+    small/large switch.  Past 16 384 segments the one-pass look-back map runs: 262 145 and
+    300 001 segments are 65 and 74 tiles, so the look-back crosses its 64-tile window.
+    Stream mode (the (iv, pos) snapshot comes from the same kernel) and package mode out
+    of place (per-wave plan inside K1r) and in place (plan launch)."""
     rng = np.random.default_rng(9000 + n)
     lens = rng.integers(0, 300, n)
     lens[rng.random(n) < 0.05] = 0
@@ -151,6 +153,36 @@ def test_block_map_round_boundaries(engine, oracle, n):
     assert np.array_equal(to_host(dst), exp)
     assert np.array_equal(to_host(ivd), iv_exp)
     assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
+
+
+@pytest.mark.parametrize("env", [{"FPNN_AES_ONEPASS": "0"}, {"FPNN_AES_ONEPASS": "1"}], ids=["scan3", "onepass"])
+def test_large_block_map_repeated_calls(oracle, env):
+    """The one-pass map resets its own tickets and tags its tile status with a per-launch
+    epoch: back-to-back calls of different sizes (more tiles, then fewer, then more
+    again) must each read only their own launch's status words.  The three-launch scan
+    (FPNN_AES_ONEPASS=0) runs the same calls."""
+    from conftest import _env_engine
+    eng = _env_engine(env)
+    try:
+        rng = np.random.default_rng(77 + len(str(env)))
+        key = rng.integers(0, 256, 32, dtype=np.uint8)
+        iv = rng.integers(0, 256, 16, dtype=np.uint8)
+        ks = keyset(eng, key, 32, iv)
+        for n in (300001, 20000, 140000, 16385, 300001):
+            lens = rng.integers(0, 200, n).astype(np.int64)
+            offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+            total = int(lens.sum()) + 16
+            plain = rng.integers(0, 256, total, dtype=np.uint8)
+            ct = plain.copy()
+            oracle.package_batch(True, plain, ct, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                                 lens=lens.astype(np.uint32), keys=key, keylen=32, ivs=iv, threads=8)
+            src, dst = to_dev(ct), to_dev(np.zeros_like(ct))
+            eng.package_decrypt(src, dst, n, ks, in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+            torch.cuda.synchronize()
+            got = to_host(dst)
+            assert np.array_equal(got[: total - 16], plain[: total - 16]), n
+    finally:
+        eng.close()
 
 
 # ------------------------------------------------------------------------------------
