@@ -245,22 +245,15 @@ uint64_t block_map_small_max() { return kSmallScanMax; }
 
 constexpr int kBuckets = 128;
 
-template <bool STREAM>
-__device__ __forceinline__ uint32_t length_bucket(const KBatch &b, uint64_t s) {
-    const uint64_t nb = nblocks_of<STREAM>(b, s) + 1;  // >= 1
+__host__ __device__ inline uint32_t bucket_of_blocks(uint64_t nblocks) {
+    const uint64_t nb = nblocks + 1;  // >= 1
     const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
     const int lz = 31 - __builtin_clz(x);
     const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
     return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);  // descending length
 }
 
-uint32_t length_bucket_of(uint64_t nblocks) {
-    const uint64_t nb = nblocks + 1;
-    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
-    const int lz = 31 - __builtin_clz(x);
-    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
-    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);
-}
+uint32_t length_bucket_of(uint64_t nblocks) { return bucket_of_blocks(nblocks); }
 
 // A wave whose lanes all fall in one bucket (uniform lengths: R1's frames, C2R) adds to
 // it once instead of 64 times: same-address LDS atomics serialise lane by lane.  Returns
@@ -287,14 +280,6 @@ __device__ __forceinline__ uint32_t bucket_add(uint32_t *h, uint32_t k, bool liv
 // The host calls these for ragged batches only (b.len set).
 constexpr int kBucketItems = 16;
 constexpr uint64_t kBucketTile = 256ull * kBucketItems;
-
-__device__ __forceinline__ uint32_t bucket_of_blocks(uint64_t nblocks) {  // = length_bucket_of
-    const uint64_t nb = nblocks + 1;
-    const uint32_t x = nb > 0xffffffffull ? 0xffffffffu : (uint32_t)nb;
-    const int lz = 31 - __builtin_clz(x);
-    const uint32_t frac = lz >= 2 ? (x >> (lz - 2)) & 3u : (x << (2 - lz)) & 3u;
-    return (uint32_t)(kBuckets - 1) - (uint32_t)(4 * lz + frac);
-}
 
 // buckets of segments tile0 + 256 i (kBuckets: past the batch)
 template <bool STREAM>
