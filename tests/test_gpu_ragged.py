@@ -155,6 +155,49 @@ def test_block_map_round_boundaries(engine, oracle, n):
     assert np.array_equal(to_host(posd).astype(np.uint32), pos_exp)
 
 
+@pytest.mark.parametrize("env", [{"FPNN_AES_K1R_RUNS": "0"}, {"FPNN_AES_K1R_RUNS": "1"}], ids=["runs0", "runs1"])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_one_kib_segments_on_chunk_boundaries(oracle, env, inplace):
+    """One-key AES-256 package batches of 1 KiB segments, each exactly one 64-block chunk
+    (R1's receive bodies, at 4-byte-misaligned offsets), broken by other lengths (1 KiB
+    +- 1, 2 KiB, 16 B, 0 B, sub-block) so chunk boundaries drift off the segments and
+    back, in place and out of place, interior runs on and off.  (A run loop over such
+    segments back to back measured slower than K1r's general path -- 904-910 against
+    942 GiB/s on R1 -- and was not kept: its per-segment descriptor loads sat on the
+    chunk's critical path.)"""
+    from conftest import _env_engine
+    eng = _env_engine(env)
+    try:
+        rng = np.random.default_rng(5150 + 2 * inplace + len(str(env)))
+        lens = []
+        for _ in range(300):
+            lens += [1024] * int(rng.integers(1, 40))
+            lens.append(int(rng.choice([0, 5, 16, 1023, 1025, 2048, 3000])))
+        lens = np.array(lens, np.int64)
+        n = len(lens)
+        gaps = np.full(n, 4, np.int64)  # the wire prefix between bodies
+        offs = (np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])]) + 4).astype(np.int64)
+        total = int(offs[-1] + lens[-1]) + 64
+        key = rng.integers(0, 256, 32, dtype=np.uint8)
+        iv = rng.integers(0, 256, 16, dtype=np.uint8)
+        ks = keyset(eng, key, 32, iv)
+        inp = rng.integers(0, 256, total, dtype=np.uint8)
+        exp = inp.copy()
+        oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), out_off=offs.astype(np.uint64),
+                             lens=lens.astype(np.uint32), keys=key, keylen=32, ivs=iv, threads=8)
+        src = to_dev(inp)
+        dst = src if inplace else to_dev(inp)
+        kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+        for _ in range(2):  # the second call: scratch reused
+            if inplace:
+                src.copy_(torch.from_numpy(inp).to(src.device))
+            eng.package_decrypt(src, dst, n, ks, **kw)
+            torch.cuda.synchronize()
+            assert np.array_equal(to_host(dst), exp)
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("env", [{"FPNN_AES_ONEPASS": "0"}, {"FPNN_AES_ONEPASS": "1"}], ids=["scan3", "onepass"])
 def test_large_block_map_repeated_calls(oracle, env):
     """The one-pass map resets its own tickets and tags its tile status with a per-launch

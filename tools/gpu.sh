@@ -16,7 +16,8 @@
 #   configs:<list>   the same for a comma list, e.g. configs:C4,R1
 #   host             tools/bench_configs.py --configs C2,S1 with the host / PCIe legs
 #   s1               S1 (stream host frames) twice with the host-stats breakdown
-#   ab:<VAR>:<list>  same-box A/B of a dispatch knob: the configs with VAR=0, VAR=1, twice
+#   ab:<VAR>:<list>[:<vals>]  same-box A/B of a dispatch knob: the configs with VAR=0, VAR=1 (or each of
+#                    the comma list vals), twice
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
@@ -76,8 +77,9 @@ for step in "$@"; do
     s1) for i in 1 2; do
         FPNN_AES_HOST_STATS=1 run "s1_$i" 300 python -u tools/bench_configs.py --reps 3 --configs S1
       done ;;
-    ab:*) spec=${step#ab:}; var=${spec%%:*}; cfgs=${spec#*:}
-      for i in 1 2; do for v in 0 1; do
+    ab:*) spec=${step#ab:}; var=${spec%%:*}; rest=${spec#*:}; cfgs=${rest%%:*}; vals=0,1
+      [ "$rest" != "$cfgs" ] && vals=${rest#*:}
+      for i in 1 2; do for v in ${vals//,/ }; do
         env "$var=$v" timeout -k 10 300 python -u tools/bench_configs.py --reps 3 --no-host --configs "$cfgs" \
           > "$OUT/ab_${var}_${v}_$i.log" 2>&1 || { echo "ab $var=$v failed"; tail -5 "$OUT/ab_${var}_${v}_$i.log"; exit 3; }
         echo "   $var=$v #$i: $(grep -h '^{"configs"' "$OUT/ab_${var}_${v}_$i.log" | cut -c1-700)"
