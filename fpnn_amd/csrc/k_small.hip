@@ -186,20 +186,28 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
     __syncthreads();
     uint4 *io = reinterpret_cast<uint4 *>(mb->io + kSmallBodyAt - 16);
     for (uint32_t it = 0;; it++) {
-        if (t == 0) {  // 0 = nothing yet, 1 = serve, 2 = leave
-            const u32x4_t h = load_sys16(&mb->req);  // seq, op, len, head
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            const uint32_t s = h.x;
-            const uint64_t now = wall_clock64();
-            uint32_t action = 0;
-            uint32_t nb = 0;
-            if (s != done) {
-                action = 1;
-                nb = (h.z - h.w + 15) >> 4;
-                nb = nb < kSmallMaxBytes / 16 ? nb : kSmallMaxBytes / 16;  // the host never asks for more
-            } else if (__hip_atomic_load(&mb->req.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                       now - t_idle > idle_ticks || now - t_start > life_ticks) {
-                action = 2;
+        // Thread 0 polls until there is a request or a reason to leave; the other waves wait
+        // at the barrier meanwhile (no barrier per poll).  An idle poll is one PCIe round trip:
+        // the stop flag is a second read, made every 32nd poll only (engine teardown waits
+        // for the idle exit anyway).
+        if (t == 0) {  // 1 = serve, 2 = leave
+            uint32_t action = 0, s = done, nb = 0;
+            for (uint32_t np = 0; action == 0; np++) {
+                const u32x4_t h = load_sys16(&mb->req);  // seq, op, len, head
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                s = h.x;
+                const uint64_t now = wall_clock64();
+                if (s != done) {
+                    action = 1;
+                    nb = (h.z - h.w + 15) >> 4;
+                    nb = nb < kSmallMaxBytes / 16 ? nb : kSmallMaxBytes / 16;  // the host never asks for more
+                } else if (now - t_idle > idle_ticks || now - t_start > life_ticks ||
+                           ((np & 31u) == 31u &&
+                            __hip_atomic_load(&mb->req.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+                    action = 2;
+                } else {
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
             ctl[it & 1][0] = action;
             ctl[it & 1][1] = s;
@@ -208,10 +216,6 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
         __syncthreads();
         const uint32_t action = ctl[it & 1][0], s = ctl[it & 1][1], nb = ctl[it & 1][2];
         if (action == 2) break;
-        if (action == 0) {
-            __builtin_amdgcn_s_sleep(4);
-            continue;
-        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // this wave sees the host's request
         // request header and the call's bytes into LDS
         if (t < sizeof(SmallReq) / 16)
