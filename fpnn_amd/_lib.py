@@ -28,6 +28,7 @@ ERR_ARG = -2
 ERR_RANGE = -3
 ERR_HIP = -4
 ERR_NODEV = -5
+ERR_DEVICE = -6
 
 F_WIRE_PREFIX = 0x1
 SCAN_OK, SCAN_FULL, SCAN_TOO_LARGE, SCAN_BAD_MAGIC, SCAN_BAD_MTYPE, SCAN_BAD_LENGTH = range(6)

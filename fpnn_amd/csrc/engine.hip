@@ -204,9 +204,8 @@ struct fpnn_aes_engine {
     uint64_t cap_snap_pos = 0;
     uint32_t *d_perm = nullptr;  // ragged encrypt: longest-first order
     uint64_t cap_perm = 0;
-    uint32_t *d_buckets = nullptr;  // two length-order blocks (kLengthOrderWords each, zeroed when grown)
-    uint64_t cap_buckets = 0;
-    uint32_t lo_parity = 0;  // the block the next length ordering uses
+    uint32_t *d_buckets = nullptr;  // the length-order block (kLengthOrderWords; zeroed when grown, then
+    uint64_t cap_buckets = 0;       // zeroed again by its last reader, kernels.hpp)
     uint64_t *d_fr_off = nullptr;  // package receive: absolute body offset per frame slot
     uint64_t cap_fr_off = 0;
     uint32_t *d_fr_slot = nullptr;  // package receive: key slot per frame slot
@@ -220,9 +219,12 @@ struct fpnn_aes_engine {
     uint32_t *d_desc_len = nullptr;
     uint64_t cap_desc_len = 0;
     uint64_t *d_total = nullptr;  // ragged block total (bstart[count]), device only
-    uint64_t *d_lookback = nullptr;  // one-pass block map: tickets + tile status (zeroed when grown)
+    uint64_t *d_lookback = nullptr;  // one-pass block map: tickets, epoch, tile status (zeroed when grown)
     uint64_t cap_lookback = 0;
-    uint32_t lb_epoch = 0;  // the last launch's status epoch (26 bits, never 0)
+    // device-side consistency checks (kFault*): a pinned word kernels may set, read when the
+    // stream is idle (fpnn_aes_engine_sync, synchronous calls) and reported as FPNN_AES_ERR_DEVICE
+    uint32_t *h_fault = nullptr;
+    uint32_t *d_fault = nullptr;
     uint8_t *d_ecdh = nullptr;  // ECDH host forms / keyset: peers | keys | ivs | ok (grown, kept)
     uint64_t cap_ecdh = 0;
     uint8_t *d_sstate = nullptr;  // stream host frames: (iv, pos) of the call's streams (grown, kept)
@@ -332,6 +334,17 @@ void free_deferred(fpnn_aes_engine *e) {  // the engine's stream is idle
     e->deferred.clear();
 }
 
+// The engine's stream is idle: release grown-out scratch, and report (once) a consistency
+// check a kernel failed since the last look (kernels.hpp, kFault*).
+int stream_idle(fpnn_aes_engine *e) {
+    free_deferred(e);
+    const uint32_t f = e->h_fault ? __atomic_exchange_n(e->h_fault, 0u, __ATOMIC_ACQ_REL) : 0u;
+    if (!f) return FPNN_AES_OK;
+    g_last_error = (f & kFaultLookback) ? "block map: a look-back gave up waiting for a tile (results of that call invalid)"
+                                        : "device-side check failed";
+    return FPNN_AES_ERR_DEVICE;
+}
+
 int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
     *pair = nullptr;
     if (!e->timing) return FPNN_AES_OK;
@@ -413,27 +426,25 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
         const uint64_t want = (lanes + threads - 1) / threads;
         const int grid = (int)(want < (uint64_t)e->num_cus ? (want ? want : 1) : (uint64_t)e->num_cus);
-        uint32_t *block = nullptr;  // the call's length-order block (ragged batches)
+        // ragged with more chains than quads: K2h (short chains one per lane, the longest
+        // on quads, both from work queues); with fewer every quad holds at most one chain
+        // and K2c's grid stride is cheaper
+        const bool hybrid = b->len && b->count > 1 && (lanes > full_chip || e->variant.hyb_force);
+        uint32_t *block = nullptr;  // the length-order block (ragged batches)
         if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
             if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
-            if (2 * kLengthOrderWords > e->cap_buckets) {  // both blocks start zeroed
-                if ((rc = grow(e, e->d_buckets, e->cap_buckets, 2 * kLengthOrderWords))) return rc;
+            if (kLengthOrderWords > e->cap_buckets) {  // starts zeroed; afterwards its last reader zeroes it
+                if ((rc = grow(e, e->d_buckets, e->cap_buckets, kLengthOrderWords))) return rc;
                 HIP_TRY(hipMemsetAsync(e->d_buckets, 0, e->cap_buckets * sizeof(uint32_t), e->stream));
             }
             if (stream) {  // bucket sizes read pos_state (the encrypt kernel reads it later)
                 k.pos_snap = pos_state;
             }
-            block = e->d_buckets + kLengthOrderWords * e->lo_parity;
-            HIP_TRY(launch_length_order(k, stream, e->d_perm, block,
-                                        e->d_buckets + kLengthOrderWords * (e->lo_parity ^ 1u), e->stream));
-            e->lo_parity ^= 1u;
+            block = e->d_buckets;
+            HIP_TRY(launch_length_order(k, stream, e->d_perm, block, !hybrid, e->stream));
             k.perm = e->d_perm;
         }
         EventPair *ev;
-        // ragged with more chains than quads: K2h (short chains one per lane, the longest
-        // on quads, both from work queues); with fewer every quad holds at most one chain
-        // and K2c's grid stride is cheaper
-        const bool hybrid = b->len && b->count > 1 && (lanes > full_chip || e->variant.hyb_force);
         if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
         if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
         if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
@@ -542,10 +553,8 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
                 if ((rc = grow(e, e->d_lookback, e->cap_lookback, words))) return rc;
                 HIP_TRY(hipMemsetAsync(e->d_lookback, 0, e->cap_lookback * sizeof(uint64_t), e->stream));
             }
-            e->lb_epoch = (e->lb_epoch + 1) & ((1u << 26) - 1);
-            if (!e->lb_epoch) e->lb_epoch = 1;
-            HIP_TRY(launch_block_map_onepass(k, stream, e->d_bstart, e->d_lookback, e->lb_epoch, e->d_total,
-                                             e->stream));
+            HIP_TRY(launch_block_map_onepass(k, stream, e->d_bstart, e->d_lookback, e->cap_lookback, e->d_fault,
+                                             e->d_total, e->stream));
         } else
             HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
         k.bstart = e->d_bstart;
@@ -695,6 +704,12 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         if (err != hipSuccess) { rc = hip_fail(err, "hipMemcpy(tables)"); break; }
         err = hipMalloc(reinterpret_cast<void **>(&e->d_total), sizeof(uint64_t));
         if (err != hipSuccess) { rc = hip_fail(err, "hipMalloc(total)"); break; }
+        err = hipHostMalloc(reinterpret_cast<void **>(&e->h_fault), 64, hipHostMallocCoherent);
+        if (err == hipSuccess) {
+            *e->h_fault = 0;
+            err = hipHostGetDevicePointer(reinterpret_cast<void **>(&e->d_fault), e->h_fault, 0);
+        }
+        if (err != hipSuccess) { rc = hip_fail(err, "hipHostMalloc(fault)"); break; }
     } while (0);
     if (rc) {
         fpnn_aes_engine_destroy(e);
@@ -722,6 +737,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         (void)hipMemPoolDestroy(e->mpool);
     }
     (void)hipFree(e->d_total);
+    if (e->h_fault) (void)hipHostFree(e->h_fault);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_small) (void)hipHostFree(e->h_small);
@@ -762,8 +778,7 @@ int fpnn_aes_engine_sync(fpnn_aes_engine *e) {
     if (!e) return FPNN_AES_ERR_ARG;
     DeviceGuard g(e->device);
     HIP_TRY(hipStreamSynchronize(e->stream));
-    free_deferred(e);
-    return FPNN_AES_OK;
+    return stream_idle(e);
 }
 
 void *fpnn_aes_engine_stream(fpnn_aes_engine *e) { return e ? (void *)e->stream : nullptr; }
@@ -815,7 +830,19 @@ int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t 
     }
     const uint64_t nchunks = (max_blocks + 63) / 64;
     if ((rc = grow(e, e->d_boundary, e->cap_boundary, nchunks + 1))) return rc;
-    if ((rc = grow(e, e->d_plan, e->cap_plan, (uint64_t)e->num_cus * (kThreads / 64)))) return rc;
+    const uint64_t nwaves = (uint64_t)e->num_cus * (kThreads / 64);
+    if ((rc = grow(e, e->d_plan, e->cap_plan, nwaves))) return rc;
+    if ((rc = grow(e, e->d_sink, e->cap_sink, 2 * nwaves))) return rc;
+    // ragged encrypt ordering, stream-decrypt snapshot, materialised descriptors
+    if ((rc = grow(e, e->d_perm, e->cap_perm, max_segments))) return rc;
+    if (kLengthOrderWords > e->cap_buckets) {
+        if ((rc = grow(e, e->d_buckets, e->cap_buckets, kLengthOrderWords))) return rc;
+        HIP_TRY(hipMemsetAsync(e->d_buckets, 0, e->cap_buckets * sizeof(uint32_t), e->stream));
+    }
+    if ((rc = grow(e, e->d_snap_iv, e->cap_snap_iv, max_segments))) return rc;
+    if ((rc = grow(e, e->d_snap_pos, e->cap_snap_pos, max_segments))) return rc;
+    if ((rc = grow(e, e->d_desc_off, e->cap_desc_off, max_segments))) return rc;
+    if ((rc = grow(e, e->d_desc_len, e->cap_desc_len, max_segments))) return rc;
     return FPNN_AES_OK;
 }
 
@@ -1299,7 +1326,7 @@ int modes_call(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int mode, const
     HIP_TRY(hipMemcpyAsync(h_iv, a.iv, 32, hipMemcpyDeviceToHost, e->stream));
     if (out_copy) HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + ipad, a.out, out_copy, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    free_deferred(e);  // the stream is idle: grown-out scratch can go
+    if (int rf = stream_idle(e)) return rf;
     if (out_copy) memcpy(out, e->h_stage + hdr + ipad, out_copy);
     if (ivec && mode != MODE_CBC_DEC) memcpy(ivec, h_iv, 16);
     if (p_num) *p_num = *h_pos;
@@ -1391,7 +1418,7 @@ int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encr
     HIP_TRY(hipMemcpyAsync(h_iv, d_iv, 32, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipMemcpyAsync(e->h_stage + hdr + pay, e->d_stage + hdr + pay, len, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    free_deferred(e);  // the stream is idle: grown-out scratch can go
+    if (int rf = stream_idle(e)) return rf;
     memcpy(out, e->h_stage + hdr + pay, len);
     memcpy(ivec, h_iv, 16);
     *p_num = *h_pos;
@@ -2186,7 +2213,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
     const double td = hst.on ? HostStats::now() : 0;
     HIP_TRY(hipStreamSynchronize(ms));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    free_deferred(e);  // the stream is idle: grown-out scratch can go
+    if (int rf = stream_idle(e)) rc = rc ? rc : rf;
     for (auto &m : e->ms) m.busy = false;
     for (auto &c : ch) c.cnt = 0;
     *done = si;
@@ -2453,7 +2480,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     const double td = hst.on ? HostStats::now() : 0;
     HIP_TRY(hipStreamSynchronize(ms));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    free_deferred(e);  // the stream is idle: grown-out scratch can go
+    if (int rf = stream_idle(e)) rc = rc ? rc : rf;
     for (auto &m : e->ms) m.busy = false;
     for (auto &c : ch) c.np = 0;
     if (!rc) {

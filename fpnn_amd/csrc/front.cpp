@@ -92,6 +92,7 @@ const char *fpnn_aes_strerror(int status) {
         case FPNN_AES_ERR_RANGE: return "batch too large";
         case FPNN_AES_ERR_HIP: return "HIP runtime error";
         case FPNN_AES_ERR_NODEV: return "no usable gfx950 device";
+        case FPNN_AES_ERR_DEVICE: return "device-side check failed";
         default: return "unknown status";
     }
 }

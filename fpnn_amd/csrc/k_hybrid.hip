@@ -532,12 +532,13 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 
     if (!LANES) {  // every chain on quads (the host routes here with quad_waves = 16)
         quad_session(true);
-        return;
+    } else {
+        if (wave < h.quad_waves) quad_session(true);
+        lane_session();
+        // long chains left (fewer quad waves than the long queue needs): join them
+        if (__atomic_load_n(&h.ctr[0], __ATOMIC_RELAXED) + static_q < n_long) quad_session(false);
     }
-    if (wave < h.quad_waves) quad_session(true);
-    lane_session();
-    // long chains left (fewer quad waves than the long queue needs): join them
-    if (__atomic_load_n(&h.ctr[0], __ATOMIC_RELAXED) + static_q < n_long) quad_session(false);
+    length_order_release(h.ctr - kTicketWords);  // the block's last reader: zero it for the next call
 }
 
 template <int NR>

@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
     if (threadIdx.x == 0 && off4) atomicOr(&counts[kWireFlagWord], 1u);
 }
 
-__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor, uint32_t *next) {
+__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
     __shared__ uint32_t sh[kBuckets];
     const int t = threadIdx.x;
     sh[t] = counts[t];
@@ -341,11 +341,10 @@ __global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint
         __syncthreads();
     }
     cursor[t] = sh[t] - counts[t];  // exclusive
-    for (int i = t; i < kLengthOrderWords; i += kBuckets) next[i] = 0u;  // the next call's block
 }
 
 template <bool STREAM>
-__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm) {
+__global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *cursor, uint32_t *perm, uint32_t *release) {
     __shared__ uint32_t cnt[kBuckets], base[kBuckets];
     if (threadIdx.x < kBuckets) cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -370,21 +369,23 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *curs
         const uint32_t slot = bucket_add(cnt, k, live);
         if (live) perm[base[k] + slot] = (uint32_t)(tile0 + 256ull * i);
     }
+    if (release) length_order_release(release);  // K2c follows: nothing reads the block again
 }
 
-hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, uint32_t *next,
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, bool zero_after,
                                hipStream_t st) {
     uint32_t *counts = block, *cursor = block + kBuckets;
     const unsigned grid = (unsigned)((b.count + kBucketTile - 1) / kBucketTile);
+    uint32_t *release = zero_after ? block : nullptr;
     if (stream)
         hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid), dim3(256), 0, st, b, counts);
     else
         hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid), dim3(256), 0, st, b, counts);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor, next);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor);
     if (stream)
-        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(grid), dim3(256), 0, st, b, cursor, perm);
+        hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(grid), dim3(256), 0, st, b, cursor, perm, release);
     else
-        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(grid), dim3(256), 0, st, b, cursor, perm);
+        hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(grid), dim3(256), 0, st, b, cursor, perm, release);
     return hipGetLastError();
 }
 
@@ -463,10 +464,13 @@ __global__ __launch_bounds__(256) void k_fill_synthetic(uint8_t *dst, uint64_t n
 // the nearest inclusive prefix (one wave, 64 tiles per round trip), publishes its own
 // inclusive prefix and writes its bstart entries.  One launch where the three-launch
 // scan took ≈ 19 µs per call at R1's 1 M frames.
-// lb[0] = ticket, lb[1] = finished workgroups (the last one resets both), lb[2 + v] =
-// tile v's status word: epoch (26 bits, never 0; stale words of earlier launches never
+// lb[0] = ticket, lb[1] = finished workgroups, lb[2] = this launch's epoch (0 = 1), lb[3 + v]
+// = tile v's status word: epoch (26 bits, never 0; stale words of earlier launches never
 // match) | flag (A = tile total, P = inclusive prefix) | value (36 bits: block totals
-// stay below 2^36, 1 TiB of data).
+// stay below 2^36, 1 TiB of data).  The last workgroup to finish resets the tickets and
+// advances the epoch; when the epoch wraps it first clears every status word of the buffer,
+// so a word 2^26 launches old cannot match either.  Nothing is passed from the host per
+// launch: a captured launch replays correctly (fpnn_aes_engine_reserve, "graph-safe").
 constexpr int kOneItems = 16;
 constexpr uint64_t kOneTile = (uint64_t)kScanThreads * kOneItems;
 static_assert(kOneItems * (kScanThreads / 64) == 64, "one wave scans the tile's group totals");
@@ -480,15 +484,22 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr uint64_t kLbEpochMask = (1ull << 26) - 1;
+
 template <bool STREAM>
 __global__ __launch_bounds__(kScanThreads) void k_scan_onepass(KBatch b, uint64_t *bstart, uint64_t *lb, uint64_t nwg,
-                                                               uint64_t tag, uint64_t *total_out) {
+                                                               uint64_t lb_words, uint32_t *fault,
+                                                               uint64_t *total_out) {
     __shared__ uint64_t grp[kOneItems * (kScanThreads / 64)];
-    __shared__ uint64_t ticket;
+    __shared__ uint64_t ticket, epoch;
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    if (t == 0) ticket = __hip_atomic_fetch_add(&lb[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) {
+        ticket = __hip_atomic_fetch_add(&lb[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t e = lb_load(&lb[2]) & kLbEpochMask;  // written by the previous launch's last workgroup
+        epoch = e ? e : 1;
+    }
     __syncthreads();
-    const uint64_t v = ticket, tile0 = v * kOneTile;
+    const uint64_t v = ticket, tile0 = v * kOneTile, tag = epoch << 38;
     uint64_t val[kOneItems], ex[kOneItems];
 #pragma unroll
     for (int k = 0; k < kOneItems; k++) val[k] = nblocks_of<STREAM>(b, tile0 + (uint64_t)k * kScanThreads + t);
@@ -500,7 +511,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_onepass(KBatch b, uint64_
     }
     __syncthreads();
     if (wv == 0) {
-        uint64_t *const st = lb + 2;
+        uint64_t *const st = lb + 3;
         const uint64_t g = grp[lane];
         const uint64_t x = wave_incl_scan64(g);
         const uint64_t agg = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63) |
@@ -515,7 +526,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_onepass(KBatch b, uint64_
                 const bool ok = (w & ~(kLbFlags | kLbValue)) == tag && (w & kLbFlags) != 0;
                 pm = __builtin_amdgcn_ballot_w64(ok && (w & kLbP));
                 need = pm ? ((pm & (0ull - pm)) << 1) - 1 : ~0ull;  // lanes up to the nearest prefix
-                if ((__builtin_amdgcn_ballot_w64(!ok) & need) == 0 || spin == kLbMaxSpin) break;
+                if ((__builtin_amdgcn_ballot_w64(!ok) & need) == 0) break;
+                if (spin == kLbMaxSpin) {  // never expected: report it rather than sum stale words silently
+                    if (lane == 0) __hip_atomic_store(fault, kFaultLookback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
             const uint64_t part = (need >> lane) & 1ull ? (w & kLbValue) : 0ull;
@@ -539,24 +554,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_onepass(KBatch b, uint64_
         if (s < b.count) bstart[s] = grp[k * (kScanThreads / 64) + wv] + ex[k];
     }
     if (t == 0 && __hip_atomic_fetch_add(&lb[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1) {
-        lb_store(&lb[0], 0);  // every workgroup has its ticket and is past its look-back
+        // every workgroup has its ticket and epoch and is past its look-back
+        uint64_t next = (epoch + 1) & kLbEpochMask;
+        if (!next) {  // wrapped: no status word of any earlier launch may match epoch 1 again
+            for (uint64_t i = 3; i < lb_words; i++) lb_store(&lb[i], 0);
+            next = 1;
+        }
+        lb_store(&lb[2], next);
+        lb_store(&lb[0], 0);
         lb_store(&lb[1], 0);
     }
 }
 
-uint64_t block_map_onepass_words(uint64_t count) { return 2 + (count + kOneTile - 1) / kOneTile; }
+uint64_t block_map_onepass_words(uint64_t count) { return 3 + (count + kOneTile - 1) / kOneTile; }
 
-hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint32_t epoch,
-                                    uint64_t *total, hipStream_t st) {
+hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint64_t lb_words,
+                                    uint32_t *fault, uint64_t *total, hipStream_t st) {
     const uint64_t nwg = (b.count + kOneTile - 1) / kOneTile;
     if (!nwg) return hipSuccess;
-    const uint64_t tag = (uint64_t)(epoch & ((1u << 26) - 1)) << 38;
     if (stream)
         hipLaunchKernelGGL((k_scan_onepass<true>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, lb, nwg,
-                           tag, total);
+                           lb_words, fault, total);
     else
         hipLaunchKernelGGL((k_scan_onepass<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, lb, nwg,
-                           tag, total);
+                           lb_words, fault, total);
     return hipGetLastError();
 }
 

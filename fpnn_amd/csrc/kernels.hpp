@@ -118,12 +118,14 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
 // words of the call's length-order block; buckets: its counts.
 // A length-order block (launch_length_order): 128 bucket counts, 128 cursors, then
 // (wire-prefix batches) a flag word, nonzero when some frame starts off the 4-byte grid,
-// then K2h's two ticket counters.  The engine keeps two and alternates: every call's
-// bucket scan zeroes the other one for the next call, so no memset launch is needed
-// (both start zeroed).
+// then K2h's two ticket counters, then a count of finished workgroups.  The block starts
+// zeroed and its LAST reader zeroes it again once every workgroup is done with it: the
+// bucket scatter's last workgroup when K2c follows, K2h's when K2h follows.  No memset
+// launch per call, and a call captured in a graph finds the block zeroed on every replay.
 constexpr int kWireFlagWord = 256;
 constexpr int kTicketWords = 257;
-constexpr int kLengthOrderWords = 259;
+constexpr int kDoneWord = 259;
+constexpr int kLengthOrderWords = 260;
 
 struct HybridArgs {
     uint32_t *ctr;
@@ -137,9 +139,10 @@ hipError_t launch_encrypt_hybrid(const KBatch &b, const HybridArgs &h, int nroun
 // length bucket of a block count (descending: bucket 0 = longest), as launch_length_order
 uint32_t length_bucket_of(uint64_t nblocks);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
-// (quarter-octave buckets).  block: this call's length-order block (zero on entry);
-// next: the other one, zeroed on the way for the next call.
-hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, uint32_t *next,
+// (quarter-octave buckets).  block: the length-order block (zero on entry); zero_after:
+// nothing reads it after the scatter (K2c follows), so the scatter's last workgroup zeroes
+// it; otherwise K2h does.
+hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, bool zero_after,
                                hipStream_t st);
 // K1 / K1d / K1k for uniform and dense layouts (every segment's block count known on the host).
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
@@ -165,12 +168,16 @@ hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchun
 // device); wg_sums scratch of ceil(count/1024) entries.
 hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
                                  uint64_t *total, hipStream_t st);
-// The same in one launch (decoupled look-back); lb = block_map_onepass_words(count) words,
-// zero when first used, reset by the kernel itself; epoch: nonzero, new for every launch
-// (26 bits).
+// The same in one launch (decoupled look-back); lb = block_map_onepass_words(count) words
+// (lb_words = the buffer's capacity), zero when first used.  Everything the next launch
+// needs is kept by the kernel itself -- tickets reset and the tile-status epoch advanced by
+// its last workgroup -- so a launch captured in a graph and replayed stays correct.
+// fault: a device-visible word (pinned host) that gets kFaultLookback if a look-back ever
+// gave up waiting (the host reports FPNN_AES_ERR_DEVICE at the next sync).
+constexpr uint32_t kFaultLookback = 1u;
 uint64_t block_map_onepass_words(uint64_t count);
-hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint32_t epoch,
-                                    uint64_t *total, hipStream_t st);
+hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint64_t lb_words,
+                                    uint32_t *fault, uint64_t *total, hipStream_t st);
 // The same for count <= block_map_small_max() in one workgroup; stream batches also
 // copy (iv_state, pos_state) into the snapshot (snap_iv / snap_pos) on the way.
 hipError_t launch_block_map_small(const KBatch &b, bool stream, const uint8_t *iv_state, const uint32_t *pos_state,

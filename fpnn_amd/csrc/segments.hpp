@@ -110,4 +110,17 @@ inline int grid_for(uint64_t items, int threads, int cap) {
     return (int)(g > (uint64_t)cap ? cap : g);
 }
 
+// The last workgroup of a kernel that reads the length-order block (kernels.hpp) returns it
+// to zeros for the next call.  Every workgroup calls this at its very end, all threads.
+__device__ __forceinline__ void length_order_release(uint32_t *block) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&block[kDoneWord], 1u) == gridDim.x - 1) {
+            for (int i = 0; i < kLengthOrderWords; i++) block[i] = 0u;
+            __threadfence();
+        }
+    }
+}
+
 }  // namespace fpnn_aes

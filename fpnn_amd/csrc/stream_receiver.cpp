@@ -35,8 +35,11 @@ size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 // Device and pinned buffers of one batch, on the engine of the thread that flushes it
 // (grown, kept), through the C-ABI's memory calls (this file is built without HIP).
 // Pool engines are never destroyed (thread_engine.hpp), so the cached engine stays valid
-// when the batch is destroyed or flushed by another thread after the first has exited.
+// when the batch is destroyed or flushed by another thread after the first has exited --
+// but another thread may hold that engine's lease by then, so release() runs under the
+// engine's mutex (with_engine_locked), never beside a call on it.
 struct StreamReceiverBatch::Dev {
+    fpnn_aes::PooledEngine *pe = nullptr;
     fpnn_aes_engine *e = nullptr;
     uint64_t eid = 0;
     fpnn_aes_keyset *ks[3] = {nullptr, nullptr, nullptr};  // per key length
@@ -84,7 +87,7 @@ StreamReceiverBatch::StreamReceiverBatch(uint32_t max_len, uint32_t max_frames)
 
 StreamReceiverBatch::~StreamReceiverBatch() {
     if (_dev) {
-        _dev->release();
+        fpnn_aes::with_engine_locked(_dev->pe, [&](fpnn_aes_engine *) { _dev->release(); });
         delete _dev;
     }
 }
@@ -125,18 +128,22 @@ int StreamReceiverBatch::status(int conn) const { return _conns.at(conn).status;
 size_t StreamReceiverBatch::pending(int conn) const { return _conns.at(conn).carry.size(); }
 
 void StreamReceiverBatch::flush() {
+    // flushed from a thread with another engine: free the buffers on the old one first,
+    // under its mutex, before this thread locks its own (one engine mutex at a time)
+    fpnn_aes::PooledEngine *mine = fpnn_aes::thread_pooled_engine();
+    if (_dev && _dev->pe != mine) {
+        fpnn_aes::with_engine_locked(_dev->pe, [&](fpnn_aes_engine *) { _dev->release(); });
+        delete _dev;
+        _dev = nullptr;
+    }
     int rc;
     const fpnn_aes::Lease lease = fpnn_aes::thread_engine(&rc);
     fpnn_aes_engine *e = lease.engine();
     const uint64_t eid = lease.id();
     if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
-    if (_dev && _dev->eid != eid) {  // flushed from a thread with another engine: move there
-        _dev->release();
-        delete _dev;
-        _dev = nullptr;
-    }
     if (!_dev) {
         _dev = new Dev();
+        _dev->pe = lease.pe;
         _dev->e = e;
         _dev->eid = eid;
     }

@@ -105,14 +105,28 @@ struct ThreadLease {
     }
 };
 
-inline Lease thread_engine(int *status) {
+// The calling thread's pool entry (leased on first use), not locked.
+inline PooledEngine *thread_pooled_engine() {
     thread_local ThreadLease tl;
     if (!tl.pe) tl.pe = EnginePool::get().acquire();
+    return tl.pe;
+}
+
+inline Lease thread_engine(int *status) {
     Lease l;
-    l.pe = tl.pe;
-    *status = tl.pe->status;
-    if (tl.pe->e) l.lk = std::unique_lock<std::mutex>(tl.pe->mu);
+    l.pe = thread_pooled_engine();
+    *status = l.pe->status;
+    if (l.pe->e) l.lk = std::unique_lock<std::mutex>(l.pe->mu);
     return l;
+}
+
+// Work on an engine some other thread may hold the lease of (a batch object that cached
+// it): under that engine's mutex, as every call on it is.  Callers hold no other engine's
+// mutex meanwhile (no lock-order cycle between two engines).
+template <class F>
+void with_engine_locked(PooledEngine *pe, F &&f) {
+    std::lock_guard<std::mutex> lk(pe->mu);
+    f(pe->e);
 }
 
 }  // namespace fpnn_aes

@@ -44,6 +44,8 @@ extern "C" {
 #define FPNN_AES_ERR_RANGE    -3  /* batch too large (more than 2^32-1 16-byte blocks or packets) */
 #define FPNN_AES_ERR_HIP      -4  /* HIP runtime error (message: fpnn_aes_last_error) */
 #define FPNN_AES_ERR_NODEV    -5  /* no usable gfx950 device / kernels not loadable */
+#define FPNN_AES_ERR_DEVICE   -6  /* a queued kernel's own consistency check failed (reported by
+                                     the next fpnn_aes_engine_sync or synchronous call) */
 
 const char *fpnn_aes_strerror(int status);
 /* Thread-local text of the last HIP error seen by this thread (or ""). */
@@ -81,7 +83,12 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e);
 int fpnn_aes_engine_sync(fpnn_aes_engine *e);
 void *fpnn_aes_engine_stream(fpnn_aes_engine *e);
 /* Pre-size scratch for batches of up to max_segments packets/streams and
- * max_blocks total 16-byte blocks, so later calls never allocate (graph-safe). */
+ * max_blocks total 16-byte blocks, so later device-batch calls of that size never
+ * allocate or memset.  They are then graph-safe: a call captured on the engine's stream
+ * (hipStreamBeginCapture) may be replayed with new data, offsets and lengths in the same
+ * device arrays, because every piece of cross-call scratch state (the block map's
+ * look-back epoch and tickets, the length-order block and K2h's tickets) is reset on the
+ * device by the kernels that use it (tests/test_gpu_graph.py). */
 int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t max_blocks);
 
 /* Placement of the engines behind the C++ classes (Encryptor, EncryptorBatch,

@@ -31,11 +31,23 @@ def oracle():
     return Oracle("port")
 
 
+def missing_reference_build(what):
+    """A reference checker under oracle/_ref/ is absent.  Where a GPU is present (the GPU
+    box, which gets the tree with the checkers built here) that is an error: the parity
+    evidence must not vanish as a skip.  On a CPU-only machine without /root/reference it
+    is a skip."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.fail(f"{what} missing on a GPU machine: build it with __graft_entry__.build() "
+                    "(make -C oracle ref framing echo percall ecdh dropin) before the GPU run")
+    pytest.skip(f"{what} not built (needs /root/reference)")
+
+
 @pytest.fixture(scope="session")
 def ref_oracle():
     from pyoracle import Oracle, ref_available
     if not ref_available():
-        pytest.skip("oracle/_ref/libfpnn_ref.so not built (needs /root/reference)")
+        missing_reference_build("oracle/_ref/libfpnn_ref.so")
     return Oracle("reference")
 
 

@@ -86,9 +86,75 @@ def test_mapped_ragged_frames(engine, oracle, arenas, keylen, wire_prefix):
         fr2 = frames_array(dst.ctypes.data, doffs, dst.ctypes.data, doffs, lens, slots)
         engine.package_host_array(False, fr2, ks)
         assert engine.last_kernel(fpnn_amd.K_HOST) == "host_mapped"
-        for i in range(0, len(lens), 7):
-            s, d, L = int(soffs[i]), int(doffs[i]), int(lens[i])
-            assert np.array_equal(dst[d:d + L], src[s:s + L])
+        bad = [i for i in range(len(lens))
+               if not np.array_equal(dst[int(doffs[i]):int(doffs[i]) + int(lens[i])],
+                                     src[int(soffs[i]):int(soffs[i]) + int(lens[i])])]
+        assert not bad, (len(bad), bad[:8])  # every frame, not a sample (the r04n failure)
+
+
+def _triples(rng, ntri, nkeys):
+    """(short slot a, short slot b, long slot a) triples: the 64-block chunk before a long
+    frame's interior holds the slots a, b, a, so K1r's last per-slot key pass in it is b's
+    while the long frame that continues is a's (the shape of the r04n mismatch)."""
+    lens, slots = [], []
+    for t in range(ntri):
+        a, b = (2 * t) % nkeys, (2 * t + 1) % nkeys
+        lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(2000, 9000))]
+        slots += [a, b, a]
+    return np.array(lens, np.uint32), np.array(slots, np.uint32)
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_mapped_perkey_inplace_after_growth(oracle, arenas, keylen):
+    """the r04n shape made deterministic.  A fresh engine encrypts
+    per-key ragged frames (mapped, out of place), then a larger unrelated ragged decrypt
+    grows the engine's scratch (block map, plan, descriptors: the old buffers are released
+    behind the stream while the move stream is idle), then the frames are decrypted back IN
+    PLACE through the mapped path.  Every byte of every frame must come back, and the
+    ciphertext must equal the oracle's."""
+    import fpnn_amd
+    from test_gpu_parity import to_dev
+    import torch
+    eng = fpnn_amd.Engine(0)
+    try:
+        rng = np.random.default_rng(7700 + keylen)
+        nkeys = 7
+        lens, slots = _triples(rng, 400, nkeys)
+        keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
+        ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), keylen, ivs.tobytes())
+        soffs, ssize = place(rng, lens)
+        doffs, dsize = place(rng, lens)
+        src = arenas(ssize, 0)
+        src[:] = rng.integers(0, 256, ssize, dtype=np.uint8)
+        dst = arenas(dsize, 0xA5)
+        fr = frames_array(src.ctypes.data, soffs, dst.ctypes.data, doffs, lens, slots)
+        eng.package_host_array(True, fr, ks)
+        assert eng.last_kernel(fpnn_amd.K_HOST) == "host_mapped"
+        exp = np.full(dsize, 0xA5, dtype=np.uint8)
+        for i in range(len(lens)):
+            exp[int(doffs[i]):int(doffs[i]) + int(lens[i])] = src[int(soffs[i]):int(soffs[i]) + int(lens[i])]
+        oracle.package_batch(True, exp.copy(), exp, len(lens), in_off=doffs.astype(np.uint64), lens=lens,
+                             key_slot=slots, keys=keys, keylen=keylen, ivs=ivs, threads=8)
+        assert np.array_equal(dst, exp)
+        # scratch growth: a ragged device decrypt with 20x the segments
+        n2 = 20 * len(lens)
+        l2 = rng.integers(0, 300, n2).astype(np.int32)
+        o2 = np.concatenate([[0], np.cumsum(l2[:-1].astype(np.int64))])
+        buf = to_dev(rng.integers(0, 256, int(o2[-1] + l2[-1]) + 64, dtype=np.uint8))
+        eng.package_decrypt(buf, buf, n2, ks, in_off=to_dev(o2), lens=to_dev(l2),
+                            key_slot=to_dev(rng.integers(0, nkeys, n2).astype(np.int32)))
+        fr2 = frames_array(dst.ctypes.data, doffs, dst.ctypes.data, doffs, lens, slots)
+        eng.package_host_array(False, fr2, ks)  # in place
+        assert eng.last_kernel(fpnn_amd.K_HOST) == "host_mapped"
+        torch.cuda.synchronize()
+        bad = [i for i in range(len(lens))
+               if not np.array_equal(dst[int(doffs[i]):int(doffs[i]) + int(lens[i])],
+                                     src[int(soffs[i]):int(soffs[i]) + int(lens[i])])]
+        assert not bad, (len(bad), bad[:8])
+    finally:
+        eng.sync()
+        eng.close()
 
 
 @pytest.mark.parametrize("nkeys", [1, 64])

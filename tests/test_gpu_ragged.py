@@ -333,13 +333,18 @@ def test_offsets_beyond_2gib(engine, oracle, stream):
 @pytest.mark.parametrize("env", [{"FPNN_AES_K1R_RUNS": "0"}, {"FPNN_AES_K1R_RUNS": "1"}], ids=["runs0", "runs1"])
 @pytest.mark.parametrize("stream", [False, True])
 @pytest.mark.parametrize("keylen", [16, 32])
-def test_interior_runs_after_key_switch(oracle, env, stream, keylen):
+@pytest.mark.parametrize("inplace", [False, True])
+def test_interior_runs_after_key_switch(oracle, env, stream, keylen, inplace):
     """K1r's interior runs (FPNN_AES_K1R_RUNS, k_ragged.hip) on per-key batches whose
     chunks end on another slot's pass: triples (short slot A, short slot B, long slot A),
     so the chunk before a long segment's run holds A, B, A and the general path's last
     key pass is B's.  Lengths off the block grid, gaps between segments, and in stream
     mode random carried (ivec, pos), two calls in a row; with runs off every chunk takes
-    the general path."""
+    the general path.  This is the r04n mismatch: a tree that built the runs
+    into the per-key kernels deciphered the long segment's interior with B's round keys;
+    tools/probe/k1r_runs_perkey.patch rebuilds that form and fails here.  In place, the
+    fresh engine first runs a ragged encrypt, so the decrypt grows the scratch the encrypt
+    left (the r04n call order)."""
     from conftest import _env_engine
     eng = _env_engine(env)
     try:
@@ -371,7 +376,7 @@ def test_interior_runs_after_key_switch(oracle, env, stream, keylen):
                                 lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys,
                                 keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
             iv_d, pos_d = to_dev(iv0), to_dev(pos0.astype(np.int32))
-            eng.stream_decrypt(to_dev(inp), dst, n, ks, iv_d, pos_d, **kw)
+            eng.stream_decrypt(dst if inplace else to_dev(inp), dst, n, ks, iv_d, pos_d, **kw)
             torch.cuda.synchronize()
             assert np.array_equal(to_host(dst), exp)
             # a second call continues every stream from the state the first one left
@@ -381,14 +386,19 @@ def test_interior_runs_after_key_switch(oracle, env, stream, keylen):
                                 lens=lens.astype(np.uint32), key_slot=slots.astype(np.uint32), keys=keys,
                                 keylen=keylen, iv_state=iv_h, pos_state=pos_h, threads=8)
             dst = to_dev(inp2)
-            eng.stream_decrypt(to_dev(inp2), dst, n, ks, iv_d, pos_d, **kw)
+            eng.stream_decrypt(dst if inplace else to_dev(inp2), dst, n, ks, iv_d, pos_d, **kw)
             torch.cuda.synchronize()
             assert np.array_equal(to_host(iv_d), iv_h)
             assert np.array_equal(to_host(pos_d).astype(np.uint32), pos_h)
         else:
             oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
                                  key_slot=slots.astype(np.uint32), keys=keys, keylen=keylen, ivs=ivs, threads=8)
-            eng.package_decrypt(to_dev(inp), dst, n, ks, **kw)
+            if inplace:
+                scratch = to_dev(inp)  # the encrypt grows the ordering scratch first
+                eng.package_encrypt(to_dev(inp), scratch, n, ks, **kw)
+                eng.package_decrypt(dst, dst, n, ks, **kw)
+            else:
+                eng.package_decrypt(to_dev(inp), dst, n, ks, **kw)
             torch.cuda.synchronize()
         assert np.array_equal(to_host(dst), exp)
     finally:

@@ -9,6 +9,8 @@
 #   tests            the whole GPU suite (pytest -m gpu, incl. slow)
 #   tests_fast       pytest -m "gpu and not slow"
 #   tests:<expr>     pytest -m gpu -k <expr>
+#   probe:<lib>:<expr>  the same against another build of the GPU library (fpnn_amd/<lib>, loaded
+#                    through FPNN_AES_GPU_LIB), e.g. a tools/probe/*.patch build
 #   bench            python bench.py (the contract line)
 #   bench_trace      bench.py under rocprofv3 --kernel-trace --stats (profiles the line's kernels)
 #   bench_pmc        bench.py under the four PMC passes (HBM bytes, LDS, VALU, waits)
@@ -66,6 +68,9 @@ for step in "$@"; do
     tests) run tests 1100 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread ;;
     tests_fast) run tests_fast 600 python -u -m pytest tests -q -m "gpu and not slow" -x --timeout 120 --timeout-method thread ;;
     tests:*) run "tests_k" 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread -k "${step#tests:}" ;;
+    probe:*) spec=${step#probe:}; lib=${spec%%:*}
+      FPNN_AES_GPU_LIB=$PWD/fpnn_amd/$lib run "probe_${lib%.so}" 600 python -u -m pytest tests -q -m gpu \
+        --timeout 300 --timeout-method thread -k "${spec#*:}" ;;
     bench) run bench 300 python -u bench.py ;;
     bench_trace) mkdir -p "$OUT/bench_trace"  # (bench_pmc's own trace pass goes to bench_prof/trace)
       run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_trace" -o run -- \
