@@ -316,6 +316,36 @@ def gen_c1_cases():
             "echo": cases, "percall": {"frames": pc["frames"], "len": pc["len"], "checksum": pc["checksum"]}}
 
 
+MULTI_REF = os.path.join(HERE, "_ref", "io_multi_ref")
+# SURVEY 8f row 1 inside FPNN's IO plumbing (oracle/io_multi.cpp):
+# (name, mode, keylen, conns, quests per conn, payload, window, threads).  M1 is the headline
+# shape: 1 024 connections x window 8 x 1 KiB AES-256 package frames.
+MULTI_CASES = [("M1", "package", 32, 1024, 32, 1024, 8, 1), ("M2", "package", 16, 1024, 16, 1024, 8, 4),
+               ("M3", "package", 24, 300, 12, 3001, 4, 2), ("M4", "stream", 32, 1024, 16, 1024, 8, 1),
+               ("M5", "stream", 16, 256, 24, 777, 4, 2)]
+
+
+def gen_multi_cases():
+    """Many connections through the reference's own SendBuffer / encrypted receivers and
+    cipher (`make -C oracle multi`): per case the folded wire digests of both directions.
+    The digests do not depend on the thread count or the transport (each connection's byte
+    stream is fixed by its key, IV and quests)."""
+    import subprocess
+    cases = []
+    for name, mode, kl, conns, q, plen, win, thr in MULTI_CASES:
+        out = subprocess.run([MULTI_REF, "1" if mode == "stream" else "0", str(kl), str(conns), str(q), str(plen),
+                              str(win), str(thr)], capture_output=True, text=True, check=True, timeout=600).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+        assert d["ok"] and d["answers_ok"], d
+        c = {"name": name, "threads": thr}
+        c.update({k: d[k] for k in ("mode", "keylen", "conns", "quests_per_conn", "payload", "window",
+                                    "wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv")})
+        cases.append(c)
+        print("  multi", c, "reference echo/s here:", d["echo_per_s"])
+    return {"source": "reference SendBuffer + encrypted receivers + core/Encryptor.cpp + base/rijndael.c, "
+                      "many connections (oracle/_ref/io_multi_ref, oracle/io_multi.cpp)", "cases": cases}
+
+
 ECDH_REF = os.path.join(HERE, "_ref", "ecdh_ref")
 
 
@@ -520,6 +550,7 @@ def main():
     ap.add_argument("--framing-only", action="store_true", help="only (re)write framing_cases.json")
     ap.add_argument("--ecdh-only", action="store_true", help="only (re)write ecdh_cases.json")
     ap.add_argument("--c1-only", action="store_true", help="only (re)write c1_cases.json")
+    ap.add_argument("--multi-only", action="store_true", help="only (re)write multi_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -542,6 +573,9 @@ def main():
     if args.c1_only:
         dump("c1_cases.json", gen_c1_cases())
         return
+    if args.multi_only:
+        dump("multi_cases.json", gen_multi_cases())
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -556,6 +590,7 @@ def main():
     dump("framing_cases.json", gen_framing_cases(ref))
     dump("ecdh_cases.json", gen_ecdh_cases())
     dump("c1_cases.json", gen_c1_cases())
+    dump("multi_cases.json", gen_multi_cases())
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

@@ -70,6 +70,50 @@ def test_c1_echo_reference_io_plumbing_on_dropin(idx):
         assert d[k] == g[k], (k, d[k], g[k])
 
 
+def _multi():
+    with open(os.path.join(ROOT, "tests", "golden", "multi_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _run_multi(exe, c, threads=None, timeout=600):
+    out = subprocess.run([exe, "1" if c["mode"] == "stream" else "0", str(c["keylen"]), str(c["conns"]),
+                          str(c["quests_per_conn"]), str(c["payload"]), str(c["window"]),
+                          str(threads or c["threads"])], capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, (out.returncode, out.stderr[-3000:])
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("case", _multi(), ids=lambda c: c["name"])
+def test_collector_in_reference_io_plumbing(case):
+    """SURVEY 8f row 1 inside FPNN's own IO plumbing: many connections
+    through the reference's SendBuffer and EncryptedPackageReceiver with INTEGRATION.md 2a
+    applied by oracle/collect_patch.py -- SendBuffer::encryptData and
+    EncryptedPackageReceiver::fetch queue into the IO thread's fpnn::EncryptorBatch, one
+    flush per loop cycle and direction (stream mode receives through StreamReceiverBatch).
+    Each direction's wire bytes equal the unpatched reference build's, and every answer
+    equals its quest.  The reference build is timed on the same box beside it."""
+    exe = _exe("io_multi_batched")
+    d = _run_multi(exe, case)
+    ref = _run_multi(_exe("io_multi_ref"), case)
+    print(json.dumps({"case": case["name"], "batched": d, "reference": ref}))
+    assert d["build"] == "batched" and d["ok"] and d["answers_ok"] and d["flushes"] > 0, d
+    for k in ("wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv"):
+        assert d[k] == case[k], (k, d[k], case[k])
+        assert ref[k] == case[k], (k, ref[k], case[k])
+
+
+def test_percall_dropin_in_reference_io_plumbing():
+    """The same plumbing UNCHANGED on libfpnn_aes.so (one GPU call per frame, the drop-in
+    of INTEGRATION.md section 1) on a small many-connection case: identical wire bytes."""
+    case = dict(_multi()[2])  # M3's shape, fewer quests: per-call is slow by design
+    d = _run_multi(_exe("io_multi_dropin"), dict(case, quests_per_conn=2, conns=64))
+    ref = _run_multi(_exe("io_multi_ref"), dict(case, quests_per_conn=2, conns=64))
+    print(json.dumps({"dropin": d, "reference": ref}))
+    assert d["build"] == "dropin" and d["ok"] and d["answers_ok"], d
+    for k in ("wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv"):
+        assert d[k] == ref[k], (k, d[k], ref[k])
+
+
 def test_c1_percall_unchanged_package_encryptor(tmp_path):
     """C1's per-call shape: 10 000 x 1 KiB AES-256 frames through the unchanged
     PackageEncryptor::encrypt / decrypt / encrypt(std::string*) one call at a time

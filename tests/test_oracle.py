@@ -285,6 +285,35 @@ def test_c1_echo_reference_reproduces_fixture():
         assert [d[k] for k in ("wire_c2s_fnv", "wire_s2c_fnv")] == [g["wire_c2s_fnv"], g["wire_s2c_fnv"]], g
 
 
+def _multi_cases():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "multi_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _multi_cases(), ids=lambda c: c["name"])
+def test_collect_patch_keeps_reference_wire_bytes_on_cpu(case):
+    """INTEGRATION.md 2a applied to the reference's IO plumbing (oracle/collect_patch.py:
+    SendBuffer::encryptData and EncryptedPackageReceiver::fetch queue their cipher calls in
+    a collect phase, the IO loop flushes once per cycle and direction) -- here over the
+    REFERENCE cipher through a CPU stand-in queue (oracle/_ref/io_multi_cpucollect).  The
+    patched plumbing's wire bytes equal the unpatched reference build's
+    (tests/golden/multi_cases.json), so the deferral and ordering are right independently
+    of the GPU; tests/test_gpu_dropin.py runs the same plumbing on EncryptorBatch."""
+    import json
+    import subprocess
+    exe = _ref_exe("io_multi_cpucollect")
+    out = subprocess.run([exe, "1" if case["mode"] == "stream" else "0", str(case["keylen"]), str(case["conns"]),
+                          str(case["quests_per_conn"]), str(case["payload"]), str(case["window"]),
+                          str(case["threads"])], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["build"] == "cpucollect" and d["ok"] and d["answers_ok"], d
+    assert d["flushes"] > 0
+    for k in ("wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv"):
+        assert d[k] == case[k], (k, d[k], case[k])
+
+
 def test_dropin_builds_bind_the_cipher_to_libfpnn_aes():
     """The drop-in builds of the reference callers (oracle/Makefile `dropin`) define no
     cipher of their own: every Encryptor method and rijndael_* call they make is an
@@ -293,7 +322,7 @@ def test_dropin_builds_bind_the_cipher_to_libfpnn_aes():
     (PackageEncryptor carries this header's _ctx member: the layout differs from
     core/Encryptor.h, so a wrong header would not link against these symbols consistently)."""
     import subprocess
-    for name in ("framing_dropin", "io_echo_dropin"):
+    for name in ("framing_dropin", "io_echo_dropin", "io_multi_dropin", "io_multi_batched"):
         exe = _ref_exe(name)
         ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
         assert "libfpnn_aes.so" in ldd, ldd
@@ -302,4 +331,7 @@ def test_dropin_builds_bind_the_cipher_to_libfpnn_aes():
         assert not [s for s in defined if "rijndael_" in s or "Encryptor::encrypt" in s or "Encryptor::decrypt" in s]
         undef = [s.split(" U ")[-1] for s in syms if " U " in s]
         assert "fpnn::encryptor_serial()" in undef  # only include/Encryptor.h's constructor calls this
-        assert any("fpnn::PackageEncryptor::decrypt" in u for u in undef)
+        if name == "io_multi_batched":  # the patched call sites queue into the product's collector
+            assert "fpnn::EncryptorBatch::flush()" in undef
+        else:
+            assert any("fpnn::PackageEncryptor::decrypt" in u for u in undef)
