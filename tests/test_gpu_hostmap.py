@@ -99,7 +99,7 @@ def _triples(rng, ntri, nkeys):
     lens, slots = [], []
     for t in range(ntri):
         a, b = (2 * t) % nkeys, (2 * t + 1) % nkeys
-        lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(2000, 9000))]
+        lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(4000, 20000))]
         slots += [a, b, a]
     return np.array(lens, np.uint32), np.array(slots, np.uint32)
 
@@ -119,7 +119,7 @@ def test_mapped_perkey_inplace_after_growth(oracle, arenas, keylen):
     try:
         rng = np.random.default_rng(7700 + keylen)
         nkeys = 7
-        lens, slots = _triples(rng, 400, nkeys)
+        lens, slots = _triples(rng, 1400, nkeys)  # ~3.5 chunks per wave of the grid: runs are reached
         keys = rng.integers(0, 256, nkeys * keylen, dtype=np.uint8)
         ivs = rng.integers(0, 256, nkeys * 16, dtype=np.uint8)
         ks = fpnn_amd.KeySet(eng, keys.tobytes(), keylen, ivs.tobytes())

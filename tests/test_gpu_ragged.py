@@ -331,10 +331,11 @@ def test_offsets_beyond_2gib(engine, oracle, stream):
 
 
 @pytest.mark.parametrize("env", [{"FPNN_AES_K1R_RUNS": "0"}, {"FPNN_AES_K1R_RUNS": "1"}], ids=["runs0", "runs1"])
-@pytest.mark.parametrize("stream", [False, True])
-@pytest.mark.parametrize("keylen", [16, 32])
-@pytest.mark.parametrize("inplace", [False, True])
-def test_interior_runs_after_key_switch(oracle, env, stream, keylen, inplace):
+@pytest.mark.parametrize("stream,keylen,inplace,nkeys",
+                         [(st, kl, ip, 8) for st in (False, True) for kl in (16, 32) for ip in (False, True)] +
+                         # one key, AES-256 package: the kernel the runs are built into (C4, R1)
+                         [(False, 32, False, 1), (False, 32, True, 1)])
+def test_interior_runs_after_key_switch(oracle, env, stream, keylen, inplace, nkeys):
     """K1r's interior runs (FPNN_AES_K1R_RUNS, k_ragged.hip) on per-key batches whose
     chunks end on another slot's pass: triples (short slot A, short slot B, long slot A),
     so the chunk before a long segment's run holds A, B, A and the general path's last
@@ -348,12 +349,14 @@ def test_interior_runs_after_key_switch(oracle, env, stream, keylen, inplace):
     from conftest import _env_engine
     eng = _env_engine(env)
     try:
-        rng = np.random.default_rng(4100 + 10 * keylen + 2 * stream + len(str(env)))
-        ntri, nkeys = 120, 8
+        rng = np.random.default_rng(4100 + 10 * keylen + 2 * stream + len(str(env)) + nkeys)
+        # big enough that every wave of the persistent grid (256 CUs x 16 waves) owns several
+        # chunks -- a wave with one chunk never reaches a run (round 4's 120 triples never did)
+        ntri = 1400
         lens, slots = [], []
         for t in range(ntri):
             a, b = (2 * t) % nkeys, (2 * t + 1) % nkeys
-            lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(2000, 9000))]
+            lens += [int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(4000, 20000))]
             slots += [a, b, a]
         lens = np.array(lens, np.int64)
         slots = np.array(slots, np.int32)

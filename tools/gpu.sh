@@ -20,6 +20,8 @@
 #   s1               S1 (stream host frames) twice with the host-stats breakdown
 #   ab:<VAR>:<list>[:<vals>]  same-box A/B of a dispatch knob: the configs with VAR=0, VAR=1 (or each of
 #                    the comma list vals), twice
+#   iomulti          tools/bench_io_multi.py (echoes/s through FPNN's IO plumbing: reference vs batched)
+#   ldsprobe         tools/probe/lds_ceiling (compute-only LDS ceilings: b32 vs b64 images, bare loops)
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
@@ -90,6 +92,8 @@ for step in "$@"; do
         echo "   $var=$v #$i: $(grep -h '^{"configs"' "$OUT/ab_${var}_${v}_$i.log" | cut -c1-700)"
       done; done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
+    ldsprobe) run lds_ceiling 300 tools/probe/lds_ceiling ;;
+    iomulti) run iomulti 600 python -u tools/bench_io_multi.py ;;  # (built on the CPU side: hipcc ... lds_ceiling.hip)
     percall) run percall 300 python -u tools/bench_percall.py ;;
     percall_trace) percall_exe
       run percall_trace 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv \
