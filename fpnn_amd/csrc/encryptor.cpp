@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -169,8 +170,7 @@ void StreamEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:63-7
 void EncryptorBatch::add(Encryptor *enc, bool encrypt, uint8_t *dest, const uint8_t *src, int len,
                          std::string *buffer) {
     if (!enc) throw EncryptorError("EncryptorBatch: null encryptor");
-    if (!dynamic_cast<PackageEncryptor *>(enc) && !dynamic_cast<StreamEncryptor *>(enc))
-        throw EncryptorError("EncryptorBatch: unsupported Encryptor subclass");
+    if (enc->_kind != 1 && enc->_kind != 2) throw EncryptorError("EncryptorBatch: unsupported Encryptor subclass");
     if (!buffer && len <= 0) return;  // the per-call methods do nothing for len <= 0
     _ops.push_back({enc, dest, src, buffer ? (uint32_t)buffer->size() : (uint32_t)len, encrypt, buffer});
     _bytes += _ops.back().len;
@@ -229,8 +229,17 @@ void encryptor_retire(uint64_t serial) {
 // (fpnn_aes_keyset_set).  Stream state of the touched slots is staged in iv/pos, sized
 // like the table, so a flush never touches more than its own connections.  The table
 // belongs to one engine, identified by its id.
+// Key-table generations: an Encryptor caches (tag, slot) of the table it was last given a
+// slot in (Encryptor::_batchTag / _batchSlot); a table takes a new tag whenever it starts
+// over, so no stale slot is ever used.  Flush ids mark the stream encryptors a flush lists.
+uint64_t next_batch_tag() {
+    static std::atomic<uint64_t> n{1};
+    return n.fetch_add(1, std::memory_order_relaxed);
+}
+
 struct EncryptorBatch::KeyTable {
     uint64_t engine_id = 0;
+    uint64_t tag = next_batch_tag();
     fpnn_aes_keyset *ks = nullptr;
     std::unordered_map<uint64_t, uint32_t> slot;
     uint32_t next = 0;
@@ -292,11 +301,33 @@ EncryptorBatch::~EncryptorBatch() {
     }
 }
 
+namespace {
+// FPNN_AES_BATCH_STATS=1: per flush, where the host time goes (stderr)
+struct BatchStats {
+    bool on = getenv("FPNN_AES_BATCH_STATS") != nullptr;
+    double t0 = 0, table = 0, frames = 0, call = 0, post = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+};
+}  // namespace
+
 void EncryptorBatch::flush() {
     std::vector<Op> ops;
     ops.swap(_ops);
     _bytes = 0;
     if (ops.empty()) return;
+    BatchStats bs;
+    if (bs.on) bs.t0 = BatchStats::now();
+    struct Report {
+        BatchStats &s;
+        size_t n;
+        ~Report() {
+            if (s.on)
+                fprintf(stderr, "[fpnn_aes batch] %zu ops: %.3f ms (table %.3f, frames %.3f, device call %.3f, post %.3f)\n",
+                        n, 1e3 * (BatchStats::now() - s.t0), 1e3 * s.table, 1e3 * s.frames, 1e3 * s.call, 1e3 * s.post);
+        }
+    } report{bs, ops.size()};
     int rc;
     const fpnn_aes::Lease lease = thread_engine(&rc);
     fpnn_aes_engine *e = lease.engine();
@@ -307,29 +338,42 @@ void EncryptorBatch::flush() {
         bool stream, encrypt, prefix;
         int nrounds;
         std::vector<size_t> idx;
+        std::vector<StreamEncryptor *> members;  // stream groups: each encryptor once, first use first
     };
     std::vector<Group> groups;
-    std::unordered_map<const StreamEncryptor *, bool> stream_dir;
+    static std::atomic<uint64_t> flush_ids{1};
+    const uint64_t fid = flush_ids.fetch_add(1, std::memory_order_relaxed);
+    size_t g = 0;  // (consecutive ops usually share a group)
     for (size_t i = 0; i < ops.size(); i++) {
         const Op &op = ops[i];
-        StreamEncryptor *se = dynamic_cast<StreamEncryptor *>(op.enc);
-        const bool stream = se != nullptr;
+        const bool stream = op.enc->_kind == 2;
+        StreamEncryptor *se = stream ? static_cast<StreamEncryptor *>(op.enc) : nullptr;
         const bool prefix = !stream && op.buffer != nullptr;
         const int nr = stream ? se->_ctx.nrounds : static_cast<PackageEncryptor *>(op.enc)->_ctx.nrounds;
-        if (stream) {
-            auto it = stream_dir.emplace(se, op.encrypt).first;
-            if (it->second != op.encrypt)
-                throw EncryptorError("EncryptorBatch: a StreamEncryptor used in both directions in one batch");
+        bool first = false;
+        if (stream) {  // _batchSeen = flush id << 1 | direction
+            if ((se->_batchSeen >> 1) == fid) {
+                if ((se->_batchSeen & 1) != (uint64_t)op.encrypt)
+                    throw EncryptorError("EncryptorBatch: a StreamEncryptor used in both directions in one batch");
+            } else {
+                se->_batchSeen = fid << 1 | (uint64_t)op.encrypt;
+                first = true;
+            }
             if (op.buffer && op.buffer->empty()) continue;  // StreamEncryptor::encrypt(std::string*) of ""
         }
-        size_t g = 0;
-        while (g < groups.size() && !(groups[g].stream == stream && groups[g].encrypt == op.encrypt &&
-                                      groups[g].prefix == prefix && groups[g].nrounds == nr))
-            g++;
-        if (g == groups.size()) groups.push_back({stream, op.encrypt, prefix, nr, {}});
+        if (!(g < groups.size() && groups[g].stream == stream && groups[g].encrypt == op.encrypt &&
+              groups[g].prefix == prefix && groups[g].nrounds == nr)) {
+            g = 0;
+            while (g < groups.size() && !(groups[g].stream == stream && groups[g].encrypt == op.encrypt &&
+                                          groups[g].prefix == prefix && groups[g].nrounds == nr))
+                g++;
+            if (g == groups.size()) groups.push_back({stream, op.encrypt, prefix, nr, {}, {}});
+        }
         groups[g].idx.push_back(i);
+        if (first) groups[g].members.push_back(se);
     }
     for (const Group &gr : groups) {
+        const double tg = bs.on ? BatchStats::now() : 0;
         // ---- this key length's table: new connections get slots, uploaded in one copy ----
         KeyTable *&tp = _tables[(gr.nrounds - 10) / 2];
         if (tp && tp->engine_id != eid) {  // flushed from another thread (engine): start a table there
@@ -350,18 +394,20 @@ void EncryptorBatch::flush() {
         if (t.collect()) {  // mostly dead connections: start over (live ones re-add below or later)
             t.slot.clear();
             t.next = 0;
+            t.tag = next_batch_tag();
         }
-        std::vector<const Encryptor *> members;  // first use in this group, in order
         std::vector<uint32_t> slots(gr.idx.size());
         for (int attempt = 0;; attempt++) {
             std::vector<fpnn_aes_schedule> scheds;
             std::vector<uint8_t> ivs;
             std::vector<uint64_t> fresh;
             const uint32_t first_new = t.next;
-            members.clear();
-            std::unordered_map<uint64_t, bool> seen;
             for (size_t k = 0; k < gr.idx.size(); k++) {
-                const Encryptor *enc = ops[gr.idx[k]].enc;
+                Encryptor *enc = ops[gr.idx[k]].enc;
+                if (enc->_batchTag == t.tag) {  // a connection this table already holds
+                    slots[k] = enc->_batchSlot;
+                    continue;
+                }
                 auto ins = t.slot.emplace(enc->_serial, t.next);
                 if (ins.second) {
                     const rijndael_context &ctx = gr.stream ? static_cast<const StreamEncryptor *>(enc)->_ctx
@@ -372,11 +418,13 @@ void EncryptorBatch::flush() {
                     t.next++;
                 }
                 slots[k] = ins.first->second;
-                if (seen.emplace(enc->_serial, true).second) members.push_back(enc);
+                enc->_batchTag = t.tag;
+                enc->_batchSlot = slots[k];
             }
             if (t.next > kTableMaxSlots && attempt == 0) {  // start over with this group's connections only
                 t.slot.clear();
                 t.next = 0;
+                t.tag = next_batch_tag();
                 continue;
             }
             rc = fpnn_aes_keyset_set(t.ks, first_new, (uint32_t)scheds.size(), scheds.data(), ivs.data());
@@ -389,51 +437,57 @@ void EncryptorBatch::flush() {
             t.watch(fresh);
             break;
         }
+        double tt = bs.on ? BatchStats::now() : 0;
+        if (bs.on) bs.table += tt - tg;
         std::vector<fpnn_aes_host_frame> frames(gr.idx.size());
-        std::vector<std::string> framed;  // package std::string outputs (len + 4)
-        if (gr.prefix) framed.resize(gr.idx.size());
         for (size_t k = 0; k < gr.idx.size(); k++) {
             Op &op = ops[gr.idx[k]];
             fpnn_aes_host_frame &f = frames[k];
             f.len = op.len;
             f.key_slot = slots[k];
             if (op.buffer) {
+                // package std::string: htole32(len) || C is written over the buffer itself,
+                // 4 bytes longer (a frame's source is read before its output is written,
+                // fpnn_aes_package_host); stream: same length, in place
+                if (gr.prefix) op.buffer->append(sizeof(uint32_t), '\0');
                 f.src = reinterpret_cast<const uint8_t *>(op.buffer->data());
-                if (gr.prefix) {
-                    framed[k].assign(op.len + sizeof(uint32_t), '\0');
-                    f.dst = reinterpret_cast<uint8_t *>(&framed[k][0]);
-                } else {
-                    f.dst = reinterpret_cast<uint8_t *>(&(*op.buffer)[0]);  // in place, same length
-                }
+                f.dst = reinterpret_cast<uint8_t *>(&(*op.buffer)[0]);
             } else {
                 f.src = op.src;
                 f.dst = op.dest;
             }
         }
+        if (bs.on) {
+            const double t = BatchStats::now();
+            bs.frames += t - tt;
+            tt = t;
+        }
         if (!gr.stream) {
             rc = fpnn_aes_package_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                        gr.prefix ? FPNN_AES_F_WIRE_PREFIX : 0);
             if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: package batch: " + describe(rc));
-            if (gr.prefix)
-                for (size_t k = 0; k < gr.idx.size(); k++) ops[gr.idx[k]].buffer->swap(framed[k]);
+            if (bs.on) {
+                const double t = BatchStats::now();
+                bs.call += t - tt;
+                tt = t;
+            }
+            if (bs.on) bs.post += BatchStats::now() - tt;
         } else {
             const uint32_t cnt = fpnn_aes_keyset_count(t.ks);
             if (t.pos.size() < cnt) {
                 t.iv.resize(16 * (size_t)cnt);
                 t.pos.resize(cnt);
             }
-            for (const Encryptor *m : members) {  // the touched streams' current (iv, pos)
-                const StreamEncryptor *se = static_cast<const StreamEncryptor *>(m);
-                const uint32_t sl = t.slot[m->_serial];
+            for (const StreamEncryptor *se : gr.members) {  // the touched streams' current (iv, pos)
+                const uint32_t sl = se->_batchSlot;
                 memcpy(&t.iv[16 * (size_t)sl], se->_iv, 16);
                 t.pos[sl] = (uint32_t)se->_pos;
             }
             rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                       t.iv.data(), t.pos.data());
             if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: stream batch: " + describe(rc));
-            for (const Encryptor *m : members) {
-                StreamEncryptor *se = const_cast<StreamEncryptor *>(static_cast<const StreamEncryptor *>(m));
-                const uint32_t sl = t.slot[m->_serial];
+            for (StreamEncryptor *se : gr.members) {
+                const uint32_t sl = se->_batchSlot;
                 memcpy(se->_iv, &t.iv[16 * (size_t)sl], 16);
                 se->_pos = t.pos[sl];
             }

@@ -115,11 +115,23 @@ public:
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
-    unsigned parts() const { return (unsigned)th_.size() + 1; }
+    // parts a host-frame call splits its copies into: this pool's threads + the caller,
+    // shared fairly among the engines whose host-frame calls run at the same moment (every
+    // engine has a pool of min(16, cores) threads: several IO threads flushing at once would
+    // otherwise oversubscribe the box's CPU share many times over)
+    // (per device: the GPU box grants each GPU its own CPU share)
+    unsigned parts() const {
+        const unsigned all = max_parts();
+        const unsigned active = std::max(1u, g_host_active[device_ & 63].load(std::memory_order_relaxed));
+        return std::max(1u, all / active);
+    }
+    unsigned max_parts() const { return (unsigned)th_.size() + 1; }
+    void set_device(int d) { device_ = d; }
+    static std::atomic<unsigned> g_host_active[64];
 
     template <class F>
     void run(unsigned want, const F &fn) {
-        want = std::max(1u, std::min(want, parts()));
+        want = std::max(1u, std::min(want, max_parts()));
         if (want == 1) {
             fn(0u);
             return;
@@ -141,7 +153,7 @@ public:
 
     // memcpy jobs split into contiguous, byte-balanced ranges
     void copy(const std::vector<CopyJob> &jobs, uint64_t total, unsigned want) {
-        want = std::max(1u, std::min<unsigned>(want, (unsigned)std::min<size_t>(jobs.size(), parts())));
+        want = std::max(1u, std::min<unsigned>(want, (unsigned)std::min<size_t>(jobs.size(), max_parts())));
         std::vector<size_t> cut(want + 1, jobs.size());
         cut[0] = 0;
         uint64_t acc = 0;
@@ -180,7 +192,19 @@ private:
     unsigned active_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    int device_ = 0;
 };
+
+std::atomic<unsigned> HostPool::g_host_active[64];
+
+// a host-frame call in progress on a device (HostPool::parts shares the copy threads
+// among the calls of that device)
+struct HostActive {
+    int d;
+    explicit HostActive(int device) : d(device & 63) { HostPool::g_host_active[d].fetch_add(1, std::memory_order_relaxed); }
+    ~HostActive() { HostPool::g_host_active[d].fetch_sub(1, std::memory_order_relaxed); }
+};
+
 
 }  // namespace
 
@@ -1439,7 +1463,10 @@ unsigned host_threads() {
 }
 
 HostPool *pool_of(fpnn_aes_engine *e) {
-    if (!e->pool) e->pool.reset(new HostPool(host_threads() - 1));
+    if (!e->pool) {
+        e->pool.reset(new HostPool(host_threads() - 1));
+        e->pool->set_device(e->device);
+    }
     return e->pool.get();
 }
 
@@ -1601,8 +1628,17 @@ void group_streams(const fpnn_aes_host_frame *frames, uint32_t n, uint32_t nkeys
 // stream split across chunks continues from the state the previous chunk left.
 int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_host_frame *frames, uint32_t n,
                   const fpnn_aes_keyset *keys, uint32_t flags, uint8_t *iv_state, uint32_t *pos_state) {
+    const HostActive active_call(e->device);
     const uint64_t pre = (!stream && (flags & FPNN_AES_F_WIRE_PREFIX)) ? 4 : 0;
-    const uint64_t kChunk = 32ull << 20;  // input bytes per pipeline chunk
+    // input bytes per pipeline chunk: 32 MiB, and for package calls of less than 128 MiB a
+    // quarter of the call (at least 1 MiB), so even one IO cycle's flush of a few MiB
+    // overlaps its gather, copies, kernel and scatter (io_multi: 8 MiB flushes)
+    uint64_t kChunk = 32ull << 20;
+    if (!stream) {
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < n && tot < (128ull << 20); i++) tot += frames[i].len;
+        kChunk = std::min<uint64_t>(kChunk, std::max<uint64_t>(1ull << 20, tot / 4));
+    }
     // ---- segments in staging order -------------------------------------------------
     std::vector<uint32_t> order;  // frame indices
     std::vector<StreamSeg> segs;  // stream mode only (package chunks walk `frames` directly)
@@ -1976,6 +2012,7 @@ int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
 // descriptors.
 int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                     const fpnn_aes_keyset *keys, uint32_t flags, const MapView &v, uint32_t *done) {
+    const HostActive active_call(e->device);
     const uint64_t pre = (flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
     static const uint64_t kChunk = [] {     // input bytes per full chunk (FPNN_AES_MAP_CHUNK_MB)
         const char *x = getenv("FPNN_AES_MAP_CHUNK_MB");
@@ -2237,6 +2274,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
 // then per stream segment off u64 | len u32 | slot u32.
 int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                            const fpnn_aes_keyset *keys, const MapView &v, uint8_t *iv_state, uint32_t *pos_state) {
+    const HostActive active_call(e->device);
     static const uint64_t kChunk = [] {
         const char *x = getenv("FPNN_AES_MAP_CHUNK_MB");
         return (x && atoi(x) > 0 ? (uint64_t)atoi(x) : 32ull) << 20;

@@ -52,6 +52,13 @@ protected:
     uint8_t _key[32];
     size_t _keyLen;
     uint64_t _serial;
+    // EncryptorBatch bookkeeping: the subclass (1 package, 2 stream; 0 other), and this
+    // encryptor's slot in the key table tagged _batchTag (a table generation), so a flush
+    // finds a known connection's slot without a lookup; _batchSeen = the last flush that
+    // listed it (stream state hand-off)
+    uint8_t _kind = 0;
+    uint32_t _batchSlot = 0;
+    uint64_t _batchTag = 0, _batchSeen = 0;
 
 public:
     Encryptor(uint8_t *key, size_t key_len, uint8_t *iv) {
@@ -60,7 +67,7 @@ public:
         _keyLen = key_len;
         _serial = encryptor_serial();
     }
-    Encryptor(const Encryptor &o) : _keyLen(o._keyLen), _serial(encryptor_serial()) {
+    Encryptor(const Encryptor &o) : _keyLen(o._keyLen), _serial(encryptor_serial()), _kind(o._kind) {
         memcpy(_iv, o._iv, 16);
         memcpy(_key, o._key, sizeof _key);
     }
@@ -71,6 +78,7 @@ public:
             _keyLen = o._keyLen;
             encryptor_retire(_serial);
             _serial = encryptor_serial();
+            _batchTag = _batchSeen = 0;  // a new serial: no table slot yet
         }
         return *this;
     }
@@ -89,6 +97,7 @@ class PackageEncryptor : public Encryptor {
 public:
     PackageEncryptor(uint8_t *key, size_t key_len, uint8_t *iv) : Encryptor(key, key_len, iv) {
         rijndael_setup_encrypt(&_ctx, (const uint8_t *)_key, key_len);
+        _kind = 1;
     }
     virtual ~PackageEncryptor() {}
 
@@ -109,6 +118,7 @@ class StreamEncryptor : public Encryptor {
 public:
     StreamEncryptor(uint8_t *key, size_t key_len, uint8_t *iv) : Encryptor(key, key_len, iv), _pos(0) {
         rijndael_setup_encrypt(&_ctx, (const uint8_t *)_key, key_len);
+        _kind = 2;
     }
     virtual ~StreamEncryptor() {}
 
