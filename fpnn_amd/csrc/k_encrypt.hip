@@ -22,6 +22,13 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
     RoundKeys<NR> rku;
     if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
+    // Package mode, one key, uniform lengths (C2): every chain starts from the same IV, so
+    // its first keystream block E_k(IV) is one constant (point 3); and
+    // every lane starts its chains at the same step, so the wave skips those 14 rounds
+    // together.  Computed once per lane here.
+    constexpr bool kConstFirst = LAYOUT == LAYOUT_UNIFORM && KM == KEY_UNIFORM && !STREAM;
+    uint4 eiv = make_uint4(0, 0, 0, 0);
+    if (kConstFirst) eiv = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
 
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
@@ -78,7 +85,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             uint32_t h = (mis & 15u) ? 0u : ((128u - mis) & 127u) >> 4;
             h = h < nfull ? h : nfull;
             for (; i < h; i++) {
-                iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ load16(p);
+                iv = (kConstFirst && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ load16(p);
                 store16(q, iv);
                 p += 16;
                 q += 16;
@@ -101,7 +108,12 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
                 for (int j = 0; j < C; j++) nx[j] = more ? load16(p + 16 * (C + j)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
                 for (int j = 0; j < C; j++) {
-                    iv = (FENCE ? aes_encrypt_block_fenced<NR, NT>(iv, rk, T) : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ a[j];
+                    uint4 ks;
+                    if (kConstFirst && j == 0 && i == 0)  // the chain's first block (wave-uniform)
+                        ks = eiv;
+                    else
+                        ks = FENCE ? aes_encrypt_block_fenced<NR, NT>(iv, rk, T) : aes_encrypt_block<NR, NT>(iv, rk, T);
+                    iv = ks ^ a[j];
                     a[j] = iv;
                 }
 #pragma unroll
@@ -115,7 +127,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
         for (; i < nfull; i++) {
             const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
-            iv = aes_encrypt_block<NR, NT>(iv, rk, T) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            iv = (kConstFirst && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ pt;  // C_i = P_i ^ E(C_{i-1})
             store16(q, iv);
             pt = pn;
             p += 16;
@@ -123,7 +135,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         }
         rem &= 15u;
         if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
-            const uint4 ks = aes_encrypt_block<NR, NT>(iv, rk, T);
+            const uint4 ks = kConstFirst && nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T);
             const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
             store_bytes(q, o, 0, (int)rem);
             iv = select_bytes(byte_mask(0, (int)rem), o, ks);
