@@ -20,6 +20,7 @@
 #   s1               S1 (stream host frames) twice with the host-stats breakdown
 #   ab:<VAR>:<list>[:<vals>]  same-box A/B of a dispatch knob: the configs with VAR=0, VAR=1 (or each of
 #                    the comma list vals), twice
+#   k0s              tools/bench_k0s.py (resident small-call servers beside batch kernels, both ways)
 #   iomulti          tools/bench_io_multi.py (echoes/s through FPNN's IO plumbing: reference vs batched)
 #   ldsprobe         tools/probe/lds_ceiling (compute-only LDS ceilings: b32 vs b64 images, bare loops)
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
@@ -93,7 +94,8 @@ for step in "$@"; do
       done; done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
     ldsprobe) run lds_ceiling 300 tools/probe/lds_ceiling ;;
-    iomulti) run iomulti 600 python -u tools/bench_io_multi.py ;;  # (built on the CPU side: hipcc ... lds_ceiling.hip)
+    iomulti) run iomulti 600 python -u tools/bench_io_multi.py ;;
+    k0s) run k0s 600 python -u tools/bench_k0s.py ;;  # (built on the CPU side: hipcc ... lds_ceiling.hip)
     percall) run percall 300 python -u tools/bench_percall.py ;;
     percall_trace) percall_exe
       run percall_trace 300 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv \
