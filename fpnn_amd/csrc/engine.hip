@@ -430,6 +430,8 @@ bool is_uniform_layout(const fpnn_aes_batch *b) {
     return !b->in_off && !b->out_off && !b->len && !b->key_slot;
 }
 
+void batch_signal(int device);  // (below, with the small-call server)
+
 int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
     int rc = check_batch(e, b);
     if (rc) return rc;
@@ -438,6 +440,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         return FPNN_AES_ERR_ARG;  // the 4-byte prefix needs a distinct output layout
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
+    batch_signal(e->device);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
@@ -514,6 +517,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (b->flags & FPNN_AES_F_WIRE_PREFIX) return FPNN_AES_ERR_ARG;
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
+    batch_signal(e->device);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     // small ragged batches: block map (+ stream snapshot) in one single-workgroup kernel
     const bool small_map = b->count <= block_map_small_max();
@@ -1100,6 +1104,7 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
     s.abs_off = e->d_fr_off;
     s.abs_slot = per_key ? e->d_fr_slot : nullptr;
     static_assert(sizeof(ScanResult) == sizeof(fpnn_aes_frame_scan), "scan layout");
+    batch_signal(e->device);
     HIP_TRY(launch_scan_frames(s, false, e->num_cus, e->stream));
     // every frame slot is one package segment (unused ones have length 0)
     fpnn_aes_batch fb;
@@ -1138,6 +1143,7 @@ int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
     s.frame_off = frame_off;
     s.frame_len = frame_len;
     s.scan = reinterpret_cast<ScanResult *>(scan);
+    batch_signal(e->device);
     HIP_TRY(launch_scan_frames(s, true, e->num_cus, e->stream));
     return FPNN_AES_OK;
 }
@@ -1241,6 +1247,36 @@ int cfb_small_launch(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encr
 // (idle, lifetime) before seeing the request is relaunched; after 20 ms of spinning the
 // stream sync -- which returns once the server has left, and reports a failed kernel --
 // settles it.
+// Batch-activity words, one per device (64-byte apart) in pinned host memory, created with
+// the first server: the host bumps its device's word before it queues batch kernels, and
+// every server of that device leaves after its current request (kernels.hpp,
+// launch_cfb_server).  An idle server would otherwise hold a CU -- and its hardware queue,
+// which the box shares among streams (GPU_MAX_HW_QUEUES = 4) -- for up to its 2 ms
+// lifetime while a persistent batch grid waits for it.
+std::atomic<uint32_t *> g_yield{nullptr};
+std::mutex g_yield_mu;
+
+uint32_t *yield_words() {
+    uint32_t *y = g_yield.load(std::memory_order_acquire);
+    if (y) return y;
+    std::lock_guard<std::mutex> lk(g_yield_mu);
+    y = g_yield.load(std::memory_order_relaxed);
+    if (!y) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, 64 * 64, hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) != hipSuccess)
+            return nullptr;
+        memset(p, 0, 64 * 64);
+        y = static_cast<uint32_t *>(p);
+        g_yield.store(y, std::memory_order_release);
+    }
+    return y;
+}
+
+// before batch kernels are queued on a device (no-op until a server ever ran)
+void batch_signal(int device) {
+    if (uint32_t *y = g_yield.load(std::memory_order_acquire)) __atomic_fetch_add(y + 16 * (device & 63), 1u, __ATOMIC_RELEASE);
+}
+
 bool server_enabled() {
     static const bool on = [] {
         const char *v = getenv("FPNN_AES_SMALL_SERVER");
@@ -1257,8 +1293,12 @@ int launch_server(fpnn_aes_engine *e) {
         e->srv_idle_ticks = (uint64_t)khz / 20;   // 50 us without a request
         e->srv_life_ticks = (uint64_t)khz * 2;    // 2 ms in any case
     }
+    uint32_t *yh = yield_words();
+    if (!yh) return hip_fail(hipErrorOutOfMemory, "hipHostMalloc(yield)");
+    uint32_t *yd = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&yd), yh + 16 * (e->device & 63), 0));
     const uint32_t epoch = ++e->srv_epoch;
-    HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, e->stream));
+    HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, yd, e->stream));
     return FPNN_AES_OK;
 }
 
@@ -2822,6 +2862,7 @@ int ecdh_launch(fpnn_aes_engine *e, int curve, const EccConst &c, const EcdhJob 
         return FPNN_AES_ERR_ARG;
     }
     DeviceGuard g(e->device);
+    batch_signal(e->device);
     HIP_TRY(launch_ecdh(c, j, curve, e->stream));
     return FPNN_AES_OK;
 }

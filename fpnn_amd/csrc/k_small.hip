@@ -15,7 +15,8 @@
 //   K0s k_cfb_server : the same call body in a workgroup that stays resident while calls
 //       keep coming: it polls a mailbox in pinned host memory, serves each request and
 //       publishes its sequence number; between requests it checks an idle interval, a
-//       lifetime bound and a stop flag, and leaves on any of them.  No launch, no table
+//       lifetime bound, a stop flag and the device's batch-activity word (bumped by the
+//       host before it queues batch kernels), and leaves on any of them.  No launch, no table
 //       fill and no kernel-argument fetch per call; the host relaunches it once it has left.
 // Decrypt: one lane per 16-byte block (block i's keystream is E(C_{i-1})).  Encrypt: the
 // serial chain on one quad (K2c's column round, coop.hpp) -- C_i = P_i ^ E(C_{i-1}).
@@ -43,9 +44,13 @@ __device__ __forceinline__ uint32_t load_acquire(const uint32_t *p) {
 // (x86 stores become visible in program order, and the line is read whole), so a new seq
 // comes with its own header.  The acquire fence that follows orders the body's loads.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t load_sys16(const void *p) {
+// with the batch-activity word read beside it (both in flight together: one PCIe round
+// trip per poll)
+__device__ __forceinline__ u32x4_t load_sys16_and(const void *p, const uint32_t *q, uint32_t &y) {
     u32x4_t v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\tglobal_load_dword %1, %3, off sc0 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(v), "=&v"(y) : "v"(p), "v"(q) : "memory");
     return v;
 }
 
@@ -170,17 +175,18 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
 // sequence number in order and stores it into resp.done after the results.
 __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *mb, const uint32_t *t0le,
                                                                  uint32_t epoch, uint64_t idle_ticks,
-                                                                 uint64_t life_ticks) {
+                                                                 uint64_t life_ticks, const uint32_t *yield) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
     __shared__ SmallShared S;
     __shared__ SmallReq rq;
     __shared__ uint32_t ctl[2][4];  // [iteration parity][action, sequence number, body blocks]
     const uint32_t t = threadIdx.x;
     fill_tables_regs(lds4, t0le[t], 32);
-    uint32_t done = 0;
+    uint32_t done = 0, y0 = 0;
     uint64_t t_start = 0, t_idle = 0;
     if (t == 0) {
         done = load_acquire(&mb->resp.done);
+        y0 = load_acquire(yield);
         t_start = t_idle = wall_clock64();
     }
     __syncthreads();
@@ -193,7 +199,8 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
         if (t == 0) {  // 1 = serve, 2 = leave
             uint32_t action = 0, s = done, nb = 0;
             for (uint32_t np = 0; action == 0; np++) {
-                const u32x4_t h = load_sys16(&mb->req);  // seq, op, len, head
+                uint32_t y;
+                const u32x4_t h = load_sys16_and(&mb->req, yield, y);  // seq, op, len, head; batch word
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 s = h.x;
                 const uint64_t now = wall_clock64();
@@ -201,7 +208,7 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
                     action = 1;
                     nb = (h.z - h.w + 15) >> 4;
                     nb = nb < kSmallMaxBytes / 16 ? nb : kSmallMaxBytes / 16;  // the host never asks for more
-                } else if (now - t_idle > idle_ticks || now - t_start > life_ticks ||
+                } else if (y != y0 || now - t_idle > idle_ticks || now - t_start > life_ticks ||
                            ((np & 31u) == 31u &&
                             __hip_atomic_load(&mb->req.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
                     action = 2;
@@ -270,9 +277,10 @@ hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipS
 }
 
 hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
-                             uint64_t life_ticks, hipStream_t st) {
+                             uint64_t life_ticks, const uint32_t *yield, hipStream_t st) {
     set_launched("cfb_server");
-    hipLaunchKernelGGL(k_cfb_server, dim3(1), dim3(kSmallThreads), 0, st, mb, t0le, epoch, idle_ticks, life_ticks);
+    hipLaunchKernelGGL(k_cfb_server, dim3(1), dim3(kSmallThreads), 0, st, mb, t0le, epoch, idle_ticks, life_ticks,
+                       yield);
     return hipGetLastError();
 }
 
