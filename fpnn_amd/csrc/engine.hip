@@ -269,6 +269,10 @@ struct fpnn_aes_engine {
     SmallMailbox *d_mb = nullptr;
     uint32_t mb_seq = 0;
     uint32_t srv_epoch = 0;
+    // the last batch work this engine queued while small-call servers exist on the device
+    // (a server relaunch on another engine waits for it: batch_fence)
+    hipEvent_t batch_ev = nullptr;
+    bool batch_ev_live = false;
     uint64_t srv_idle_ticks = 0, srv_life_ticks = 0;
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
@@ -387,6 +391,7 @@ int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
 // after the main kernel of a call: close its timing pair, remember what was launched
 int timing_end(fpnn_aes_engine *e, EventPair *pair, int which) {
     e->last_kernel[which] = last_launched();
+    batch_queued(e);
     if (pair) HIP_TRY(hipEventRecord(pair->end, e->stream));
     return FPNN_AES_OK;
 }
@@ -430,7 +435,11 @@ bool is_uniform_layout(const fpnn_aes_batch *b) {
     return !b->in_off && !b->out_off && !b->len && !b->key_slot;
 }
 
-void batch_signal(int device);  // (below, with the small-call server)
+// (below, with the small-call server)
+void batch_signal(int device);
+void batch_queued(fpnn_aes_engine *e);
+void register_engine(fpnn_aes_engine *e);
+void unregister_engine(fpnn_aes_engine *e);
 
 int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
     int rc = check_batch(e, b);
@@ -743,6 +752,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
         fpnn_aes_engine_destroy(e);
         return rc;
     }
+    register_engine(e);
     *out = e;
     return FPNN_AES_OK;
 }
@@ -797,6 +807,8 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         if (m.done) (void)hipEventDestroy(m.done);
     }
     if (e->map_stream) (void)hipStreamDestroy(e->map_stream);
+    unregister_engine(e);  // (no-op for an engine whose creation failed)
+    if (e->batch_ev) (void)hipEventDestroy(e->batch_ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return FPNN_AES_OK;
@@ -1277,6 +1289,49 @@ void batch_signal(int device) {
     if (uint32_t *y = g_yield.load(std::memory_order_acquire)) __atomic_fetch_add(y + 16 * (device & 63), 1u, __ATOMIC_RELEASE);
 }
 
+// Engines per device, for batch_fence.
+struct DeviceEngines {
+    std::mutex mu;
+    std::vector<fpnn_aes_engine *> list;
+};
+DeviceEngines g_dev_engines[64];
+
+void register_engine(fpnn_aes_engine *e) {
+    DeviceEngines &d = g_dev_engines[e->device & 63];
+    std::lock_guard<std::mutex> lk(d.mu);
+    d.list.push_back(e);
+}
+
+void unregister_engine(fpnn_aes_engine *e) {
+    DeviceEngines &d = g_dev_engines[e->device & 63];
+    std::lock_guard<std::mutex> lk(d.mu);
+    d.list.erase(std::remove(d.list.begin(), d.list.end(), e), d.list.end());
+}
+
+// after an engine queued batch kernels (once servers exist): remember where they end
+void batch_queued(fpnn_aes_engine *e) {
+    if (!g_yield.load(std::memory_order_acquire)) return;  // no server ever ran: nothing waits
+    if (!e->batch_ev && hipEventCreateWithFlags(&e->batch_ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(e->batch_ev, e->stream) == hipSuccess) e->batch_ev_live = true;
+}
+
+// Before (re)launching a small-call server: wait until the batch work other engines queued
+// on this device has finished.  A server launched meanwhile would take a CU from a
+// persistent batch grid (every workgroup holds a static share of the work, so the whole
+// call waits for that CU) -- servers leave when batch work is queued (batch_signal), and
+// do not come back until it is done.  The per-call request waits for the batch instead,
+// which it would do anyway: the batch grid holds every CU.
+void batch_fence(fpnn_aes_engine *e) {
+    DeviceEngines &d = g_dev_engines[e->device & 63];
+    std::lock_guard<std::mutex> lk(d.mu);
+    for (fpnn_aes_engine *o : d.list) {
+        if (o == e || !o->batch_ev_live) continue;
+        hipError_t q;
+        while ((q = hipEventQuery(o->batch_ev)) == hipErrorNotReady) __builtin_ia32_pause();
+        if (q == hipSuccess) o->batch_ev_live = false;
+    }
+}
+
 bool server_enabled() {
     static const bool on = [] {
         const char *v = getenv("FPNN_AES_SMALL_SERVER");
@@ -1325,13 +1380,16 @@ int cfb_small_server(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encr
     const int which = encrypt ? FPNN_AES_K_ENCRYPT : FPNN_AES_K_DECRYPT;
     e->last_kernel[which] = "cfb_server";
     // a server is alive unless none was launched or the last one has stored its epoch
-    if (e->srv_epoch == 0 || __atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch)
+    if (e->srv_epoch == 0 || __atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch) {
+        batch_fence(e);
         if (int rc = launch_server(e)) return rc;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spins = 0; __atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq; spins++) {
         __builtin_ia32_pause();
         if (__atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch &&
             __atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq) {
+            batch_fence(e);
             if (int rc = launch_server(e)) return rc;  // it left before seeing this request
             continue;
         }
@@ -2864,6 +2922,7 @@ int ecdh_launch(fpnn_aes_engine *e, int curve, const EccConst &c, const EcdhJob 
     DeviceGuard g(e->device);
     batch_signal(e->device);
     HIP_TRY(launch_ecdh(c, j, curve, e->stream));
+    batch_queued(e);
     return FPNN_AES_OK;
 }
 
