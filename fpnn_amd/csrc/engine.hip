@@ -373,6 +373,12 @@ int stream_idle(fpnn_aes_engine *e) {
     return FPNN_AES_ERR_DEVICE;
 }
 
+// (below, with the small-call server)
+void batch_signal(int device);
+void batch_queued(fpnn_aes_engine *e);
+void register_engine(fpnn_aes_engine *e);
+void unregister_engine(fpnn_aes_engine *e);
+
 int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
     *pair = nullptr;
     if (!e->timing) return FPNN_AES_OK;
@@ -435,11 +441,6 @@ bool is_uniform_layout(const fpnn_aes_batch *b) {
     return !b->in_off && !b->out_off && !b->len && !b->key_slot;
 }
 
-// (below, with the small-call server)
-void batch_signal(int device);
-void batch_queued(fpnn_aes_engine *e);
-void register_engine(fpnn_aes_engine *e);
-void unregister_engine(fpnn_aes_engine *e);
 
 int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
     int rc = check_batch(e, b);
