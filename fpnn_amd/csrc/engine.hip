@@ -272,7 +272,8 @@ struct fpnn_aes_engine {
     // the last batch work this engine queued while small-call servers exist on the device
     // (a server relaunch on another engine waits for it: batch_fence)
     hipEvent_t batch_ev = nullptr;
-    bool batch_ev_live = false;
+    std::atomic<bool> batch_pending{false};  // batch kernels about to be queued (batch_signal)
+    std::atomic<bool> batch_ev_live{false};  // batch_ev marks the end of queued batch work
     uint64_t srv_idle_ticks = 0, srv_life_ticks = 0;
     // host staging for fpnn_aes_cfb_host
     uint8_t *h_stage = nullptr;
@@ -374,7 +375,7 @@ int stream_idle(fpnn_aes_engine *e) {
 }
 
 // (below, with the small-call server)
-void batch_signal(int device);
+void batch_signal(fpnn_aes_engine *e);
 void batch_queued(fpnn_aes_engine *e);
 void register_engine(fpnn_aes_engine *e);
 void unregister_engine(fpnn_aes_engine *e);
@@ -450,7 +451,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         return FPNN_AES_ERR_ARG;  // the 4-byte prefix needs a distinct output layout
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
-    batch_signal(e->device);
+    batch_signal(e);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
@@ -527,7 +528,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (b->flags & FPNN_AES_F_WIRE_PREFIX) return FPNN_AES_ERR_ARG;
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
-    batch_signal(e->device);
+    batch_signal(e);
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     // small ragged batches: block map (+ stream snapshot) in one single-workgroup kernel
     const bool small_map = b->count <= block_map_small_max();
@@ -1117,8 +1118,9 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
     s.abs_off = e->d_fr_off;
     s.abs_slot = per_key ? e->d_fr_slot : nullptr;
     static_assert(sizeof(ScanResult) == sizeof(fpnn_aes_frame_scan), "scan layout");
-    batch_signal(e->device);
+    batch_signal(e);
     HIP_TRY(launch_scan_frames(s, false, e->num_cus, e->stream));
+    batch_queued(e);
     // every frame slot is one package segment (unused ones have length 0)
     fpnn_aes_batch fb;
     memset(&fb, 0, sizeof fb);
@@ -1156,8 +1158,9 @@ int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
     s.frame_off = frame_off;
     s.frame_len = frame_len;
     s.scan = reinterpret_cast<ScanResult *>(scan);
-    batch_signal(e->device);
+    batch_signal(e);
     HIP_TRY(launch_scan_frames(s, true, e->num_cus, e->stream));
+    batch_queued(e);
     return FPNN_AES_OK;
 }
 
@@ -1285,9 +1288,13 @@ uint32_t *yield_words() {
     return y;
 }
 
-// before batch kernels are queued on a device (no-op until a server ever ran)
-void batch_signal(int device) {
-    if (uint32_t *y = g_yield.load(std::memory_order_acquire)) __atomic_fetch_add(y + 16 * (device & 63), 1u, __ATOMIC_RELEASE);
+// before batch kernels are queued on a device (no-op until a server ever ran): servers
+// leave, and no server is relaunched until the work is done (batch_fence)
+void batch_signal(fpnn_aes_engine *e) {
+    if (uint32_t *y = g_yield.load(std::memory_order_acquire)) {
+        e->batch_pending.store(true, std::memory_order_release);
+        __atomic_fetch_add(y + 16 * (e->device & 63), 1u, __ATOMIC_RELEASE);
+    }
 }
 
 // Engines per device, for batch_fence.
@@ -1312,8 +1319,9 @@ void unregister_engine(fpnn_aes_engine *e) {
 // after an engine queued batch kernels (once servers exist): remember where they end
 void batch_queued(fpnn_aes_engine *e) {
     if (!g_yield.load(std::memory_order_acquire)) return;  // no server ever ran: nothing waits
-    if (!e->batch_ev && hipEventCreateWithFlags(&e->batch_ev, hipEventDisableTiming) != hipSuccess) return;
-    if (hipEventRecord(e->batch_ev, e->stream) == hipSuccess) e->batch_ev_live = true;
+    if (e->batch_ev || hipEventCreateWithFlags(&e->batch_ev, hipEventDisableTiming) == hipSuccess)
+        if (hipEventRecord(e->batch_ev, e->stream) == hipSuccess) e->batch_ev_live.store(true, std::memory_order_release);
+    e->batch_pending.store(false, std::memory_order_release);
 }
 
 // Before (re)launching a small-call server: wait until the batch work other engines queued
@@ -1322,14 +1330,32 @@ void batch_queued(fpnn_aes_engine *e) {
 // call waits for that CU) -- servers leave when batch work is queued (batch_signal), and
 // do not come back until it is done.  The per-call request waits for the batch instead,
 // which it would do anyway: the batch grid holds every CU.
+// The wait is bounded (kBatchFenceMs): an engine that queues batch after batch would
+// otherwise starve the per-call path; past the bound the server is launched and waits for
+// a CU like any kernel.
 void batch_fence(fpnn_aes_engine *e) {
+    constexpr int kBatchFenceMs = 5;
     DeviceEngines &d = g_dev_engines[e->device & 63];
     std::lock_guard<std::mutex> lk(d.mu);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto late = [&]() { return std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kBatchFenceMs); };
     for (fpnn_aes_engine *o : d.list) {
-        if (o == e || !o->batch_ev_live) continue;
-        hipError_t q;
-        while ((q = hipEventQuery(o->batch_ev)) == hipErrorNotReady) __builtin_ia32_pause();
-        if (q == hipSuccess) o->batch_ev_live = false;
+        if (o == e) continue;
+        for (uint32_t spins = 0;; spins++) {
+            if (o->batch_pending.load(std::memory_order_acquire)) {  // its kernels are being queued
+                __builtin_ia32_pause();
+            } else if (o->batch_ev_live.load(std::memory_order_acquire)) {
+                const hipError_t q = hipEventQuery(o->batch_ev);
+                if (q != hipErrorNotReady) {
+                    if (q == hipSuccess) o->batch_ev_live.store(false, std::memory_order_release);
+                    break;
+                }
+                __builtin_ia32_pause();
+            } else {
+                break;
+            }
+            if ((spins & 255) == 255 && late()) return;
+        }
     }
 }
 
@@ -2921,7 +2947,7 @@ int ecdh_launch(fpnn_aes_engine *e, int curve, const EccConst &c, const EcdhJob 
         return FPNN_AES_ERR_ARG;
     }
     DeviceGuard g(e->device);
-    batch_signal(e->device);
+    batch_signal(e);
     HIP_TRY(launch_ecdh(c, j, curve, e->stream));
     batch_queued(e);
     return FPNN_AES_OK;
