@@ -1379,8 +1379,9 @@ int launch_server(fpnn_aes_engine *e) {
     if (!yh) return hip_fail(hipErrorOutOfMemory, "hipHostMalloc(yield)");
     uint32_t *yd = nullptr;
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&yd), yh + 16 * (e->device & 63), 0));
+    const uint32_t y0 = __atomic_load_n(yh + 16 * (e->device & 63), __ATOMIC_ACQUIRE);  // after batch_fence
     const uint32_t epoch = ++e->srv_epoch;
-    HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, yd, e->stream));
+    HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, yd, y0, e->stream));
     return FPNN_AES_OK;
 }
 

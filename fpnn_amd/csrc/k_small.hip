@@ -175,18 +175,18 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_single(SmallArgs a) {
 // sequence number in order and stores it into resp.done after the results.
 __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *mb, const uint32_t *t0le,
                                                                  uint32_t epoch, uint64_t idle_ticks,
-                                                                 uint64_t life_ticks, const uint32_t *yield) {
+                                                                 uint64_t life_ticks, const uint32_t *yield,
+                                                                 uint32_t y0) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
     __shared__ SmallShared S;
     __shared__ SmallReq rq;
     __shared__ uint32_t ctl[2][4];  // [iteration parity][action, sequence number, body blocks]
     const uint32_t t = threadIdx.x;
     fill_tables_regs(lds4, t0le[t], 32);
-    uint32_t done = 0, y0 = 0;
+    uint32_t done = 0;
     uint64_t t_start = 0, t_idle = 0;
     if (t == 0) {
         done = load_acquire(&mb->resp.done);
-        y0 = load_acquire(yield);
         t_start = t_idle = wall_clock64();
     }
     __syncthreads();
@@ -277,10 +277,10 @@ hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipS
 }
 
 hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
-                             uint64_t life_ticks, const uint32_t *yield, hipStream_t st) {
+                             uint64_t life_ticks, const uint32_t *yield, uint32_t y0, hipStream_t st) {
     set_launched("cfb_server");
     hipLaunchKernelGGL(k_cfb_server, dim3(1), dim3(kSmallThreads), 0, st, mb, t0le, epoch, idle_ticks, life_ticks,
-                       yield);
+                       yield, y0);
     return hipGetLastError();
 }
 

@@ -235,11 +235,12 @@ struct SmallMailbox {
     SmallResp resp;
     alignas(64) uint8_t io[kSmallBodyAt + kSmallMaxBytes + 64];
 };
-// yield: the device's batch-activity word (pinned host memory): the host bumps it before
-// it queues batch kernels; a server that sees it change leaves after its current request,
-// so no batch workgroup waits for a CU (or a hardware queue) an idle server holds.
+// yield: the device's batch-activity word (pinned host memory), y0 its value when the host
+// launched the server: the host bumps it before it queues batch kernels; a server that sees
+// it differ from y0 leaves after its current request (also one that only started after the
+// bump), so no batch workgroup waits for a CU (or a hardware queue) a server holds.
 hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
-                             uint64_t life_ticks, const uint32_t *yield, hipStream_t st);
+                             uint64_t life_ticks, const uint32_t *yield, uint32_t y0, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
 // Host-mapped frame moves: a job copies n segments, segment i from address sbase + soff[i]
