@@ -1367,6 +1367,11 @@ bool server_enabled() {
     return on;
 }
 
+// Relaunch order: read the device's batch-activity value y0 FIRST, then wait out batch
+// work (batch_fence), then launch the server with y0.  A batch that signals after the read
+// makes the server leave at its first poll; one that signalled before it set its pending
+// flag first (batch_signal), so the fence waits for it.  (Reading y0 after the fence let a
+// batch slip in between: its server then never saw a change and held a CU through it.)
 int launch_server(fpnn_aes_engine *e) {
     if (!e->srv_idle_ticks) {
         int khz = 0;  // device wall clock (wall_clock64), kHz
@@ -1379,7 +1384,8 @@ int launch_server(fpnn_aes_engine *e) {
     if (!yh) return hip_fail(hipErrorOutOfMemory, "hipHostMalloc(yield)");
     uint32_t *yd = nullptr;
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&yd), yh + 16 * (e->device & 63), 0));
-    const uint32_t y0 = __atomic_load_n(yh + 16 * (e->device & 63), __ATOMIC_ACQUIRE);  // after batch_fence
+    const uint32_t y0 = __atomic_load_n(yh + 16 * (e->device & 63), __ATOMIC_ACQUIRE);
+    batch_fence(e);
     const uint32_t epoch = ++e->srv_epoch;
     HIP_TRY(launch_cfb_server(e->d_mb, t0le_of(e), epoch, e->srv_idle_ticks, e->srv_life_ticks, yd, y0, e->stream));
     return FPNN_AES_OK;
@@ -1409,7 +1415,6 @@ int cfb_small_server(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encr
     e->last_kernel[which] = "cfb_server";
     // a server is alive unless none was launched or the last one has stored its epoch
     if (e->srv_epoch == 0 || __atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch) {
-        batch_fence(e);
         if (int rc = launch_server(e)) return rc;
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -1417,7 +1422,6 @@ int cfb_small_server(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, bool encr
         __builtin_ia32_pause();
         if (__atomic_load_n(&mb->resp.exited, __ATOMIC_ACQUIRE) == e->srv_epoch &&
             __atomic_load_n(&mb->resp.done, __ATOMIC_ACQUIRE) != seq) {
-            batch_fence(e);
             if (int rc = launch_server(e)) return rc;  // it left before seeing this request
             continue;
         }
