@@ -102,10 +102,14 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 #pragma unroll
             for (int j = 0; j < C; j++) a[j] = load16(p + 16 * j);
             for (; i + C <= nfull; i += C) {
+                // the next chunk's loads, unconditional (the last chunk re-reads itself): a
+                // load under a branch leaves the waitcnt pass unsure how many are in
+                // flight, and it then drains all of them (vmcnt(0)) inside the next chunk
                 const bool more = i + 2 * C <= nfull;
+                const uint8_t *pn = more ? p + 16 * C : p;
                 uint4 nx[C];
 #pragma unroll
-                for (int j = 0; j < C; j++) nx[j] = more ? load16(p + 16 * (C + j)) : make_uint4(0, 0, 0, 0);
+                for (int j = 0; j < C; j++) nx[j] = load16(pn + 16 * j);
 #pragma unroll
                 for (int j = 0; j < C; j++) {
                     uint4 ks;
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 // lane instead of 60.  Used when chains are few (streams) or long/ragged.
 
 template <int NR, int LAYOUT, int KM, bool STREAM, int NT>
-__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
+__global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cfb_encrypt_coop(KBatch b) {
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -214,10 +218,15 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
             const uint32_t rkx = rkq[NR] ^ rkq[0];
             uint32_t sw = iv ^ rkq[0];
             for (; i + CH <= nfull; i += CH) {
+                // the next step's words, unconditional (the last step re-reads itself): loads
+                // under a branch made the waitcnt pass drain them all (vmcnt(0)) at the end of
+                // the step's first block -- one memory latency per 8-block step (C5: K2c's
+                // SQ_WAIT_ANY 0.40 against SQ_WAIT_INST_LDS 0.09)
                 const bool more = i + 2 * CH <= nfull;
+                const uint8_t *pn = (more ? p + 16 * CH : p) + wlo;
                 uint32_t nx[CH], c[CH];
 #pragma unroll
-                for (int j = 0; j < CH; j++) nx[j] = more ? *reinterpret_cast<const uint32_u *>(p + 16 * (CH + j) + wlo) : 0u;
+                for (int j = 0; j < CH; j++) nx[j] = *reinterpret_cast<const uint32_u *>(pn + 16 * j);
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
                     sw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
@@ -226,8 +235,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_coop(KBatch b) {
                 iv = c[CH - 1];
 #pragma unroll
                 for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
+                // the loaded words are handed on here, after the rounds: without this the
+                // register allocator moved each nx[j] into a round's registers as soon as it
+                // could, waiting (vmcnt) for loads issued one block earlier
 #pragma unroll
-                for (int j = 0; j < CH; j++) a[j] = nx[j];
+                for (int j = 0; j < CH; j++) {
+                    asm volatile("" : "+v"(nx[j]));
+                    a[j] = nx[j];
+                }
                 p += 16 * CH;
                 o += 16 * CH;
             }
