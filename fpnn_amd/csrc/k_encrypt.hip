@@ -233,6 +233,11 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                     c[j] = sw ^ rkq[0];
                 }
                 iv = c[CH - 1];
+                // the step's 8 words go out together, each quad's 128-B line in 8 back-to-back
+                // stores: stored one per block, a line sat partly written in L2 for a whole
+                // step and C5 wrote 1.42x its output bytes to HBM (profiles/r05/C5)
+#pragma unroll
+                for (int j = 0; j < CH; j++) asm volatile("" : "+v"(c[j]));
 #pragma unroll
                 for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
                 // the loaded words are handed on here, after the rounds: without this the

@@ -346,6 +346,38 @@ def gen_multi_cases():
                       "many connections (oracle/_ref/io_multi_ref, oracle/io_multi.cpp)", "cases": cases}
 
 
+UDP_REF = os.path.join(HERE, "_ref", "udp_v2_ref")
+# (curve, reinforce package, reinforce data, datagrams per session, seed): every curve, both
+# key lengths on each channel
+UDP_CASES = [("secp256k1", 0, 0, 300, 7001), ("secp256r1", 1, 1, 300, 7002), ("secp224r1", 0, 1, 200, 7003),
+             ("secp192r1", 1, 0, 200, 7004)]
+
+
+def gen_udp_cases():
+    """The reference's UDPEncryptor (core/UDP.v2/UDPCommon.v2.cpp, oracle/udp_v2.cpp) on the
+    reference cipher and key exchange (`make -C oracle udp`): per case the server's
+    createPair sessions with two clients from ecdh_cases.json, datagrams both ways, and the
+    ciphertext digests per channel and direction."""
+    import subprocess
+    with open(os.path.join(GOLDEN, "ecdh_cases.json")) as f:
+        curves = {c["curve"]: c for c in json.load(f)["curves"]}
+    cases = []
+    for curve, rp, rd, n, seed in UDP_CASES:
+        c = curves[curve]
+        cl = [x for x in c["clients"] if x["ok"]][:2]
+        line = " ".join([curve, c["server_private"], c["server_public"], cl[0]["private"], cl[0]["public"],
+                         cl[1]["private"], cl[1]["public"], str(rp), str(rd), str(n), str(seed)])
+        out = subprocess.run([UDP_REF], input=line + "\n", capture_output=True, text=True, check=True,
+                             timeout=600).stdout
+        d = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+        assert d["init_ok"] and d["pair_a"] and d["pair_b"] and d["client_ok"] and d["roundtrip_ok"], d
+        secs = d.pop("seconds")
+        cases.append({"input": line, "expect": d})
+        print("  udp", curve, d, "reference seconds here:", secs)
+    return {"source": "core/UDP.v2/UDPCommon.v2.cpp + core/KeyExchange.cpp + micro-ecc + core/Encryptor.cpp + "
+                      "base/rijndael.c (oracle/_ref/udp_v2_ref, oracle/udp_v2.cpp)", "cases": cases}
+
+
 ECDH_REF = os.path.join(HERE, "_ref", "ecdh_ref")
 
 
@@ -551,6 +583,7 @@ def main():
     ap.add_argument("--ecdh-only", action="store_true", help="only (re)write ecdh_cases.json")
     ap.add_argument("--c1-only", action="store_true", help="only (re)write c1_cases.json")
     ap.add_argument("--multi-only", action="store_true", help="only (re)write multi_cases.json")
+    ap.add_argument("--udp-only", action="store_true", help="only (re)write udp_cases.json")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 4)
     args = ap.parse_args()
     ref = Oracle("reference")
@@ -576,6 +609,9 @@ def main():
     if args.multi_only:
         dump("multi_cases.json", gen_multi_cases())
         return
+    if args.udp_only:
+        dump("udp_cases.json", gen_udp_cases())
+        return
     if args.shards_only:
         with open(os.path.join(GOLDEN, "digests.json")) as f:
             d = json.load(f)
@@ -591,6 +627,7 @@ def main():
     dump("ecdh_cases.json", gen_ecdh_cases())
     dump("c1_cases.json", gen_c1_cases())
     dump("multi_cases.json", gen_multi_cases())
+    dump("udp_cases.json", gen_udp_cases())
     if not args.skip_large:
         d = {"generator": "oracle/gen_golden.py with oracle/_ref (reference base/rijndael.c + core/Encryptor.cpp)",
              "configs": configs.describe()}

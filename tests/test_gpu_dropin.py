@@ -114,6 +114,31 @@ def test_percall_dropin_in_reference_io_plumbing():
         assert d[k] == ref[k], (k, d[k], ref[k])
 
 
+def _udp():
+    with open(os.path.join(ROOT, "tests", "golden", "udp_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _udp(), ids=lambda c: c["input"].split()[0])
+def test_reference_udp_encryptor_on_dropin(case):
+    """SURVEY 8f rows 2 + 4 with the reference's own UDP caller:
+    core/UDP.v2/UDPCommon.v2.cpp compiled unchanged against include/Encryptor.h +
+    include/KeyExchange.h (oracle/_ref/udp_v2_dropin).  The server's
+    UDPEncryptor::createPair (both forms: package only, package + reinforced data) runs the
+    ECDH on the GPU; clients configure theirs from ECCKeyExchange::calcKey; datagrams go
+    both ways through packageEncrypt/packageDecrypt and data segments through
+    dataEncrypt/dataDecrypt.  Every ciphertext digest equals the reference build's
+    (tests/golden/udp_cases.json, oracle/_ref/udp_v2_ref), every decrypt returns its
+    plaintext, and a malformed public key gets an empty pair on both."""
+    out = subprocess.run([_exe("udp_v2_dropin")], input=case["input"] + "\n", capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, (out.returncode, out.stderr[-3000:])
+    d = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    print(json.dumps(d))
+    d.pop("seconds")
+    assert d == case["expect"]
+
+
 def test_c1_percall_unchanged_package_encryptor(tmp_path):
     """C1's per-call shape: 10 000 x 1 KiB AES-256 frames through the unchanged
     PackageEncryptor::encrypt / decrypt / encrypt(std::string*) one call at a time
