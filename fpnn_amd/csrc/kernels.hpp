@@ -66,6 +66,7 @@ struct Variant {
     int hyb_quad_waves = 12;
     int hyb_wire_lanes = 0;  // wire-prefix batches also use the lane session (else all quads)
     int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
+    int64_t coop_below = -1;  // uniform batches of fewer chains take K2c (-1: a full chip's lanes)
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;
