@@ -12,6 +12,7 @@
 #   probe:<lib>:<expr>  the same against another build of the GPU library (fpnn_amd/<lib>, loaded
 #                    through FPNN_AES_GPU_LIB), e.g. a tools/probe/*.patch build
 #   bench            python bench.py (the contract line)
+#   bench_driver     bench.py three times with the driver's arguments (--steps 20 --warmup 5)
 #   bench_trace      bench.py under rocprofv3 --kernel-trace --stats (profiles the line's kernels)
 #   bench_pmc        bench.py under the four PMC passes (HBM bytes, LDS, VALU, waits)
 #   configs          tools/bench_configs.py --no-host, every device config (steady-state medians)
@@ -75,6 +76,9 @@ for step in "$@"; do
       FPNN_AES_GPU_LIB=$PWD/fpnn_amd/$lib run "probe_${lib%.so}" 600 python -u -m pytest tests -q -m gpu \
         --timeout 300 --timeout-method thread -k "${spec#*:}" ;;
     bench) run bench 300 python -u bench.py ;;
+    bench_driver) for i in 1 2 3; do  # the driver's own arguments (BENCH_rNN.json: --steps 20 --warmup 5)
+        run "bench_driver_$i" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
     bench_trace) mkdir -p "$OUT/bench_trace"  # (bench_pmc's own trace pass goes to bench_prof/trace)
       run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_trace" -o run -- \
         python3 bench.py --no-cpu-baseline ;;
