@@ -102,11 +102,13 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 #pragma unroll
             for (int j = 0; j < C; j++) a[j] = load16(p + 16 * j);
             for (; i + C <= nfull; i += C) {
-                // the next chunk's loads, unconditional (the last chunk re-reads itself): a
-                // load under a branch leaves the waitcnt pass unsure how many are in
-                // flight, and it then drains all of them (vmcnt(0)) inside the next chunk
+                // the next chunk's loads, unconditional (the last chunk reads the first
+                // DevKey's 128+ bytes, an L2 hit, not its own chunk again: that cost C2 an
+                // eighth of its reads in HBM traffic): a load under a branch leaves the
+                // waitcnt pass unsure how many are in flight, and it then drains all of them
+                // (vmcnt(0)) inside the next chunk
                 const bool more = i + 2 * C <= nfull;
-                const uint8_t *pn = more ? p + 16 * C : p;
+                const uint8_t *pn = more ? p + 16 * C : reinterpret_cast<const uint8_t *>(b.keys);
                 uint4 nx[C];
 #pragma unroll
                 for (int j = 0; j < C; j++) nx[j] = load16(pn + 16 * j);
@@ -218,12 +220,13 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint32_t rkx = rkq[NR] ^ rkq[0];
             uint32_t sw = iv ^ rkq[0];
             for (; i + CH <= nfull; i += CH) {
-                // the next step's words, unconditional (the last step re-reads itself): loads
-                // under a branch made the waitcnt pass drain them all (vmcnt(0)) at the end of
-                // the step's first block -- one memory latency per 8-block step (C5: K2c's
-                // SQ_WAIT_ANY 0.40 against SQ_WAIT_INST_LDS 0.09)
+                // the next step's words, unconditional (the last step reads the first
+                // DevKey, an L2 hit): loads under a branch made the waitcnt pass drain them
+                // all (vmcnt(0)) at the end of the step's first block -- one memory latency
+                // per 8-block step (C5: K2c's SQ_WAIT_ANY 0.40 against SQ_WAIT_INST_LDS 0.09,
+                // VERDICT r04 item 5)
                 const bool more = i + 2 * CH <= nfull;
-                const uint8_t *pn = (more ? p + 16 * CH : p) + wlo;
+                const uint8_t *pn = (more ? p + 16 * CH : reinterpret_cast<const uint8_t *>(b.keys)) + wlo;
                 uint32_t nx[CH], c[CH];
 #pragma unroll
                 for (int j = 0; j < CH; j++) nx[j] = *reinterpret_cast<const uint32_u *>(pn + 16 * j);
