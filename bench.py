@@ -40,8 +40,8 @@ METRIC = "AES-256 GiB/s on device-resident packet batch; 1/2/4/8-GPU scaling"  #
 # newest committed PMC summary of the bench command (tools/pmc_summary.py output), per workload
 # (C2: this bench command under the PMC passes, `tools/gpu.sh <tag> bench_pmc`; C4 / C5:
 # `tools/gpu.sh <tag> prof:C4` -- the same kernels on the same batches through tools/bench_configs.py)
-PMC_SUMMARIES = {"C2": "profiles/r04/bench/pmc_summary.json", "C4": "profiles/r04/C4/pmc_summary.json",
-                 "C5": "profiles/r04/C5/pmc_summary.json"}
+PMC_SUMMARIES = {"C2": "profiles/r05/bench/pmc_summary.json", "C4": "profiles/r04/C4/pmc_summary.json",
+                 "C5": "profiles/r05/C5/pmc_summary.json"}
 
 
 def parse():
