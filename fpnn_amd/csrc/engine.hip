@@ -296,6 +296,7 @@ struct fpnn_aes_keyset {
     fpnn_aes_engine *e = nullptr;  // creating engine (may be destroyed before the key set)
     int device = 0;
     DevKey *d_keys = nullptr;
+    uint4 *d_eiv = nullptr;  // E_k(IV) per slot (launch_slot_eiv after every write), or null
     uint32_t count = 0;
     int nrounds = 0;
     uint32_t keylen = 0;
@@ -435,6 +436,7 @@ KBatch make_kbatch(const fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
     k.iv_state = iv_state;
     k.pos_state = pos_state;
     k.t0le = t0le_of(e);
+    k.eiv = e->variant.eiv ? b->keys->d_eiv : nullptr;
     return k;
 }
 
@@ -702,6 +704,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_COOP_BELOW")) e->variant.coop_below = atoll(v);
+    if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed
@@ -920,6 +923,9 @@ int fpnn_aes_keyset_create(fpnn_aes_engine *e, uint32_t count, size_t keylen, co
             iv_dev = ivs ? d_raw + kb : nullptr;
         }
         err = launch_expand_keys(k_dev, (uint32_t)keylen, iv_dev, count, sbox_of(e), ks->d_keys, e->stream);
+        if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void **>(&ks->d_eiv), sizeof(uint4) * (size_t)count);
+        if (err == hipSuccess)
+            err = launch_slot_eiv(ks->d_keys, 0, count, ks->nrounds, t0le_of(e), ks->d_eiv, e->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
         if (err != hipSuccess) { rc = hip_fail(err, "expand_keys"); break; }
     } while (0);
@@ -957,6 +963,9 @@ int fpnn_aes_keyset_from_schedules(fpnn_aes_engine *e, uint32_t count, const fpn
     ks->keylen = (uint32_t)(nr - 6) * 4;
     hipError_t err = hipMalloc(reinterpret_cast<void **>(&ks->d_keys), sizeof(DevKey) * (size_t)count);
     if (err == hipSuccess) err = hipMemcpy(ks->d_keys, host.data(), sizeof(DevKey) * (size_t)count, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void **>(&ks->d_eiv), sizeof(uint4) * (size_t)count);
+    if (err == hipSuccess) err = launch_slot_eiv(ks->d_keys, 0, count, nr, t0le_of(e), ks->d_eiv, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) {
         int rc = hip_fail(err, "upload(schedules)");
         fpnn_aes_keyset_destroy(ks);
@@ -975,6 +984,7 @@ int fpnn_aes_keyset_destroy(fpnn_aes_keyset *ks) {
     }
     if (ks->h_up) (void)hipHostFree(ks->h_up);
     if (ks->d_keys) (void)hipFree(ks->d_keys);  // hipFree waits for outstanding work on the device
+    if (ks->d_eiv) (void)hipFree(ks->d_eiv);
     delete ks;
     return FPNN_AES_OK;
 }
@@ -993,6 +1003,9 @@ int fpnn_aes_keyset_reserve(fpnn_aes_engine *e, uint32_t capacity, int nrounds, 
     ks->capacity = capacity;
     hipError_t err = hipMalloc(reinterpret_cast<void **>(&ks->d_keys), sizeof(DevKey) * (size_t)capacity);
     if (err == hipSuccess) err = hipMemsetAsync(ks->d_keys, 0, sizeof(DevKey) * (size_t)capacity, e->stream);
+    if (err == hipSuccess) err = hipMalloc(reinterpret_cast<void **>(&ks->d_eiv), sizeof(uint4) * (size_t)capacity);
+    if (err == hipSuccess)  // (unset slots too: a batch naming one sees what the rounds would give)
+        err = launch_slot_eiv(ks->d_keys, 0, capacity, nrounds, t0le_of(e), ks->d_eiv, e->stream);
     if (err == hipSuccess) err = hipEventCreateWithFlags(&ks->up_done, hipEventDisableTiming);
     if (err != hipSuccess) {
         const int rc = hip_fail(err, "keyset_reserve");
@@ -1021,9 +1034,16 @@ int fpnn_aes_keyset_set(fpnn_aes_keyset *ks, uint32_t first, uint32_t count, con
         HIP_TRY(hipMemsetAsync(nk + ks->capacity, 0, sizeof(DevKey) * (size_t)(cap - ks->capacity), e->stream));
         HIP_TRY(hipMemcpyAsync(nk, ks->d_keys, sizeof(DevKey) * (size_t)ks->capacity, hipMemcpyDeviceToDevice,
                                e->stream));
+        uint4 *ne = nullptr;
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ne), sizeof(uint4) * (size_t)cap));
+        HIP_TRY(hipMemcpyAsync(ne, ks->d_eiv, sizeof(uint4) * (size_t)ks->capacity, hipMemcpyDeviceToDevice,
+                               e->stream));
+        HIP_TRY(launch_slot_eiv(nk, ks->capacity, cap - ks->capacity, ks->nrounds, t0le_of(e), ne, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));  // the old table may still be read by queued kernels
         (void)hipFree(ks->d_keys);
+        (void)hipFree(ks->d_eiv);
         ks->d_keys = nk;
+        ks->d_eiv = ne;
         ks->capacity = cap;
     }
     if (ks->up_pending) {  // the staging still feeds the previous upload
@@ -1049,6 +1069,7 @@ int fpnn_aes_keyset_set(fpnn_aes_keyset *ks, uint32_t first, uint32_t count, con
     HIP_TRY(hipMemcpyAsync(ks->d_keys + first, ks->h_up, sizeof(DevKey) * (size_t)count, hipMemcpyHostToDevice,
                            e->stream));
     HIP_TRY(hipEventRecord(ks->up_done, e->stream));
+    HIP_TRY(launch_slot_eiv(ks->d_keys, first, count, ks->nrounds, t0le_of(e), ks->d_eiv, e->stream));
     ks->up_pending = true;
     ks->count = std::max(ks->count, need);
     return FPNN_AES_OK;

@@ -22,13 +22,15 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
     RoundKeys<NR> rku;
     if (KM == KEY_UNIFORM) rku = load_round_keys<NR>(b.keys);
-    // Package mode, one key, uniform lengths (C2): every chain starts from the same IV, so
-    // its first keystream block E_k(IV) is one constant (point 3); and
-    // every lane starts its chains at the same step, so the wave skips those 14 rounds
-    // together.  Computed once per lane here.
-    constexpr bool kConstFirst = LAYOUT == LAYOUT_UNIFORM && KM == KEY_UNIFORM && !STREAM;
-    uint4 eiv = make_uint4(0, 0, 0, 0);
-    if (kConstFirst) eiv = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
+    // Package mode: every chain of a key slot starts from the slot's IV, so its first
+    // keystream block E_k(IV) is a per-slot constant (point 3) -- with one
+    // key computed once per lane here, with per-lane keys read from the key set's table
+    // (b.eiv).  Where a wave's lanes start their chains at the same step (uniform lengths:
+    // C2, U1) the wave skips block 0's rounds together.
+    constexpr bool kFirst = !STREAM;
+    const bool use_eiv = kFirst && (KM == KEY_UNIFORM || b.eiv != nullptr);
+    uint4 eiv_u = make_uint4(0, 0, 0, 0);
+    if (kFirst && KM == KEY_UNIFORM) eiv_u = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
 
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
@@ -39,6 +41,8 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             rk = rku;
         else
             rk = load_round_keys<NR>(key);
+        uint4 eiv = eiv_u;
+        if (kFirst && KM != KEY_UNIFORM && use_eiv) eiv = b.eiv[g.slot];
 
         uint4 iv;
         uint32_t n = 0;
@@ -85,7 +89,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             uint32_t h = (mis & 15u) ? 0u : ((128u - mis) & 127u) >> 4;
             h = h < nfull ? h : nfull;
             for (; i < h; i++) {
-                iv = (kConstFirst && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ load16(p);
+                iv = (use_eiv && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ load16(p);
                 store16(q, iv);
                 p += 16;
                 q += 16;
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 #pragma unroll
                 for (int j = 0; j < C; j++) {
                     uint4 ks;
-                    if (kConstFirst && j == 0 && i == 0)  // the chain's first block (wave-uniform)
+                    if (use_eiv && j == 0 && i == 0)  // the chain's first block (wave-uniform)
                         ks = eiv;
                     else
                         ks = FENCE ? aes_encrypt_block_fenced<NR, NT>(iv, rk, T) : aes_encrypt_block<NR, NT>(iv, rk, T);
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
         for (; i < nfull; i++) {
             const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
-            iv = (kConstFirst && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ pt;  // C_i = P_i ^ E(C_{i-1})
+            iv = (use_eiv && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ pt;  // C_i = P_i ^ E(C_{i-1})
             store16(q, iv);
             pt = pn;
             p += 16;
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         }
         rem &= 15u;
         if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
-            const uint4 ks = kConstFirst && nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T);
+            const uint4 ks = use_eiv && nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T);
             const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
             store_bytes(q, o, 0, (int)rem);
             iv = select_bytes(byte_mask(0, (int)rem), o, ks);
@@ -182,11 +186,16 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 
         uint32_t iv;  // this lane's word of the 16-byte feedback register
         uint32_t n = 0;
+        // package mode: block 0's keystream E_k(IV) from the key set's table (the quads of a
+        // wave start their chains together on C5-like batches: the wave skips those rounds)
+        const bool use_eiv = !STREAM && b.eiv != nullptr;
+        uint32_t ew = 0;  // this lane's word of E_k(IV)
         if (STREAM) {
             iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
             n = b.pos_state[s];
         } else {
             iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
+            if (use_eiv) ew = reinterpret_cast<const uint32_t *>(b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot))[q];
         }
         const uint8_t *p = g.in;
         uint8_t *o = g.out;
@@ -232,7 +241,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 for (int j = 0; j < CH; j++) nx[j] = *reinterpret_cast<const uint32_u *>(pn + 16 * j);
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
-                    sw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
+                    if (j == 0 && use_eiv && i == 0)  // the chain's first block (quad-uniform)
+                        sw = ew ^ a[j] ^ rkq[0];
+                    else
+                        sw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
                     c[j] = sw ^ rkq[0];
                 }
                 iv = c[CH - 1];
@@ -257,14 +269,14 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         }
         for (; i < nfull; i++) {
             const uint32_t pt = *reinterpret_cast<const uint32_u *>(p + wlo);
-            iv = aes_encrypt_column<NR, NT>(iv, rkq, T) ^ pt;
+            iv = (use_eiv && i == 0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T)) ^ pt;
             *reinterpret_cast<uint32_u *>(o + wlo) = iv;
             p += 16;
             o += 16;
         }
         rem &= 15u;
         if (rem) {  // partial final block
-            const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+            const uint32_t ks = use_eiv && nfull == 0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T);
             const int lo = 0, hi = min((int)rem, wlo + 4) - wlo;
             if (hi > lo) {
                 const uint32_t c = load_word_bytes(p + wlo, lo, hi) ^ ks;

@@ -122,6 +122,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 #pragma unroll
         for (int j = 0; j < 8; j++) held[j] = 0u;
         bool active = false, exhausted = false, fresh = false;
+        // package mode: at0 = no block of the chain ciphered yet; ew = this lane's word of the
+        // slot's E_k(IV) (kernels.hpp KBatch::eiv), block 0's keystream
+        bool at0 = false;
+        uint32_t ew = 0;
         uint32_t a[8], nx[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) a[j] = nx[j] = 0u;
@@ -143,6 +147,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             } else {
                 v = reinterpret_cast<const uint32_t *>(key->iv)[q];
                 pos = 0;
+                at0 = true;
+                if (b.eiv) ew = reinterpret_cast<const uint32_t *>(b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot))[q];
             }
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 if (k && lo < 4) store_word_bytes(o - 16 + wlo, praw, lo > 0 ? lo : 0, 4);
             }
             if (tail) {
-                const uint32_t ks = aes_encrypt_column<NR, NT>(iv, rkq, T);
+                const uint32_t ks = !STREAM && b.eiv && at0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T);
                 const int hi = min((int)tail, wlo + 4) - wlo;
                 if (hi > 0) {
                     const uint32_t c = load_word_bytes(p + wlo, 0, hi) ^ ks;
@@ -290,6 +296,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             // grid somewhere in the batch), else block words are output words
             uint8_t *const dst = o - d + wlo;
             const bool head = SHIFT && lo0 != 0 && kk != 0;  // the chain's first slot: from byte lo0 on
+            // every quad that ciphers a block this step is at its chain's block 0: the wave
+            // takes that block's keystream from the key set (a quad at block 0 would compute
+            // the same value: sw = IV ^ rk[0])
+            const bool all0 = !STREAM && b.eiv && __builtin_amdgcn_ballot_w64(kk != 0 && !at0) == 0;
             auto body = [&](auto fun_c) {
                 constexpr bool FUN = decltype(fun_c)::value;
                 // the chain carries C ^ rk[0] (aes_chain_column: its XORs folded into the keys)
@@ -297,7 +307,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 uint32_t sw = iv ^ rkq[0];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    const uint32_t nsw = aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
+                    const uint32_t nsw =
+                        j == 0 && all0 ? ew ^ a[j] ^ rkq[0] : aes_chain_column<NR, NT>(sw, rkq, rkx ^ a[j], T);
                     const uint32_t c = nsw ^ rkq[0];  // C_i = P_i ^ E(C_{i-1})
                     const bool use = j < (int)kk;
                     sw = use ? nsw : sw;
@@ -348,6 +359,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 lo0 = 0;
                 pv = 16;
             }
+            if (kk) at0 = false;
             p += 16 * kk;
             o += 16 * kk;
             nfull -= kk;
@@ -371,6 +383,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         uint32_t nfull = 0, tail = 0, n = 0, d = 0, pv = 0, lo0 = 0;
         uint4 iv = make_uint4(0, 0, 0, 0), prev = make_uint4(0, 0, 0, 0);
         bool valid = false, exhausted = false, fresh = false;
+        bool at0 = false;                     // package mode: no block of the chain ciphered yet
+        uint4 eivl = make_uint4(0, 0, 0, 0);  // the slot's E_k(IV) (KBatch::eiv)
         uint4 a[CH], nx[CH];
 #pragma unroll
         for (int j = 0; j < CH; j++) a[j] = nx[j] = make_uint4(0, 0, 0, 0);
@@ -392,6 +406,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             } else {
                 iv = *reinterpret_cast<const uint4 *>(key->iv);
                 n = 0;
+                at0 = true;
+                if (b.eiv) eivl = b.eiv[KM == KEY_UNIFORM ? 0u : g.slot];
             }
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
@@ -431,7 +447,13 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const bool fin = valid && nfull == 0;
             if (__builtin_amdgcn_ballot_w64(fin)) {
                 uint4 ks = make_uint4(0, 0, 0, 0);
-                if (__builtin_amdgcn_ballot_w64(fin && tail != 0)) ks = enc(iv);
+                if (__builtin_amdgcn_ballot_w64(fin && tail != 0)) {
+                    // chains of one partial block all at block 0: E_k(IV) from the key set
+                    if (!STREAM && b.eiv && __builtin_amdgcn_ballot_w64(fin && tail != 0 && !at0) == 0)
+                        ks = eivl;
+                    else
+                        ks = enc(iv);
+                }
                 if (fin) {
                     const uint32_t k = d < pv ? d : pv;
                     if (SHIFT && k) store_bytes(o - 16, prev, (int)(16 - k), 16);
@@ -482,10 +504,14 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 for (int j = 0; j < CH; j++)
                     if (j < (int)kk2) nx[j] = load16(p + 16 * (kk + j));
             }
+            // every lane that ciphers a block this step is at its chain's block 0: the wave
+            // takes that block's keystream from the key set (a lane at block 0 would compute
+            // the same E_k(IV))
+            const bool all0 = !STREAM && b.eiv && __builtin_amdgcn_ballot_w64(kk != 0 && !at0) == 0;
             if (!SHIFT) {
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
-                    const uint4 c = enc(iv) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                    const uint4 c = (j == 0 && all0 ? eivl : enc(iv)) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
                     iv = sel4(j < (int)kk, c, iv);
                     a[j] = c;
                 }
@@ -501,7 +527,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 const uint32_t r = t & 3u;
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
-                    const uint4 c = enc(iv) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                    const uint4 c = (j == 0 && all0 ? eivl : enc(iv)) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
                     iv = sel4(j < (int)kk, c, iv);
                     a[j] = sel4(d != 0, funnel_slot(prev, c, c1, c2, r), c);
                     prev = sel4(j < (int)kk, c, prev);
@@ -519,6 +545,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                     pv = 16;
                 }
             }
+            if (kk) at0 = false;
             p += 16 * kk;
             o += 16 * kk;
             nfull -= kk;

@@ -257,7 +257,38 @@ __global__ __launch_bounds__(kSmallThreads, 1) void k_cfb_server(SmallMailbox *m
     if (t == 0) store_release(&mb->resp.exited, epoch);
 }
 
+// E_k(IV) of key slots: the keystream block every package-mode chain of a slot starts
+// with (the IV is the same for every frame, core/Encryptor.cpp:12-19; SURVEY section 0,
+// point 3).  The batch encrypt kernels use it for block 0 and skip its rounds where a whole
+// wave starts its chains together.  One thread per slot, after every key-set write.
+template <int NR>
+__global__ __launch_bounds__(kSmallThreads, 1) void k_slot_eiv(const DevKey *keys, uint32_t first, uint32_t count,
+                                                               const uint32_t *t0le, uint4 *eiv) {
+    __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    fill_tables_regs(lds4, t0le[threadIdx.x], 32);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kSmallThreads + threadIdx.x;
+    if (i >= count) return;
+    const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+    const DevKey *k = keys + first + i;
+    const RoundKeys<NR> rk = load_round_keys<NR>(k);
+    eiv[first + i] = aes_encrypt_block<NR, 4>(*reinterpret_cast<const uint4 *>(k->iv), rk, T);
+}
+
 }  // namespace
+
+hipError_t launch_slot_eiv(const DevKey *keys, uint32_t first, uint32_t count, int nrounds, const uint32_t *t0le,
+                           uint4 *eiv, hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    const dim3 grid((count + kSmallThreads - 1) / kSmallThreads);
+    switch (nrounds) {
+        case 10: hipLaunchKernelGGL(k_slot_eiv<10>, grid, dim3(kSmallThreads), 0, st, keys, first, count, t0le, eiv); break;
+        case 12: hipLaunchKernelGGL(k_slot_eiv<12>, grid, dim3(kSmallThreads), 0, st, keys, first, count, t0le, eiv); break;
+        case 14: hipLaunchKernelGGL(k_slot_eiv<14>, grid, dim3(kSmallThreads), 0, st, keys, first, count, t0le, eiv); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_cfb_single(const SmallArgs &a, int nrounds, bool encrypt, hipStream_t st) {
     set_launched(encrypt ? "cfb_single_encrypt" : "cfb_single_decrypt");

@@ -42,6 +42,9 @@ struct KBatch {
     const uint32_t *pos_snap;
     // encrypt of ragged batches: segment visiting order (longest first), or null
     const uint32_t *perm;
+    // package mode: E_k(IV) per key slot (the first keystream block of every chain of the
+    // slot, fpnn_aes_keyset.d_eiv), or null (then computed)
+    const uint4 *eiv;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with
@@ -67,6 +70,7 @@ struct Variant {
     int hyb_wire_lanes = 0;  // wire-prefix batches also use the lane session (else all quads)
     int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
     int64_t coop_below = -1;  // uniform batches of fewer chains take K2c (-1: a full chip's lanes)
+    int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;
@@ -242,6 +246,9 @@ struct SmallMailbox {
 // bump), so no batch workgroup waits for a CU (or a hardware queue) a server holds.
 hipError_t launch_cfb_server(SmallMailbox *mb, const uint32_t *t0le, uint32_t epoch, uint64_t idle_ticks,
                              uint64_t life_ticks, const uint32_t *yield, uint32_t y0, hipStream_t st);
+// E_k(IV) of key slots [first, first + count) into eiv[first ...] (k_small.hip)
+hipError_t launch_slot_eiv(const DevKey *keys, uint32_t first, uint32_t count, int nrounds, const uint32_t *t0le,
+                           uint4 *eiv, hipStream_t st);
 hipError_t launch_expand_keys(const uint8_t *keys, uint32_t keylen, const uint8_t *ivs, uint32_t count,
                               const uint8_t *sbox, DevKey *out, hipStream_t st);
 // Host-mapped frame moves: a job copies n segments, segment i from address sbase + soff[i]

@@ -305,6 +305,31 @@ def main():
         del a, b, r
         print(json.dumps({"U1": out["U1"]}), flush=True)
 
+    if "Q1" in todo:
+        # FPNN's typical quest frames (145 B: core/test/tcp-test/asyncStressClient.cpp:13-29)
+        # from 16 384 connections, each with its own key and IV, as one collector flush would
+        # pass them (ragged layout, slot per frame): 9 whole blocks and a 1-byte tail per
+        # chain, so block 0 is a tenth of each chain (SURVEY section 0 point 3: E_k(IV))
+        P, L, NC = 2 << 20, 145, 16384
+        keys, ivs = W.many_keys(dict(W.U1, connections=NC, keylen=32))
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), 32, ivs.tobytes())
+        offs = torch.arange(P, dtype=torch.int64, device="cuda") * L
+        lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
+        slots = (torch.arange(P, dtype=torch.int32, device="cuda") % NC).contiguous()
+        a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
+        eng.fill_synthetic(a, 11)
+        b, r = torch.empty_like(a), torch.empty_like(a)
+        kw = dict(in_off=offs, lens=lens, key_slot=slots)
+        we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, **kw), args.reps)
+        wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
+        assert torch.equal(r, a)
+        out["Q1"] = {"frames": P, "frame_bytes": L, "encrypt_kernel_GiBs": gib(P * L, ke),
+                     "decrypt_kernel_GiBs": gib(P * L, kd), "encrypt_wall_GiBs": gib(P * L, we),
+                     "decrypt_wall_GiBs": gib(P * L, wd), "frames_per_s_encrypt_wall": round(P / we),
+                     "cipher_sha256_16": __import__("hashlib").sha256(b.cpu().numpy()).hexdigest()[:16]}
+        del a, b, r
+        print(json.dumps({"Q1": out["Q1"]}), flush=True)
+
     if "C4" in todo:
         c = W.C4
         sizes = W.zipf_sizes(c)
