@@ -416,6 +416,23 @@ class KeySet:
         self.engine = engine
 
     @classmethod
+    def reserve(cls, engine: Engine, capacity: int, keylen: int) -> "KeySet":
+        """An updatable table (fpnn_aes_keyset_reserve): slots are written with set()."""
+        h = C.c_void_p()
+        check(lib.fpnn_aes_keyset_reserve(engine.handle, capacity, keylen // 4 + 6, C.byref(h)), "keyset_reserve")
+        return cls.adopt(engine, h, 0, keylen)
+
+    def set(self, first: int, keys, ivs=None):
+        """fpnn_aes_keyset_set: slots [first, first + len(keys)) get these keys (host key
+        expansion, as EncryptorBatch does) and IVs; queued on the creating engine's stream."""
+        keys = [bytes(k) for k in keys]
+        n = len(keys)
+        ctx = (Schedule * n)(*[setup_encrypt(k) for k in keys])
+        ib = b"".join(bytes(v) for v in ivs) if ivs is not None else None
+        check(lib.fpnn_aes_keyset_set(self._h, first, n, ctx, C.c_char_p(ib) if ib is not None else None), "keyset_set")
+        self.count = max(self.count, first + n)
+
+    @classmethod
     def adopt(cls, engine: Engine, h, count: int, keylen: int) -> "KeySet":
         """Wrap a key set the library created (e.g. fpnn_ecdh_keyset)."""
         ks = cls.__new__(cls)

@@ -286,6 +286,53 @@ def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind)
 
 
 @pytest.mark.parametrize("keylen", [16, 32])
+@pytest.mark.parametrize("eng_kind", ["engine", "hybrid_lane_engine", "hybrid_quad_engine"])
+def test_keyset_writes_refresh_first_keystream_block(request, oracle, keylen, eng_kind):
+    """Block 0 of a package chain takes its keystream from the key set's per-slot E_k(IV)
+    (KBatch::eiv, k_slot_eiv; SURVEY section 0 point 3), which every key-set write must
+    refresh: slots set into a reserved table, two slots rewritten with new keys / IVs, and
+    the table grown past its capacity.  Frames of FPNN's typical 145 B (whole waves start
+    their chains together, so the kernels skip block 0's rounds), sub-block frames (the
+    keystream of a lone partial block) and a spread of other lengths, against the oracle
+    after each write."""
+    import fpnn_amd
+    engine = request.getfixturevalue(eng_kind)
+    rng = np.random.default_rng(8800 + keylen + len(eng_kind))
+    keys = rng.integers(0, 256, (6, keylen), dtype=np.uint8)
+    ivs = rng.integers(0, 256, (6, 16), dtype=np.uint8)
+    ks = fpnn_amd.KeySet.reserve(engine, 4, keylen)
+
+    def check(nused):
+        n = 3000
+        lens = np.full(n, 145, np.int64)
+        pick = rng.random(n) < 0.25
+        lens[pick] = rng.choice(np.array([1, 7, 15, 16, 17, 31, 32, 160, 1024]), pick.sum())
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+        slots = rng.integers(0, nused, n).astype(np.int32)
+        total = int(offs[-1] + lens[-1] + 16)
+        inp = rng.integers(0, 256, total, dtype=np.uint8)
+        exp = inp.copy()
+        oracle.package_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                             key_slot=slots.astype(np.uint32), keys=keys[:nused].reshape(-1).copy(),
+                             keylen=keylen, ivs=ivs[:nused].reshape(-1).copy(), threads=8)
+        src, dst = to_dev(inp), to_dev(inp)
+        engine.package_encrypt(src, dst, n, ks, in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)),
+                               key_slot=to_dev(slots))
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(dst), exp), nused
+
+    ks.set(0, keys[:4], ivs[:4])
+    check(4)
+    keys[1] = rng.integers(0, 256, keylen, dtype=np.uint8)
+    ivs[2] = rng.integers(0, 256, 16, dtype=np.uint8)
+    ks.set(1, keys[1:3], ivs[1:3])
+    check(4)
+    ks.set(4, keys[4:6], ivs[4:6])  # past the reserved capacity: the table grows
+    check(6)
+    ks.close()
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
 @pytest.mark.parametrize("length", [1, 5, 16, 17, 64, 100, 1024, 1040, 4096])
 def test_uniform_layout(engine, oracle, keylen, length):
     """Uniform fast path (stride/length, one key), incl. the in-place variant."""
