@@ -305,7 +305,7 @@ def main():
         del a, b, r
         print(json.dumps({"U1": out["U1"]}), flush=True)
 
-    if "Q1" in todo:
+    for qname in [q for q in ("Q1", "Q1g") if q in todo]:
         # FPNN's typical quest frames (145 B: core/test/tcp-test/asyncStressClient.cpp:13-29)
         # from 16 384 connections, each with its own key and IV, as one collector flush would
         # pass them (ragged layout, slot per frame): 9 whole blocks and a 1-byte tail per
@@ -315,7 +315,10 @@ def main():
         ks = fpnn_amd.KeySet(eng, keys.tobytes(), 32, ivs.tobytes())
         offs = torch.arange(P, dtype=torch.int64, device="cuda") * L
         lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
-        slots = (torch.arange(P, dtype=torch.int32, device="cuda") % NC).contiguous()
+        # Q1: consecutive frames from different connections (one quest per connection per
+        # IO cycle); Q1g: 8 consecutive frames per connection (a window of 8 per cycle)
+        idx = torch.arange(P, dtype=torch.int32, device="cuda")
+        slots = ((idx % NC) if qname == "Q1" else ((idx // 8) % NC)).contiguous()
         a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
         eng.fill_synthetic(a, 11)
         b, r = torch.empty_like(a), torch.empty_like(a)
@@ -323,12 +326,12 @@ def main():
         we, ke, _ = timed(eng, E, lambda: eng.package_encrypt(a, b, P, ks, **kw), args.reps)
         wd, kd, _ = timed(eng, D, lambda: eng.package_decrypt(b, r, P, ks, **kw), args.reps)
         assert torch.equal(r, a)
-        out["Q1"] = {"frames": P, "frame_bytes": L, "encrypt_kernel_GiBs": gib(P * L, ke),
+        out[qname] = {"frames": P, "frame_bytes": L, "encrypt_kernel_GiBs": gib(P * L, ke),
                      "decrypt_kernel_GiBs": gib(P * L, kd), "encrypt_wall_GiBs": gib(P * L, we),
                      "decrypt_wall_GiBs": gib(P * L, wd), "frames_per_s_encrypt_wall": round(P / we),
                      "cipher_sha256_16": __import__("hashlib").sha256(b.cpu().numpy()).hexdigest()[:16]}
         del a, b, r
-        print(json.dumps({"Q1": out["Q1"]}), flush=True)
+        print(json.dumps({qname: out[qname]}), flush=True)
 
     if "C4" in todo:
         c = W.C4
