@@ -180,6 +180,36 @@ __device__ __forceinline__ uint4 aes_encrypt_block_fenced(uint4 in, const RoundK
     return o;
 }
 
+// aes_encrypt_block with per-lane round keys read from LDS, one 16-byte row per round
+// (krow[r] = round key r): lanes of a wave that use different keys (K1r chunks spanning
+// several connections' frames) run one pass instead of one pass per key.  A row read is
+// one ds_read_b128 per round beside the round's 16 lookups.
+template <int NR, int NT, bool FENCE>
+__device__ __forceinline__ uint4 aes_encrypt_block_ldsk(uint4 in, const uint4 *krow, const Tables4<NT> &T) {
+    const uint4 k0 = krow[0];
+    uint32_t s0 = in.x ^ k0.x, s1 = in.y ^ k0.y, s2 = in.z ^ k0.z, s3 = in.w ^ k0.w;
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t a0 = T.template t<0>(s0), a1 = T.template t<1>(s1), a2 = T.template t<2>(s2), a3 = T.template t<3>(s3);
+        const uint32_t b0 = T.template t<0>(s1), b1 = T.template t<1>(s2), b2 = T.template t<2>(s3), b3 = T.template t<3>(s0);
+        const uint32_t c0 = T.template t<0>(s2), c1 = T.template t<1>(s3), c2 = T.template t<2>(s0), c3 = T.template t<3>(s1);
+        const uint32_t d0 = T.template t<0>(s3), d1 = T.template t<1>(s0), d2 = T.template t<2>(s1), d3 = T.template t<3>(s2);
+        const uint4 kr = krow[r];
+        if (FENCE) __builtin_amdgcn_sched_barrier(0);
+        s0 = xor3(xor3(a0, a1, a2), a3, kr.x);
+        s1 = xor3(xor3(b0, b1, b2), b3, kr.y);
+        s2 = xor3(xor3(c0, c1, c2), c3, kr.z);
+        s3 = xor3(xor3(d0, d1, d2), d3, kr.w);
+    }
+    const uint4 kn = krow[NR];
+    uint4 o;
+    o.x = T.last(s0, s1, s2, s3, kn.x);
+    o.y = T.last(s1, s2, s3, s0, kn.y);
+    o.z = T.last(s2, s3, s0, s1, kn.z);
+    o.w = T.last(s3, s0, s1, s2, kn.w);
+    return o;
+}
+
 template <bool FENCE, int NR, int NT>
 __device__ __forceinline__ uint4 aes_encrypt_block_sel(uint4 in, const RoundKeys<NR> &rk, const Tables4<NT> &T) {
     return FENCE ? aes_encrypt_block_fenced<NR, NT>(in, rk, T) : aes_encrypt_block<NR, NT>(in, rk, T);

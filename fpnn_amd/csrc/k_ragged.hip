@@ -138,14 +138,21 @@ __device__ __forceinline__ void set_keys(RoundKeys<NR> &rk, ConstDevKeyR *kp) {
     }
 }
 
+// key rows per wave in LDS for chunks spanning several key slots (process()): 8 AES-256
+// keys = 1 920 B per wave, 30 KiB per 16-wave workgroup beside the 128 KiB table image
+constexpr int kLdsKeys = 8;
+
 template <int NR, bool STREAM, int KM, bool FENCE>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, const RaggedPlan *__restrict__ plan,
                                                                      uint4 *sink) {
     __shared__ uint4 lds4[Lds<4>::kBytes / 16];
+    // KEY_LANE: each wave's rows for the round keys of up to kLdsKeys slots (process())
+    __shared__ uint4 lkeys[KM == KEY_LANE ? (kThreads / 64) * kLdsKeys * (NR + 1) : 1];
     lds_fill_tables<4>(lds4, b.t0le);
     __syncthreads();
     const Tables4<4> T{reinterpret_cast<const char *>(lds4), LaneBase()};
     const uint32_t lane = threadIdx.x & 63u;
+    uint4 *const wkeys = lkeys + (KM == KEY_LANE ? (threadIdx.x >> 6) * kLdsKeys * (NR + 1) : 0);
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t w = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
     const uint64_t count = b.count;
@@ -320,6 +327,39 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
         if (KM == KEY_UNIFORM) {
             ks = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
         } else {
+            // The chunk's distinct key slots.  One: a single pass with wave-uniform keys
+            // (below).  Two to kLdsKeys (small frames of many connections in one chunk --
+            // 145-B quests: about 7): the slots' round keys are staged in this wave's LDS
+            // rows and every lane runs ONE pass with its own row (aes_encrypt_block_ldsk);
+            // a pass per slot cost that many full AES passes of the wave.  More: one pass
+            // per slot as below.
+            uint32_t np = 0, kidx = 0, slotv = 0;
+            if (NR >= 12) {
+                uint64_t seen = __builtin_amdgcn_read_exec();
+                do {
+                    const uint32_t first = (uint32_t)__builtin_ctzll(seen);
+                    const uint32_t slotk = __builtin_amdgcn_readlane(X.slot, first);
+                    const bool mine = X.slot == slotk;
+                    seen &= ~__builtin_amdgcn_ballot_w64(mine);
+                    if (mine) kidx = np;
+                    slotv = lane == np ? slotk : slotv;  // lane k holds the k-th slot
+                    np++;
+                } while (seen);
+            }
+            if (NR >= 12 && np >= 2 && np <= (uint32_t)kLdsKeys) {  // (AES-128: its cached VGPR keys leave no room; below)
+                // lane l copies round-key rows [2 (l & 7), +2) of slot (l >> 3)'s key
+                constexpr int kRows = NR + 1;
+                const uint32_t kk = lane >> 3, r0 = 2 * (lane & 7);
+                const uint32_t sk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * kk), (int)slotv);
+                const uint4 *src = reinterpret_cast<const uint4 *>(b.keys[kk < np ? sk : 0u].rk);
+                uint4 v[2];
+#pragma unroll
+                for (int m = 0; m < 2; m++) v[m] = src[(r0 + m) < (uint32_t)kRows ? r0 + m : 0];
+#pragma unroll
+                for (int m = 0; m < 2; m++)
+                    if (kk < np && r0 + m < (uint32_t)kRows) wkeys[kk * kRows + r0 + m] = v[m];
+                ks = aes_encrypt_block_ldsk<NR, 4, FENCE && NR != 10>(kin, wkeys + kidx * kRows, T);
+            } else {
             // one pass per distinct key slot in the chunk, each with wave-uniform (SGPR)
             // round keys; a lane keeps the pass of its own slot.  Chunks inside one segment
             // (the common case) take one pass; no per-lane key registers.
@@ -350,6 +390,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 }
                 if (mine) ks = e;
             } while (todo);
+            }
         }
         if (STREAM && X.bi == 0 && X.n0 != 0) ks = ivs;  // keystream bytes already in the carried ivec
         // Stores are unconditional (lanes with nothing to store write the wave's scratch
