@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
             // a pass per slot cost that many full AES passes of the wave.  More: one pass
             // per slot as below.
             uint32_t np = 0, kidx = 0, slotv = 0;
-            if (NR >= 12) {
+            {
                 uint64_t seen = __builtin_amdgcn_read_exec();
                 do {
                     const uint32_t first = (uint32_t)__builtin_ctzll(seen);
@@ -346,9 +346,45 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                     np++;
                 } while (seen);
             }
-            if (NR >= 12 && np >= 2 && np <= (uint32_t)kLdsKeys) {  // (AES-128: its cached VGPR keys leave no room; below)
+            constexpr int kRows = NR + 1;
+            if (NR == 10) {
+                // AES-128 takes every chunk from the LDS rows: row 0 doubles as the cache of
+                // the last single slot (a stream's or connection's chunks follow each
+                // other), so one AES code path holds no key registers (the VGPR-cached keys
+                // beside the pipeline state left no room for a second path).  More than
+                // kLdsKeys slots: one pass per slot through row 0.
+                const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slotv);
+                if (np <= (uint32_t)kLdsKeys) {
+                    if (np != 1 || slot0 != key_slot) {
+                        const uint32_t kk = lane >> 3, r0 = 2 * (lane & 7);
+                        const uint32_t sk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * kk), (int)slotv);
+                        const uint4 *src = reinterpret_cast<const uint4 *>(b.keys[kk < np ? sk : 0u].rk);
+                        uint4 v[2];
+#pragma unroll
+                        for (int m = 0; m < 2; m++) v[m] = src[(r0 + m) < (uint32_t)kRows ? r0 + m : 0];
+#pragma unroll
+                        for (int m = 0; m < 2; m++)
+                            if (kk < np && r0 + m < (uint32_t)kRows) wkeys[kk * kRows + r0 + m] = v[m];
+                        key_slot = slot0;
+                    }
+                    ks = aes_encrypt_block_ldsk<NR, 4, false>(kin, wkeys + kidx * kRows, T);
+                } else {
+                    uint64_t todo = __builtin_amdgcn_read_exec();
+                    ks = make_uint4(0, 0, 0, 0);
+                    do {
+                        const uint32_t first = (uint32_t)__builtin_ctzll(todo);
+                        const uint32_t slotk = __builtin_amdgcn_readlane(X.slot, first);
+                        const bool mine = X.slot == slotk;
+                        todo &= ~__builtin_amdgcn_ballot_w64(mine);
+                        if (lane < (uint32_t)kRows)
+                            wkeys[lane] = reinterpret_cast<const uint4 *>(b.keys[slotk].rk)[lane];
+                        const uint4 e = aes_encrypt_block_ldsk<NR, 4, false>(kin, wkeys, T);
+                        if (mine) ks = e;
+                    } while (todo);
+                    key_slot = ~0u;
+                }
+            } else if (np >= 2 && np <= (uint32_t)kLdsKeys) {
                 // lane l copies round-key rows [2 (l & 7), +2) of slot (l >> 3)'s key
-                constexpr int kRows = NR + 1;
                 const uint32_t kk = lane >> 3, r0 = 2 * (lane & 7);
                 const uint32_t sk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * kk), (int)slotv);
                 const uint4 *src = reinterpret_cast<const uint4 *>(b.keys[kk < np ? sk : 0u].rk);
@@ -360,13 +396,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                     if (kk < np && r0 + m < (uint32_t)kRows) wkeys[kk * kRows + r0 + m] = v[m];
                 ks = aes_encrypt_block_ldsk<NR, 4, FENCE && NR != 10>(kin, wkeys + kidx * kRows, T);
             } else {
-            // one pass per distinct key slot in the chunk, each with wave-uniform (SGPR)
-            // round keys; a lane keeps the pass of its own slot.  Chunks inside one segment
-            // (the common case) take one pass; no per-lane key registers.
-            // AES-128: the round keys live in VGPRs and are reloaded only when the slot
-            // changes (a stream's or connection's chunks follow each other).  AES-192/256:
-            // scalar loads per pass (their 52-60 words fit neither register file for the
-            // whole loop beside the pipeline state).
+            // AES-192/256, one or more than kLdsKeys slots: one pass per distinct key slot in
+            // the chunk, each with wave-uniform (SGPR) round keys from scalar loads; a lane
+            // keeps the pass of its own slot.  Chunks inside one segment (the common case)
+            // take one pass; no per-lane key registers (52-60 words fit neither register
+            // file for the whole loop beside the pipeline state).
             uint64_t todo = __builtin_amdgcn_read_exec();
             ks = make_uint4(0, 0, 0, 0);
             do {
@@ -374,20 +408,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 const uint32_t slotk = __builtin_amdgcn_readlane(X.slot, first);
                 const bool mine = X.slot == slotk;
                 todo &= ~__builtin_amdgcn_ballot_w64(mine);
-                uint4 e;
-                if (NR == 10) {
-                    if (slotk != key_slot) {
-                        // fenced rounds hold 16 lookups in flight: 12 key words then stay in SGPRs
-                        // (all in VGPRs spill to scratch, more in SGPRs spill SGPRs)
-                        set_keys<NR, FENCE ? 12 : 0>(rku, (ConstDevKeyR *)b.keys + slotk);
-                        key_slot = slotk;
-                    }
-                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
-                } else {
-                    RoundKeys<NR> rk;
-                    set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
-                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rk, T);
-                }
+                RoundKeys<NR> rk;
+                set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
+                const uint4 e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rk, T);
                 if (mine) ks = e;
             } while (todo);
             }

@@ -305,20 +305,22 @@ def main():
         del a, b, r
         print(json.dumps({"U1": out["U1"]}), flush=True)
 
-    for qname in [q for q in ("Q1", "Q1g") if q in todo]:
+    for qname in [q for q in ("Q1", "Q1g", "Q1s") if q in todo]:
         # FPNN's typical quest frames (145 B: core/test/tcp-test/asyncStressClient.cpp:13-29)
         # from 16 384 connections, each with its own key and IV, as one collector flush would
         # pass them (ragged layout, slot per frame): 9 whole blocks and a 1-byte tail per
         # chain, so block 0 is a tenth of each chain (SURVEY section 0 point 3: E_k(IV))
+        # (Q1s: the same as Q1 with FPNN's default 16-byte keys instead of reinforced 32)
         P, L, NC = 2 << 20, 145, 16384
-        keys, ivs = W.many_keys(dict(W.U1, connections=NC, keylen=32))
-        ks = fpnn_amd.KeySet(eng, keys.tobytes(), 32, ivs.tobytes())
+        kl = 16 if qname == "Q1s" else 32
+        keys, ivs = W.many_keys(dict(W.U1, connections=NC, keylen=kl))
+        ks = fpnn_amd.KeySet(eng, keys.tobytes(), kl, ivs.tobytes())
         offs = torch.arange(P, dtype=torch.int64, device="cuda") * L
         lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
         # Q1: consecutive frames from different connections (one quest per connection per
         # IO cycle); Q1g: 8 consecutive frames per connection (a window of 8 per cycle)
         idx = torch.arange(P, dtype=torch.int32, device="cuda")
-        slots = ((idx % NC) if qname == "Q1" else ((idx // 8) % NC)).contiguous()
+        slots = ((idx // 8) % NC if qname == "Q1g" else idx % NC).contiguous()
         a = torch.empty(P * L, dtype=torch.uint8, device="cuda")
         eng.fill_synthetic(a, 11)
         b, r = torch.empty_like(a), torch.empty_like(a)
