@@ -161,9 +161,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     wave_chunk_range((total + 63) >> 6, nwaves, w, c0, c1);
     if (c0 >= c1) return;
 
-    // round keys (VGPRs): the batch's one key, or (KEY_LANE) the last slot used
+    // round keys: the batch's one key (KEY_LANE: per chunk in process())
     RoundKeys<NR> rku;
-    uint32_t key_slot = ~0u;
     uint4 ivu = make_uint4(0, 0, 0, 0);
     if (KM == KEY_UNIFORM) {
         ConstDevKeyR *kp = (ConstDevKeyR *)b.keys;
@@ -348,14 +347,16 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
             }
             constexpr int kRows = NR + 1;
             if (NR == 10) {
-                // AES-128 takes every chunk from the LDS rows: row 0 doubles as the cache of
-                // the last single slot (a stream's or connection's chunks follow each
-                // other), so one AES code path holds no key registers (the VGPR-cached keys
-                // beside the pipeline state left no room for a second path).  More than
-                // kLdsKeys slots: one pass per slot through row 0.
+                // AES-128: one slot -- SGPR keys (scalar loads per chunk; the VGPR-cached keys
+                // of earlier rounds left no room beside the pipeline state for the LDS-row
+                // path); 2..kLdsKeys -- the LDS rows; more -- one pass per slot through row 0.
                 const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slotv);
-                if (np <= (uint32_t)kLdsKeys) {
-                    if (np != 1 || slot0 != key_slot) {
+                if (np == 1) {  // one slot: wave-uniform keys from scalar loads (SGPRs), no LDS rows
+                    RoundKeys<NR> rk;
+                    set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slot0);
+                    ks = aes_encrypt_block<NR, 4>(kin, rk, T);
+                } else if (np <= (uint32_t)kLdsKeys) {
+                    {
                         const uint32_t kk = lane >> 3, r0 = 2 * (lane & 7);
                         const uint32_t sk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * kk), (int)slotv);
                         const uint4 *src = reinterpret_cast<const uint4 *>(b.keys[kk < np ? sk : 0u].rk);
@@ -365,7 +366,6 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
 #pragma unroll
                         for (int m = 0; m < 2; m++)
                             if (kk < np && r0 + m < (uint32_t)kRows) wkeys[kk * kRows + r0 + m] = v[m];
-                        key_slot = slot0;
                     }
                     ks = aes_encrypt_block_ldsk<NR, 4, false>(kin, wkeys + kidx * kRows, T);
                 } else {
@@ -381,7 +381,6 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                         const uint4 e = aes_encrypt_block_ldsk<NR, 4, false>(kin, wkeys, T);
                         if (mine) ks = e;
                     } while (todo);
-                    key_slot = ~0u;
                 }
             } else if (np >= 2 && np <= (uint32_t)kLdsKeys) {
                 // lane l copies round-key rows [2 (l & 7), +2) of slot (l >> 3)'s key
