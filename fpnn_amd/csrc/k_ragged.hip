@@ -161,8 +161,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
     wave_chunk_range((total + 63) >> 6, nwaves, w, c0, c1);
     if (c0 >= c1) return;
 
-    // round keys: the batch's one key (KEY_LANE: per chunk in process())
+    // round keys: the batch's one key; KEY_LANE AES-128 stream batches: the last slot's
+    // (VGPRs, reloaded when the slot changes -- a stream's chunks follow each other)
     RoundKeys<NR> rku;
+    uint32_t key_slot = ~0u;
     uint4 ivu = make_uint4(0, 0, 0, 0);
     if (KM == KEY_UNIFORM) {
         ConstDevKeyR *kp = (ConstDevKeyR *)b.keys;
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
             // a pass per slot cost that many full AES passes of the wave.  More: one pass
             // per slot as below.
             uint32_t np = 0, kidx = 0, slotv = 0;
-            {
+            if (NR >= 12 || !STREAM) {
                 uint64_t seen = __builtin_amdgcn_read_exec();
                 do {
                     const uint32_t first = (uint32_t)__builtin_ctzll(seen);
@@ -346,8 +348,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 } while (seen);
             }
             constexpr int kRows = NR + 1;
-            if (NR == 10) {
-                // AES-128: one slot -- SGPR keys (scalar loads per chunk; the VGPR-cached keys
+            if (NR == 10 && !STREAM) {
+                // AES-128 package batches (FPNN's receive frames): one slot -- SGPR keys (scalar loads per chunk; the VGPR-cached keys
                 // of earlier rounds left no room beside the pipeline state for the LDS-row
                 // path); 2..kLdsKeys -- the LDS rows; more -- one pass per slot through row 0.
                 const uint32_t slot0 = __builtin_amdgcn_readfirstlane(slotv);
@@ -395,11 +397,12 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                     if (kk < np && r0 + m < (uint32_t)kRows) wkeys[kk * kRows + r0 + m] = v[m];
                 ks = aes_encrypt_block_ldsk<NR, 4, FENCE && NR != 10>(kin, wkeys + kidx * kRows, T);
             } else {
-            // AES-192/256, one or more than kLdsKeys slots: one pass per distinct key slot in
-            // the chunk, each with wave-uniform (SGPR) round keys from scalar loads; a lane
-            // keeps the pass of its own slot.  Chunks inside one segment (the common case)
-            // take one pass; no per-lane key registers (52-60 words fit neither register
-            // file for the whole loop beside the pipeline state).
+            // One pass per distinct key slot in the chunk (AES-192/256 with one or more than
+            // kLdsKeys slots; AES-128 stream batches, whose VGPR-cached keys leave no room for
+            // the LDS rows -- their long segments seldom share a chunk), a lane keeping the
+            // pass of its own slot.  Chunks inside one segment (the common case) take one
+            // pass.  AES-192/256: SGPR keys from scalar loads per pass (52-60 words fit
+            // neither register file for the whole loop beside the pipeline state).
             uint64_t todo = __builtin_amdgcn_read_exec();
             ks = make_uint4(0, 0, 0, 0);
             do {
@@ -407,9 +410,20 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_decrypt_ragged(KBatch b, co
                 const uint32_t slotk = __builtin_amdgcn_readlane(X.slot, first);
                 const bool mine = X.slot == slotk;
                 todo &= ~__builtin_amdgcn_ballot_w64(mine);
-                RoundKeys<NR> rk;
-                set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
-                const uint4 e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rk, T);
+                uint4 e;
+                if (NR == 10) {  // (stream batches) VGPR keys, reloaded when the slot changes
+                    if (slotk != key_slot) {
+                        // fenced rounds hold 16 lookups in flight: 12 key words then stay in SGPRs
+                        // (all in VGPRs spill to scratch, more in SGPRs spill SGPRs)
+                        set_keys<NR, FENCE ? 12 : 0>(rku, (ConstDevKeyR *)b.keys + slotk);
+                        key_slot = slotk;
+                    }
+                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rku, T);
+                } else {
+                    RoundKeys<NR> rk;
+                    set_keys<NR, 4 * (NR + 1)>(rk, (ConstDevKeyR *)b.keys + slotk);
+                    e = aes_encrypt_block_sel<FENCE, NR, 4>(kin, rk, T);
+                }
                 if (mine) ks = e;
             } while (todo);
             }
