@@ -461,7 +461,8 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // chain (K2c); otherwise one lane per chain with 8-block chunks (K2).
     const uint64_t full_chip = (uint64_t)e->num_cus * kThreads;
     const uint64_t coop_below = e->variant.coop_below < 0 ? full_chip : (uint64_t)e->variant.coop_below;
-    if (b->count < coop_below || b->len != nullptr) {
+    const bool k2_ragged = e->variant.k2_ragged && b->len && b->count >= full_chip && !(b->flags & FPNN_AES_F_WIRE_PREFIX);
+    if ((b->count < coop_below || b->len != nullptr) && !k2_ragged) {
         const uint64_t lanes = 4 * b->count;
         int threads = 64;
         while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
@@ -705,6 +706,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_COOP_BELOW")) e->variant.coop_below = atoll(v);
     if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed

@@ -71,6 +71,7 @@ struct Variant {
     int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
     int64_t coop_below = -1;  // uniform batches of fewer chains take K2c (-1: a full chip's lanes)
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
+    int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;
