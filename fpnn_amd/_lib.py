@@ -71,7 +71,7 @@ class BatchDesc(C.Structure):
         ("key_slot", C.c_void_p),
         ("keys", C.c_void_p),
         ("flags", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("max_len", C.c_uint32),
     ]
 
 

@@ -461,7 +461,14 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // chain (K2c); otherwise one lane per chain with 8-block chunks (K2).
     const uint64_t full_chip = (uint64_t)e->num_cus * kThreads;
     const uint64_t coop_below = e->variant.coop_below < 0 ? full_chip : (uint64_t)e->variant.coop_below;
-    const bool k2_ragged = e->variant.k2_ragged && b->len && b->count >= full_chip && !(b->flags & FPNN_AES_F_WIRE_PREFIX);
+    // Ragged package batches of many short frames (the caller's max_len bound): one lane
+    // per chain in grid-stride order (K2) -- Q1, 2 M x 145-B quests of 16 384 keyed
+    // connections: 491 against K2h's 343 GiB/s (its work-queue atomics and length-order
+    // indirection per chain; profiles/r05/ab_k2_short).  Without a bound K2h, which also
+    // balances Zipf-like lengths (C4 on K2: 88 GiB/s).
+    const bool k2_ragged = b->len && !stream && !(b->flags & FPNN_AES_F_WIRE_PREFIX) &&
+                           ((e->variant.k2_ragged && b->count >= full_chip) ||
+                            (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= 4 * full_chip));
     if ((b->count < coop_below || b->len != nullptr) && !k2_ragged) {
         const uint64_t lanes = 4 * b->count;
         int threads = 64;
@@ -707,6 +714,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_COOP_BELOW")) e->variant.coop_below = atoll(v);
     if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_SHORT")) e->variant.k2_short = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed

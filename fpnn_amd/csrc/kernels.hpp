@@ -72,6 +72,7 @@ struct Variant {
     int64_t coop_below = -1;  // uniform batches of fewer chains take K2c (-1: a full chip's lanes)
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
+    int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;

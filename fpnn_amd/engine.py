@@ -321,7 +321,7 @@ class Engine:
 
     # -- batches ----------------------------------------------------------------------------
     def _desc(self, inp, out, count, keys, *, stride=0, uniform_len=0, in_off=None, out_off=None, lens=None,
-              key_slot=None, flags=0) -> BatchDesc:
+              key_slot=None, flags=0, max_len=0) -> BatchDesc:
         d = BatchDesc()
         d.in_ = _ptr(inp).value if inp is not None else None
         d.out = _ptr(out).value if out is not None else None
@@ -338,6 +338,7 @@ class Engine:
                 setattr(d, name, _ptr(t).value)
         d.keys = keys.handle.value
         d.flags = flags
+        d.max_len = max_len  # optional bound on every length (fpnn_aes.h: picks K2 for many short frames)
         return d
 
     def package_encrypt(self, inp, out, count, keys: "KeySet", wire_prefix: bool = False, **kw):
