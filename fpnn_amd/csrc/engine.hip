@@ -466,7 +466,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // connections: 491 against K2h's 343 GiB/s (its work-queue atomics and length-order
     // indirection per chain; profiles/r05/ab_k2_short).  Without a bound K2h, which also
     // balances Zipf-like lengths (C4 on K2: 88 GiB/s).
-    const bool k2_ragged = b->len && !stream && !(b->flags & FPNN_AES_F_WIRE_PREFIX) &&
+    const bool k2_ragged = b->len && !stream &&
                            ((e->variant.k2_ragged && b->count >= full_chip) ||
                             (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= 4 * full_chip));
     if ((b->count < coop_below || b->len != nullptr) && !k2_ragged) {

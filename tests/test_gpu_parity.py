@@ -318,6 +318,18 @@ def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keyle
         torch.cuda.synchronize()
         assert engine.last_kernel(fpnn_amd.K_ENCRYPT) == kernel, (bound, engine.last_kernel(fpnn_amd.K_ENCRYPT))
         assert np.array_equal(to_host(dst), exp), bound
+    # the wire frames of the same batch (htole32(len) || C, PackageEncryptor::encrypt(std::string*))
+    wout = (offs + 4 * np.arange(n)).astype(np.int64)  # frames back to back, 4 bytes longer each
+    for bound, kernel in ((300, "cfb_encrypt_chains"), (0, "cfb_encrypt_hybrid")):
+        wdst = torch.zeros(total + 4 * n, dtype=torch.uint8, device="cuda")
+        engine.package_encrypt(src, wdst, n, ks, wire_prefix=True, max_len=bound, out_off=to_dev(wout), **kw)
+        torch.cuda.synchronize()
+        assert engine.last_kernel(fpnn_amd.K_ENCRYPT) == kernel
+        got = to_host(wdst)
+        for i in rng.integers(0, n, 2000):  # a sample of frames against the ciphertext above
+            o, ln = int(wout[i]), int(lens[i])
+            assert np.array_equal(got[o:o + 4 + ln], np.concatenate(
+                [np.frombuffer(ln.to_bytes(4, "little"), np.uint8), exp[int(offs[i]):int(offs[i]) + ln]])), (bound, i)
 
 
 @pytest.mark.parametrize("keylen", [16, 32])

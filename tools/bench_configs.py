@@ -457,7 +457,8 @@ def main():
         out_off = torch.arange(P, dtype=torch.int64, device="cuda") * (L + 4)
         lens = torch.full((P,), L, dtype=torch.int32, device="cuda")
         def wire_encrypt():  # the send side: bodies -> htole32(len) || ciphertext (K2q)
-            eng.package_encrypt(a, wire, P, ks, in_off=in_off, out_off=out_off, lens=lens, wire_prefix=True)
+            eng.package_encrypt(a, wire, P, ks, in_off=in_off, out_off=out_off, lens=lens, wire_prefix=True,
+                                max_len=L)  # (the sender knows its frames' length bound)
 
         we, ke, _ = timed(eng, E, wire_encrypt, args.reps)
         conn_off = torch.arange(NC, dtype=torch.int64, device="cuda") * (F * (L + 4))
