@@ -1635,7 +1635,11 @@ HostPool *pool_of(fpnn_aes_engine *e) {
 
 // parts for `bytes` of copying: about 1 MiB per thread at least
 unsigned copy_parts(fpnn_aes_engine *e, uint64_t bytes) {
-    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pool_of(e)->parts(), bytes >> 20));
+    static const int grain = [] {  // bytes per copy thread: 2^grain (FPNN_AES_COPY_GRAIN, A/B)
+        const char *v = getenv("FPNN_AES_COPY_GRAIN");
+        return v ? std::max(12, std::min(30, atoi(v))) : 20;
+    }();
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pool_of(e)->parts(), bytes >> grain));
 }
 
 void parallel_copy(fpnn_aes_engine *e, const std::vector<CopyJob> &jobs, uint64_t total) {
