@@ -33,14 +33,20 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
     if (kFirst && KM == KEY_UNIFORM) eiv_u = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
 
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    // per-lane keys: kept while the lane's next chain has the same slot (a connection's
+    // frames a grid stride apart; Q1's 16 384 connections: every chain of a lane) -- the
+    // reload is 240 B per lane from L2 / the Infinity Cache per chain otherwise
+    RoundKeys<NR> rk;
+    uint32_t rk_slot = ~0u;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
         const Seg g = get_seg<LAYOUT>(b, s);
         const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
-        RoundKeys<NR> rk;
-        if (KM == KEY_UNIFORM)
+        if (KM == KEY_UNIFORM) {
             rk = rku;
-        else
+        } else if (g.slot != rk_slot) {
             rk = load_round_keys<NR>(key);
+            rk_slot = g.slot;
+        }
         uint4 eiv = eiv_u;
         if (kFirst && KM != KEY_UNIFORM && use_eiv) eiv = b.eiv[g.slot];
 
