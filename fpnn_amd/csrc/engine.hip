@@ -370,8 +370,11 @@ int stream_idle(fpnn_aes_engine *e) {
     free_deferred(e);
     const uint32_t f = e->h_fault ? __atomic_exchange_n(e->h_fault, 0u, __ATOMIC_ACQ_REL) : 0u;
     if (!f) return FPNN_AES_OK;
-    g_last_error = (f & kFaultLookback) ? "block map: a look-back gave up waiting for a tile (results of that call invalid)"
-                                        : "device-side check failed";
+    if ((f & kFaultLengthOrder) && e->d_buckets)  // start the next ragged call from a zero block
+        (void)hipMemsetAsync(e->d_buckets, 0, e->cap_buckets * sizeof(uint32_t), e->stream);
+    g_last_error = (f & kFaultLookback)      ? "block map: a look-back gave up waiting for a tile (results of that call invalid)"
+                   : (f & kFaultLengthOrder) ? "length order: bucket counts did not add up to the batch (results of that call invalid)"
+                                             : "device-side check failed";
     return FPNN_AES_ERR_DEVICE;
 }
 
@@ -490,7 +493,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
                 k.pos_snap = pos_state;
             }
             block = e->d_buckets;
-            HIP_TRY(launch_length_order(k, stream, e->d_perm, block, !hybrid, e->stream));
+            HIP_TRY(launch_length_order(k, stream, e->d_perm, block, !hybrid, e->d_fault, e->stream));
             k.perm = e->d_perm;
         }
         EventPair *ev;

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 
     const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
     for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; t < b.count; t += nquads) {
-        const uint64_t s = b.perm ? b.perm[t] : t;  // longest chains first (ragged batches)
+        const uint64_t s = b.perm ? min(b.perm[t], (uint32_t)b.count - 1u) : t;  // longest chains first (ragged batches)
         const Seg g = get_seg<LAYOUT>(b, s);
         const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
         uint32_t rkq[NR + 1];

@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 16 readable bytes
         uint8_t *const sinkw = reinterpret_cast<uint8_t *>(h.sink + 2 * ((uint64_t)blockIdx.x * (kThreads / 64) + wave));
         auto begin = [&](uint64_t t) {
-            const uint64_t s = b.perm[t];
+            const uint64_t s = min(b.perm[t], (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
             const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             return KM == KEY_UNIFORM ? aes_encrypt_block<NR, NT>(x, rku, T) : aes_encrypt_block<NR, NT>(x, rkl, T);
         };
         auto begin = [&](uint64_t t) {
-            const uint64_t s = b.perm[t];
+            const uint64_t s = min(b.perm[t], (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
             const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);

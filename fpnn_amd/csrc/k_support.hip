@@ -329,7 +329,8 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
     if (threadIdx.x == 0 && off4) atomicOr(&counts[kWireFlagWord], 1u);
 }
 
-__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor) {
+__global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor, uint64_t count,
+                                                          uint32_t *fault) {
     __shared__ uint32_t sh[kBuckets];
     const int t = threadIdx.x;
     sh[t] = counts[t];
@@ -341,6 +342,9 @@ __global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint
         __syncthreads();
     }
     cursor[t] = sh[t] - counts[t];  // exclusive
+    // the counts of a block that was zero on entry add up to the batch
+    if (t == kBuckets - 1 && sh[t] != count && fault)
+        __hip_atomic_store(fault, kFaultLengthOrder, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <bool STREAM>
@@ -367,13 +371,14 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *curs
         const bool live = kb[i] < (uint32_t)kBuckets;
         const uint32_t k = live ? kb[i] : 0u;
         const uint32_t slot = bucket_add(cnt, k, live);
-        if (live) perm[base[k] + slot] = (uint32_t)(tile0 + 256ull * i);
+        const uint32_t at = base[k] + slot;
+        if (live && at < b.count) perm[at] = (uint32_t)(tile0 + 256ull * i);  // (past it: a bad block, see scan)
     }
     if (release) length_order_release(release);  // K2c follows: nothing reads the block again
 }
 
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, bool zero_after,
-                               hipStream_t st) {
+                               uint32_t *fault, hipStream_t st) {
     uint32_t *counts = block, *cursor = block + kBuckets;
     const unsigned grid = (unsigned)((b.count + kBucketTile - 1) / kBucketTile);
     uint32_t *release = zero_after ? block : nullptr;
@@ -381,7 +386,7 @@ hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uin
         hipLaunchKernelGGL((k_bucket_count<true>), dim3(grid), dim3(256), 0, st, b, counts);
     else
         hipLaunchKernelGGL((k_bucket_count<false>), dim3(grid), dim3(256), 0, st, b, counts);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(kBuckets), 0, st, counts, cursor, b.count, fault);
     if (stream)
         hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(grid), dim3(256), 0, st, b, cursor, perm, release);
     else

@@ -148,9 +148,12 @@ uint32_t length_bucket_of(uint64_t nblocks);
 // Ragged batches: perm[] = segment indices ordered by block count, longest first
 // (quarter-octave buckets).  block: the length-order block (zero on entry); zero_after:
 // nothing reads it after the scatter (K2c follows), so the scatter's last workgroup zeroes
-// it; otherwise K2h does.
+// it; otherwise K2h does.  fault: as for the block map below -- gets kFaultLengthOrder when
+// the bucket counts do not add up to b.count (a block not zero on entry); the scatter then
+// writes no perm[] entry past the batch and K2h clamps what it reads, so a bad block gives
+// FPNN_AES_ERR_DEVICE at the next sync instead of wild addresses.
 hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uint32_t *block, bool zero_after,
-                               hipStream_t st);
+                               uint32_t *fault, hipStream_t st);
 // K1 / K1d / K1k for uniform and dense layouts (every segment's block count known on the host).
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
                                  hipStream_t st);
@@ -182,6 +185,7 @@ hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart,
 // fault: a device-visible word (pinned host) that gets kFaultLookback if a look-back ever
 // gave up waiting (the host reports FPNN_AES_ERR_DEVICE at the next sync).
 constexpr uint32_t kFaultLookback = 1u;
+constexpr uint32_t kFaultLengthOrder = 2u;
 uint64_t block_map_onepass_words(uint64_t count);
 hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *lb, uint64_t lb_words,
                                     uint32_t *fault, uint64_t *total, hipStream_t st);
