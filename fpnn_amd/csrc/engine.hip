@@ -493,6 +493,10 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
                 k.pos_snap = pos_state;
             }
             block = e->d_buckets;
+            if (e->variant.poison_order > 0) {  // (tests) bucket counts left over as if by a lost call
+                e->variant.poison_order--;
+                HIP_TRY(hipMemsetAsync(block, 0x01, kWireFlagWord / 2 * sizeof(uint32_t), e->stream));
+            }
             HIP_TRY(launch_length_order(k, stream, e->d_perm, block, !hybrid, e->d_fault, e->stream));
             k.perm = e->d_perm;
         }
@@ -718,6 +722,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_SHORT")) e->variant.k2_short = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_DEBUG_POISON_ORDER")) e->variant.poison_order = std::max(0, atoi(v));
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     uint32_t part = 0;
     if (lane <= h.long_bucket) part += h.buckets[lane];
     if (lane + 64 <= h.long_bucket) part += h.buckets[lane + 64];
-    const uint64_t n_long = __builtin_amdgcn_readfirstlane(wave_sum32(part));
+    // (at most the batch even when the block's counts are bad, kernels.hpp kFaultLengthOrder)
+    const uint64_t n_long = min((uint64_t)__builtin_amdgcn_readfirstlane(wave_sum32(part)), b.count);
     // quad tickets below static_q are dealt at start, the rest come from h.ctr[0]
     const uint64_t static_q = (uint64_t)h.quad_waves * 16u * gridDim.x;
     // wire batches: every body starts on the 4-byte grid (flag set by the length ordering)

@@ -73,6 +73,9 @@ struct Variant {
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
     int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
+    // tests only: the next poison_order ragged encrypts find their length-order block's
+    // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
+    int poison_order = 0;
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
     // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
     int k1r_runs = 1;

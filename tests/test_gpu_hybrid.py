@@ -152,3 +152,51 @@ def test_many_stream_segments(request, oracle, eng_kind, keylen):
         assert np.array_equal(_host(dst), exp), call
         assert np.array_equal(_host(iv_d), iv_h), call
         assert np.array_equal(_host(pos_d).astype(np.uint32), pos_h), call
+
+
+@pytest.mark.parametrize("path,wire", [("k2c", False), ("k2h", False), ("k2h", True), ("k2h_lanes", True)])
+def test_dirty_length_order_block_reported(oracle, path, wire):
+    """The length-order block must be zero when a ragged encrypt starts (kernels.hpp).  With
+    its bucket counts dirtied on purpose (FPNN_AES_DEBUG_POISON_ORDER: once, before the call)
+    the call must stay in bounds -- no HIP fault -- and report FPNN_AES_ERR_DEVICE at the next
+    sync; the engine then zeroes the block and the next call is right again."""
+    import fpnn_amd
+    from fpnn_amd._lib import ERR_DEVICE, FpnnAesError
+    from conftest import _env_engine
+    env = {"FPNN_AES_DEBUG_POISON_ORDER": "1"}
+    if path != "k2c":
+        env["FPNN_AES_HYB_FORCE"] = "1"
+    if path == "k2h_lanes":
+        env.update({"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2", "FPNN_AES_HYB_WIRE_LANES": "1"})
+    eng = _env_engine(env)
+    try:
+        rng = np.random.default_rng(5150 + len(path) + wire)
+        n = 3000
+        lens = rng.integers(0, 2000, n)
+        in_off = np.concatenate([[0], np.cumsum(lens[:-1] + 3)]).astype(np.int64) + 1
+        out_off = np.concatenate([[0], np.cumsum(lens[:-1] + 7)]).astype(np.int64) + 2
+        plain = rng.integers(0, 256, int(in_off[-1] + lens[-1] + 32), dtype=np.uint8)
+        dst0 = rng.integers(0, 256, int(out_off[-1] + lens[-1] + 64), dtype=np.uint8)
+        key, iv = rng.integers(0, 256, 16, dtype=np.uint8), rng.integers(0, 256, 16, dtype=np.uint8)
+        ks = fpnn_amd.KeySet(eng, key.tobytes(), 16, iv.tobytes())
+        if wire:
+            exp = _wire_expected(oracle, plain, dst0, n, in_off, out_off, lens, None, key, 16, iv)
+        else:
+            exp = dst0.copy()
+            oracle.package_batch(True, plain, exp, n, in_off=in_off.astype(np.uint64),
+                                 out_off=out_off.astype(np.uint64), lens=lens.astype(np.uint32),
+                                 keys=key, keylen=16, ivs=iv, threads=8)
+        args = dict(in_off=_dev(in_off), out_off=_dev(out_off), lens=_dev(lens.astype(np.int32)), wire_prefix=wire)
+        src = _dev(plain)
+        dst = _dev(dst0)
+        eng.package_encrypt(src, dst, n, ks, **args)
+        torch.cuda.synchronize()  # a wild access would surface here as a HIP error
+        with pytest.raises(FpnnAesError) as ei:
+            eng.sync()
+        assert ei.value.status == ERR_DEVICE and "length order" in str(ei.value)
+        dst = _dev(dst0)
+        eng.package_encrypt(src, dst, n, ks, **args)
+        assert np.array_equal(_host(dst), exp)
+        eng.sync()
+    finally:
+        eng.close()
