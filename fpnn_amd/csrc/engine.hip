@@ -535,7 +535,9 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream,
+                                  (e->variant.k2_fence ? kEncFenceGeneral : 0u) |
+                                      (e->variant.k2_lane_c4 ? kEncLaneChunk4 : 0u)));
     return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
 }
 
@@ -722,6 +724,8 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_SHORT")) e->variant.k2_short = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_FENCE")) e->variant.k2_fence = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_LANE_C4")) e->variant.k2_lane_c4 = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEBUG_POISON_ORDER")) e->variant.poison_order = std::max(0, atoi(v));
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;

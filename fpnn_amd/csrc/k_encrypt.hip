@@ -308,13 +308,35 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 // round issued before any fold); the other layouts hold more live registers per lane and
 // keep the plain round.
 template <int NR>
-static void enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads, hipStream_t st) {
+static void enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, unsigned opts, int grid, int threads,
+                   hipStream_t st) {
 #define FPNN_ENC(L, K, S) hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, 4, 8>), dim3(grid), dim3(threads), 0, st, b)
+    const bool fence_general = opts & kEncFenceGeneral;
+    if (layout != LAYOUT_UNIFORM && km == KEY_LANE && (opts & kEncLaneChunk4) && NR != 14) {
+        // per-lane AES-128/192 round keys beside 8-block chunks spill VGPRs: 4-block chunks (A/B)
+        if (stream)
+            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, true, 4, 4>), dim3(grid), dim3(threads),
+                               0, st, b);
+        else if (fence_general)
+            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 4, true>), dim3(grid),
+                               dim3(threads), 0, st, b);
+        else
+            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 4>), dim3(grid),
+                               dim3(threads), 0, st, b);
+        return;
+    }
     if (layout == LAYOUT_UNIFORM && !stream) {
         hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_UNIFORM, KEY_UNIFORM, false, 4, 8, true>), dim3(grid),
                            dim3(threads), 0, st, b);
     } else if (layout == LAYOUT_UNIFORM) {
         FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true);
+    } else if (!stream && fence_general) {  // (Variant::k2_fence: ragged package batches, A/B)
+        if (km == KEY_UNIFORM)
+            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_UNIFORM, false, 4, 8, true>), dim3(grid),
+                               dim3(threads), 0, st, b);
+        else
+            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 8, true>), dim3(grid),
+                               dim3(threads), 0, st, b);
     } else if (km == KEY_UNIFORM) {
         if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false);
     } else {
@@ -356,12 +378,12 @@ const char *last_launched() { return g_launched; }
 void set_launched(const char *name) { g_launched = name; }
 
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
-                                 int threads, hipStream_t st) {
+                                 int threads, hipStream_t st, unsigned opts) {
     set_launched("cfb_encrypt_chains");
     switch (nrounds) {
-        case 10: enc_nr<10>(b, layout, km, stream, grid, threads, st); break;
-        case 12: enc_nr<12>(b, layout, km, stream, grid, threads, st); break;
-        case 14: enc_nr<14>(b, layout, km, stream, grid, threads, st); break;
+        case 10: enc_nr<10>(b, layout, km, stream, opts, grid, threads, st); break;
+        case 12: enc_nr<12>(b, layout, km, stream, opts, grid, threads, st); break;
+        case 14: enc_nr<14>(b, layout, km, stream, opts, grid, threads, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -73,6 +73,8 @@ struct Variant {
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
     int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
+    int k2_fence = 0;         // K2 on ragged package batches with the fenced round (C2's), else the plain one
+    int k2_lane_c4 = 0;       // K2 with per-lane AES-128/192 keys in 4-block chunks (8: VGPR spills)
     // tests only: the next poison_order ragged encrypts find their length-order block's
     // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
     int poison_order = 0;
@@ -118,7 +120,10 @@ struct KScan {
 
 hipError_t launch_scan_frames(const KScan &s, bool stream, int num_cus, hipStream_t st);
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
-                                 int threads, hipStream_t st);
+                                 int threads, hipStream_t st, unsigned opts = 0);
+// launch_encrypt_chains opts: the fenced round on ragged package batches (Variant::k2_fence);
+// 4-block chunks for per-lane AES-128/192 keys (Variant::k2_lane_c4)
+constexpr unsigned kEncFenceGeneral = 1u, kEncLaneChunk4 = 2u;
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st);
