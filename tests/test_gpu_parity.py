@@ -285,22 +285,21 @@ def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind)
         assert np.array_equal(to_host(dst), exp), f"encrypt={encrypt}"
 
 
-@pytest.mark.parametrize("keylen", [16, 32])
-def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keylen):
+@pytest.mark.parametrize("keylen,nk", [(16, 1000), (32, 1000), (32, 1)])
+def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keylen, nk):
     """fpnn_aes_batch.max_len: a ragged per-key package encrypt of >= 4 chains per GPU lane
     whose lengths the caller bounds by <= 2048 bytes runs one lane per chain in grid-stride
     order (K2) instead of the length-ordered hybrid (Q1: 491 vs 343 GiB/s).  1.1 M frames of
     1-300 bytes (sub-block, block-aligned and ragged tails) from 1000 keyed connections,
-    the ciphertext against the oracle; the same batch without the bound takes K2h and must
-    give the same bytes."""
+    the ciphertext against the oracle (and from one key: R1's send side); the same batch
+    without the bound takes K2h and must give the same bytes."""
     import fpnn_amd
-    rng = np.random.default_rng(9900 + keylen)
+    rng = np.random.default_rng(9900 + keylen + nk)
     n = 1_100_000
     lens = rng.integers(1, 301, n).astype(np.int64)
     pick = rng.random(n) < 0.1
     lens[pick] = 16 * rng.integers(1, 19, int(pick.sum()))  # whole blocks
     offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
-    nk = 1000
     keys = rng.integers(0, 256, nk * keylen, dtype=np.uint8)
     ivs = rng.integers(0, 256, nk * 16, dtype=np.uint8)
     slots = rng.integers(0, nk, n).astype(np.int32)
