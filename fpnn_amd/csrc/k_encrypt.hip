@@ -312,12 +312,10 @@ static void enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, unsi
                    hipStream_t st) {
 #define FPNN_ENC(L, K, S) hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, 4, 8>), dim3(grid), dim3(threads), 0, st, b)
     const bool fence_general = opts & kEncFenceGeneral;
-    if (layout != LAYOUT_UNIFORM && km == KEY_LANE && (opts & kEncLaneChunk4) && NR != 14) {
-        // per-lane AES-128/192 round keys beside 8-block chunks spill VGPRs: 4-block chunks (A/B)
-        if (stream)
-            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, true, 4, 4>), dim3(grid), dim3(threads),
-                               0, st, b);
-        else if (fence_general)
+    if (layout != LAYOUT_UNIFORM && km == KEY_LANE && !stream && (opts & kEncLaneChunk4) && NR != 14) {
+        // per-lane AES-128/192 round keys beside 8-block chunks spill VGPRs: 4-block chunks
+        // (measured on package batches, Q1s; stream batches keep 8)
+        if (fence_general)
             hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 4, true>), dim3(grid),
                                dim3(threads), 0, st, b);
         else

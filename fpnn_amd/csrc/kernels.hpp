@@ -73,8 +73,12 @@ struct Variant {
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
     int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
-    int k2_fence = 0;         // K2 on ragged package batches with the fenced round (C2's), else the plain one
-    int k2_lane_c4 = 0;       // K2 with per-lane AES-128/192 keys in 4-block chunks (8: VGPR spills)
+    // K2 on ragged package batches with the fenced round (C2's): R1 wire send 919-930 -> 966-975,
+    // Q1 +1 % (profiles/r05/ab_k2_fence_c4)
+    int k2_fence = 1;
+    // K2 with per-lane AES-128/192 keys in 4-block chunks (8-block chunks spill 14-26 VGPRs):
+    // Q1s encrypt 559-560 -> 636-638 GiB/s (profiles/r05/ab_k2_fence_c4)
+    int k2_lane_c4 = 1;
     // tests only: the next poison_order ragged encrypts find their length-order block's
     // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
     int poison_order = 0;
