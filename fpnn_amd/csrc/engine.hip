@@ -532,8 +532,8 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     while (threads < kThreads && (uint64_t)threads * slots < b->count) threads *= 2;
     const uint64_t want = (b->count + threads - 1) / threads;
     const int grid = (int)(want < slots ? (want ? want : 1) : slots);
-    // (ragged batches: FPNN_AES_K2_ALIGN_RAGGED=0 drops the line-alignment singles, A/B --
-    // a few 16-B aligned frames per wave make the whole wave run their singles)
+    // (not for ragged batches by default, Variant::k2_align_ragged: a few 16-B aligned
+    // frames per wave made the whole wave run their singles)
     if (!b->len || e->variant.k2_align_ragged) k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;

@@ -79,7 +79,10 @@ struct Variant {
     // K2 with per-lane AES-128/192 keys in 4-block chunks (8-block chunks spill 14-26 VGPRs):
     // Q1s encrypt 559-560 -> 636-638 GiB/s (profiles/r05/ab_k2_fence_c4)
     int k2_lane_c4 = 1;
-    int k2_align_ragged = 1;  // K2 on ragged batches: line-alignment single blocks before the chunks
+    // K2 on ragged batches: line-alignment single blocks before the chunks.  Off: the few
+    // 16-B aligned frames of a wave made all its lanes wait out their singles -- Q1 encrypt
+    // 503-504 -> 705, Q1s 642-644 -> 741-753, R1 send equal (profiles/r05/ab_k2_align)
+    int k2_align_ragged = 0;
     // tests only: the next poison_order ragged encrypts find their length-order block's
     // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
     int poison_order = 0;
