@@ -534,7 +534,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     const int grid = (int)(want < slots ? (want ? want : 1) : slots);
     // (not for ragged batches by default, Variant::k2_align_ragged: a few 16-B aligned
     // frames per wave made the whole wave run their singles)
-    if (!b->len || e->variant.k2_align_ragged) k.flags |= F_ALIGN_CHUNKS;
+    if (b->len ? e->variant.k2_align_ragged : e->variant.k2_align) k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
     HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream,
@@ -729,6 +729,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_K2_FENCE")) e->variant.k2_fence = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_LANE_C4")) e->variant.k2_lane_c4 = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_ALIGN_RAGGED")) e->variant.k2_align_ragged = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_ALIGN")) e->variant.k2_align = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEBUG_POISON_ORDER")) e->variant.poison_order = std::max(0, atoi(v));
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;

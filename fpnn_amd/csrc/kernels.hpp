@@ -83,6 +83,7 @@ struct Variant {
     // 16-B aligned frames of a wave made all its lanes wait out their singles -- Q1 encrypt
     // 503-504 -> 705, Q1s 642-644 -> 741-753, R1 send equal (profiles/r05/ab_k2_align)
     int k2_align_ragged = 0;
+    int k2_align = 1;  // the same for batches without per-frame lengths (U1's 1472-B datagrams, A/B)
     // tests only: the next poison_order ragged encrypts find their length-order block's
     // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
     int poison_order = 0;
