@@ -471,7 +471,7 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     // balances Zipf-like lengths (C4 on K2: 88 GiB/s).
     const bool k2_ragged = b->len && !stream &&
                            ((e->variant.k2_ragged && b->count >= full_chip) ||
-                            (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= 4 * full_chip));
+                            (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= (uint64_t)e->variant.k2_short_min * full_chip));
     if ((b->count < coop_below || b->len != nullptr) && !k2_ragged) {
         const uint64_t lanes = 4 * b->count;
         int threads = 64;
@@ -726,6 +726,7 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_SHORT")) e->variant.k2_short = atoi(v) != 0;
+    if (const char *v = getenv("FPNN_AES_K2_SHORT_MIN")) e->variant.k2_short_min = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_K2_FENCE")) e->variant.k2_fence = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_LANE_C4")) e->variant.k2_lane_c4 = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_K2_ALIGN_RAGGED")) e->variant.k2_align_ragged = atoi(v) != 0;

@@ -305,13 +305,14 @@ def main():
         del a, b, r
         print(json.dumps({"U1": out["U1"]}), flush=True)
 
-    for qname in [q for q in ("Q1", "Q1g", "Q1s") if q in todo]:
+    for qname in [q for q in ("Q1", "Q1g", "Q1s", "Q1h") if q in todo]:
         # FPNN's typical quest frames (145 B: core/test/tcp-test/asyncStressClient.cpp:13-29)
         # from 16 384 connections, each with its own key and IV, as one collector flush would
         # pass them (ragged layout, slot per frame): 9 whole blocks and a 1-byte tail per
         # chain, so block 0 is a tenth of each chain (SURVEY section 0 point 3: E_k(IV))
         # (Q1s: the same as Q1 with FPNN's default 16-byte keys instead of reinforced 32)
-        P, L, NC = 2 << 20, 145, 16384
+        # (Q1h: a quarter of Q1's frames, 2 per GPU lane -- the K2 / K2h cut-over)
+        P, L, NC = (2 << 20) >> (2 if qname == "Q1h" else 0), 145, 16384
         kl = 16 if qname == "Q1s" else 32
         keys, ivs = W.many_keys(dict(W.U1, connections=NC, keylen=kl))
         ks = fpnn_amd.KeySet(eng, keys.tobytes(), kl, ivs.tobytes())
