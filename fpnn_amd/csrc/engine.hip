@@ -466,9 +466,10 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     const uint64_t coop_below = e->variant.coop_below < 0 ? full_chip : (uint64_t)e->variant.coop_below;
     // Ragged package batches of many short frames (the caller's max_len bound): one lane
     // per chain in grid-stride order (K2) -- Q1, 2 M x 145-B quests of 16 384 keyed
-    // connections: 491 against K2h's 343 GiB/s (its work-queue atomics and length-order
-    // indirection per chain; profiles/r05/ab_k2_short).  Without a bound K2h, which also
-    // balances Zipf-like lengths (C4 on K2: 88 GiB/s).
+    // connections: 705 against K2h's 343 GiB/s (its work-queue atomics and length-order
+    // indirection per chain; profiles/r05/ab_k2_short, ab_k2_align), from one chain per
+    // GPU lane on (Variant::k2_short_min).  Without a bound K2h, which also balances
+    // Zipf-like lengths (C4 on K2: 88 GiB/s).
     const bool k2_ragged = b->len && !stream &&
                            ((e->variant.k2_ragged && b->count >= full_chip) ||
                             (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= (uint64_t)e->variant.k2_short_min * full_chip));

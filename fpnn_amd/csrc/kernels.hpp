@@ -73,7 +73,9 @@ struct Variant {
     int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
     int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
     int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
-    int k2_short_min = 4;     // ... and the batch holds at least this many chains per GPU lane
+    // ... and the batch holds at least this many chains per GPU lane (4 until round 5's K2
+    // changes; Q1h, 2 per lane: K2h 182-184 vs K2 767-770 GiB/s, profiles/r05/ab_k2_short_min)
+    int k2_short_min = 1;
     // K2 on ragged package batches with the fenced round (C2's): R1 wire send 919-930 -> 966-975,
     // Q1 +1 % (profiles/r05/ab_k2_fence_c4)
     int k2_fence = 1;
