@@ -230,7 +230,7 @@ void encryptor_retire(uint64_t serial) {
 // like the table, so a flush never touches more than its own connections.  The table
 // belongs to one engine, identified by its id.
 // Key-table generations: an Encryptor caches (tag, slot) of the table it was last given a
-// slot in (Encryptor::_batchTag / _batchSlot); a table takes a new tag whenever it starts
+// slot in (Encryptor::_batchCache, one atomic word); a table takes a new tag whenever it starts
 // over, so no stale slot is ever used.  Flush ids mark the stream encryptors a flush lists.
 uint64_t next_batch_tag() {
     static std::atomic<uint64_t> n{1};
@@ -291,6 +291,10 @@ namespace {
 
 // A table past this many slots starts over whatever is live.
 constexpr uint32_t kTableMaxSlots = 1u << 20;
+// Encryptor::_batchCache = (table tag: 40 bits) << 24 | slot (24 bits)
+constexpr unsigned kCacheSlotBits = 24;
+constexpr uint64_t kCacheSlotMask = (1ull << kCacheSlotBits) - 1;
+constexpr uint64_t kCacheTagMask = (1ull << (64 - kCacheSlotBits)) - 1;
 
 }  // namespace
 
@@ -338,7 +342,8 @@ void EncryptorBatch::flush() {
         bool stream, encrypt, prefix;
         int nrounds;
         std::vector<size_t> idx;
-        std::vector<StreamEncryptor *> members;  // stream groups: each encryptor once, first use first
+        // stream groups: each encryptor once, first use first, with its position in idx
+        std::vector<std::pair<StreamEncryptor *, size_t>> members;
     };
     std::vector<Group> groups;
     static std::atomic<uint64_t> flush_ids{1};
@@ -352,14 +357,18 @@ void EncryptorBatch::flush() {
         const int nr = stream ? se->_ctx.nrounds : static_cast<PackageEncryptor *>(op.enc)->_ctx.nrounds;
         bool first = false;
         if (stream) {  // _batchSeen = flush id << 1 | direction
+            // StreamEncryptor::encrypt(std::string*) of "" does nothing (core/Encryptor.cpp:63-70):
+            // it is not grouped, so it must not mark the encryptor as listed either -- its
+            // first grouped op has to stage the stream's (iv, pos) and take the result back
+            const bool empty = op.buffer && op.buffer->empty();
             if ((se->_batchSeen >> 1) == fid) {
                 if ((se->_batchSeen & 1) != (uint64_t)op.encrypt)
                     throw EncryptorError("EncryptorBatch: a StreamEncryptor used in both directions in one batch");
-            } else {
+            } else if (!empty) {
                 se->_batchSeen = fid << 1 | (uint64_t)op.encrypt;
                 first = true;
             }
-            if (op.buffer && op.buffer->empty()) continue;  // StreamEncryptor::encrypt(std::string*) of ""
+            if (empty) continue;
         }
         if (!(g < groups.size() && groups[g].stream == stream && groups[g].encrypt == op.encrypt &&
               groups[g].prefix == prefix && groups[g].nrounds == nr)) {
@@ -369,8 +378,8 @@ void EncryptorBatch::flush() {
                 g++;
             if (g == groups.size()) groups.push_back({stream, op.encrypt, prefix, nr, {}, {}});
         }
+        if (first) groups[g].members.emplace_back(se, groups[g].idx.size());
         groups[g].idx.push_back(i);
-        if (first) groups[g].members.push_back(se);
     }
     for (const Group &gr : groups) {
         const double tg = bs.on ? BatchStats::now() : 0;
@@ -404,8 +413,9 @@ void EncryptorBatch::flush() {
             const uint32_t first_new = t.next;
             for (size_t k = 0; k < gr.idx.size(); k++) {
                 Encryptor *enc = ops[gr.idx[k]].enc;
-                if (enc->_batchTag == t.tag) {  // a connection this table already holds
-                    slots[k] = enc->_batchSlot;
+                const uint64_t c = enc->_batchCache.load(std::memory_order_relaxed);
+                if (c != 0 && (c >> kCacheSlotBits) == (t.tag & kCacheTagMask)) {  // a connection this table holds
+                    slots[k] = (uint32_t)(c & kCacheSlotMask);
                     continue;
                 }
                 auto ins = t.slot.emplace(enc->_serial, t.next);
@@ -418,8 +428,10 @@ void EncryptorBatch::flush() {
                     t.next++;
                 }
                 slots[k] = ins.first->second;
-                enc->_batchTag = t.tag;
-                enc->_batchSlot = slots[k];
+                // (slots past the 24-bit field are found through the map every time)
+                enc->_batchCache.store(slots[k] <= kCacheSlotMask
+                                           ? (t.tag & kCacheTagMask) << kCacheSlotBits | slots[k] : 0u,
+                                       std::memory_order_relaxed);
             }
             if (t.next > kTableMaxSlots && attempt == 0) {  // start over with this group's connections only
                 t.slot.clear();
@@ -486,18 +498,18 @@ void EncryptorBatch::flush() {
                 t.iv.resize(16 * (size_t)cnt);
                 t.pos.resize(cnt);
             }
-            for (const StreamEncryptor *se : gr.members) {  // the touched streams' current (iv, pos)
-                const uint32_t sl = se->_batchSlot;
-                memcpy(&t.iv[16 * (size_t)sl], se->_iv, 16);
-                t.pos[sl] = (uint32_t)se->_pos;
+            for (const auto &m : gr.members) {  // the touched streams' current (iv, pos)
+                const uint32_t sl = slots[m.second];
+                memcpy(&t.iv[16 * (size_t)sl], m.first->_iv, 16);
+                t.pos[sl] = (uint32_t)m.first->_pos;
             }
             rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                       t.iv.data(), t.pos.data());
             if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: stream batch: " + describe(rc));
-            for (StreamEncryptor *se : gr.members) {
-                const uint32_t sl = se->_batchSlot;
-                memcpy(se->_iv, &t.iv[16 * (size_t)sl], 16);
-                se->_pos = t.pos[sl];
+            for (const auto &m : gr.members) {
+                const uint32_t sl = slots[m.second];
+                memcpy(m.first->_iv, &t.iv[16 * (size_t)sl], 16);
+                m.first->_pos = t.pos[sl];
             }
         }
     }

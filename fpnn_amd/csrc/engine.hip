@@ -285,6 +285,8 @@ struct fpnn_aes_engine {
     hipStream_t map_stream = nullptr;  // host-mapped moves (both PCIe directions in one launch)
     const char *host_path = "";  // "host_staged" / "host_mapped": the last host-frame call's path
     std::unique_ptr<HostPool> pool;  // created on first use
+    // the address-audit build (audit.hpp): the extent table kernels check against
+    AuditTable *d_aud = nullptr;
     // instrumentation
     bool timing = false;
     const char *last_kernel[2] = {"", ""};  // base name of the last main kernel per direction
@@ -384,6 +386,18 @@ void batch_queued(fpnn_aes_engine *e);
 void register_engine(fpnn_aes_engine *e);
 void unregister_engine(fpnn_aes_engine *e);
 
+// batch_signal for the lifetime of a call: the pending flag that batch_signal sets (and
+// batch_queued clears once the kernels are queued) is cleared on EVERY exit, so a call
+// that returns an error between the two never leaves other engines' server relaunches
+// spinning out their batch_fence bound
+struct BatchScope {
+    fpnn_aes_engine *e;
+    explicit BatchScope(fpnn_aes_engine *eng) : e(eng) { batch_signal(e); }
+    ~BatchScope();
+    BatchScope(const BatchScope &) = delete;
+    BatchScope &operator=(const BatchScope &) = delete;
+};
+
 int timing_begin(fpnn_aes_engine *e, int which, EventPair **pair) {
     *pair = nullptr;
     if (!e->timing) return FPNN_AES_OK;
@@ -448,7 +462,114 @@ bool is_uniform_layout(const fpnn_aes_batch *b) {
 }
 
 
+#ifdef FPNN_AES_BOUNDS
+// ---- the address-audit build (audit.hpp, `make audit`) ----------------------------------
+// Before an encrypt call: the extents of every buffer the call's kernels may touch, in the
+// engine's table (synchronous; the audit build is a checker, not a product).  The scratch
+// the call grows is grown here first so that its extent is known.
+int audit_begin(fpnn_aes_engine *e, const fpnn_aes_batch *b, const uint8_t *iv_state, const uint32_t *pos_state,
+                KBatch &k) {
+    int rc;
+    if (!e->d_aud) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_aud), sizeof(AuditTable)));
+    if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
+    if ((rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
+    if (kLengthOrderWords > e->cap_buckets) {
+        if ((rc = grow(e, e->d_buckets, e->cap_buckets, kLengthOrderWords))) return rc;
+        HIP_TRY(hipMemsetAsync(e->d_buckets, 0, e->cap_buckets * sizeof(uint32_t), e->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    AuditTable t;
+    memset(&t, 0, sizeof t);
+    const uint64_t n = b->count;
+    auto set = [&](AuditBuf i, const void *p, uint64_t bytes) {
+        if (!p) return;
+        t.lo[i] = (uint64_t)(uintptr_t)p;
+        t.hi[i] = t.lo[i] + bytes;
+    };
+    set(AB_IN_OFF, b->in_off, 8 * n);
+    set(AB_OUT_OFF, b->out_off, 8 * n);
+    set(AB_LEN, b->len, 4 * n);
+    set(AB_SLOT, b->key_slot, 4 * n);
+    const uint64_t slots = std::max<uint64_t>(b->keys->count, b->keys->capacity);
+    set(AB_KEYS, b->keys->d_keys, sizeof(DevKey) * slots);
+    set(AB_EIV, b->keys->d_eiv, 16 * slots);
+    set(AB_IV_STATE, iv_state, 16 * n);
+    set(AB_POS_STATE, pos_state, 4 * n);
+    set(AB_POS_SNAP, pos_state, 4 * n);
+    set(AB_PERM, e->d_perm, 4 * n);
+    set(AB_SINK, e->d_sink, 16 * e->cap_sink);
+    set(AB_BLOCK, e->d_buckets, 4 * (uint64_t)kLengthOrderWords);
+    // the payload: the union of the segments' byte ranges (the kernels also check each
+    // access against its own segment)
+    std::vector<uint64_t> io(n), oo(n);
+    std::vector<uint32_t> ln(n);
+    if (b->in_off) HIP_TRY(hipMemcpy(io.data(), b->in_off, 8 * n, hipMemcpyDeviceToHost));
+    else for (uint64_t i = 0; i < n; i++) io[i] = i * b->stride;
+    if (b->out_off) HIP_TRY(hipMemcpy(oo.data(), b->out_off, 8 * n, hipMemcpyDeviceToHost));
+    else oo = io;
+    if (b->len) HIP_TRY(hipMemcpy(ln.data(), b->len, 4 * n, hipMemcpyDeviceToHost));
+    else std::fill(ln.begin(), ln.end(), b->uniform_len);
+    const uint64_t wire = (b->flags & FPNN_AES_F_WIRE_PREFIX) ? 4 : 0;
+    uint64_t ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ln[i]) {
+            ilo = std::min(ilo, io[i]);
+            ihi = std::max(ihi, io[i] + ln[i]);
+        }
+        if (ln[i] + wire) {
+            olo = std::min(olo, oo[i]);
+            ohi = std::max(ohi, oo[i] + ln[i] + wire);
+        }
+    }
+    if (ihi) set(AB_IN, b->in + ilo, ihi - ilo);
+    else set(AB_IN, b->in, 1);  // (nothing may be read)
+    if (ohi) set(AB_OUT, b->out + olo, ohi - olo);
+    else set(AB_OUT, b->out, 1);
+    // (the audit's own test: an `out` extent this many bytes short must be reported)
+    if (const char *v = getenv("FPNN_AES_AUDIT_SHRINK_OUT"))
+        if (t.hi[AB_OUT] > t.lo[AB_OUT] + (uint64_t)atoll(v)) t.hi[AB_OUT] -= (uint64_t)atoll(v);
+    HIP_TRY(hipMemcpy(e->d_aud, &t, sizeof t, hipMemcpyHostToDevice));
+    k.aud = e->d_aud;
+    return FPNN_AES_OK;
+}
+
+const char *audit_buf_name(uint32_t i) {
+    static const char *const names[kAuditBufs] = {"in", "out", "in_off", "out_off", "len", "key_slot", "keys", "eiv",
+                                                  "iv_state", "pos_state", "perm", "sink", "length-order block",
+                                                  "pos_snap", "in (outside its segment)", "out (outside its segment)"};
+    return i < kAuditBufs ? names[i] : "?";
+}
+
+// After the call's kernels: wait, and report the first access outside its extent.
+int audit_end(fpnn_aes_engine *e, int rc) {
+    if (rc != FPNN_AES_OK || !e->d_aud) return rc;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    AuditTable t;
+    HIP_TRY(hipMemcpy(&t, e->d_aud, sizeof t, hipMemcpyDeviceToHost));
+    if (!t.hits) return FPNN_AES_OK;
+    char buf[512];
+    snprintf(buf, sizeof buf,
+             "address audit: %u access(es) outside their extent; first: %s (%s) line %u, workgroup %u thread %u, "
+             "bytes [0x%llx, +%llu) against [0x%llx, 0x%llx)",
+             t.hits, last_launched(), audit_buf_name(t.buf), t.site, t.block, t.thread, (unsigned long long)t.addr,
+             (unsigned long long)t.len, (unsigned long long)t.elo, (unsigned long long)t.ehi);
+    g_last_error = buf;
+    fprintf(stderr, "[fpnn_aes audit] %s\n", buf);
+    return FPNN_AES_ERR_DEVICE;
+}
+#endif
+
+int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream);
+
 int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
+#ifdef FPNN_AES_BOUNDS
+    return audit_end(e, run_encrypt_calls(e, b, iv_state, pos_state, stream));
+#else
+    return run_encrypt_calls(e, b, iv_state, pos_state, stream);
+#endif
+}
+
+int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, uint32_t *pos_state, bool stream) {
     int rc = check_batch(e, b);
     if (rc) return rc;
     if (stream && b->count && (!iv_state || !pos_state || ((uintptr_t)iv_state & 15))) return FPNN_AES_ERR_ARG;
@@ -456,8 +577,11 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         return FPNN_AES_ERR_ARG;  // the 4-byte prefix needs a distinct output layout
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
-    batch_signal(e);
+    const BatchScope batch_scope(e);  // (an early return clears the pending flag)
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
+#ifdef FPNN_AES_BOUNDS
+    if ((rc = audit_begin(e, b, iv_state, pos_state, k))) return rc;
+#endif
     const Layout layout = is_uniform_layout(b) ? LAYOUT_UNIFORM : LAYOUT_GENERAL;
     const KeyMode km = (b->key_slot && b->keys->count > 1) ? KEY_LANE : KEY_UNIFORM;
     // Few chains (fewer than the lanes of a full chip) or ragged lengths: one quad per
@@ -484,6 +608,9 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
         // and K2c's grid stride is cheaper
         const bool hybrid = b->len && b->count > 1 && (lanes > full_chip || e->variant.hyb_force);
         uint32_t *block = nullptr;  // the length-order block (ragged batches)
+        // (everything that can fail is done before the length order is queued: its block is
+        // left dirty until its last reader runs)
+        if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
         if (b->len && b->count > 1) {  // ragged: visit the longest chains first, similar lengths per wave
             if ((rc = grow(e, e->d_perm, e->cap_perm, b->count))) return rc;
             if (kLengthOrderWords > e->cap_buckets) {  // starts zeroed; afterwards its last reader zeroes it
@@ -502,8 +629,10 @@ int run_encrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.perm = e->d_perm;
         }
         EventPair *ev;
-        if (hybrid && (rc = grow(e, e->d_sink, e->cap_sink, 2ull * e->num_cus * (kThreads / 64)))) return rc;
-        if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
+        if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) {
+            if (block) (void)hipMemsetAsync(block, 0, kLengthOrderWords * sizeof(uint32_t), e->stream);
+            return rc;
+        }
         if (hybrid) {  // K2h: one lane per chain, quads for the longest; one workgroup per CU
             k.flags |= F_ALIGN_CHUNKS;
             HybridArgs h;
@@ -551,7 +680,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (b->flags & FPNN_AES_F_WIRE_PREFIX) return FPNN_AES_ERR_ARG;
     if (!b->count) return FPNN_AES_OK;
     DeviceGuard g(e->device);
-    batch_signal(e);
+    const BatchScope batch_scope(e);  // (an early return clears the pending flag)
     KBatch k = make_kbatch(e, b, iv_state, pos_state);
     // small ragged batches: block map (+ stream snapshot) in one single-workgroup kernel
     const bool small_map = b->count <= block_map_small_max();
@@ -810,6 +939,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
         (void)hipMemPoolDestroy(e->mpool);
     }
     (void)hipFree(e->d_total);
+    if (e->d_aud) (void)hipFree(e->d_aud);
     if (e->h_fault) (void)hipHostFree(e->h_fault);
     (void)hipFree(e->d_stage);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -1169,7 +1299,7 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
     s.abs_off = e->d_fr_off;
     s.abs_slot = per_key ? e->d_fr_slot : nullptr;
     static_assert(sizeof(ScanResult) == sizeof(fpnn_aes_frame_scan), "scan layout");
-    batch_signal(e);
+    const BatchScope batch_scope(e);  // (an early return clears the pending flag)
     HIP_TRY(launch_scan_frames(s, false, e->num_cus, e->stream));
     batch_queued(e);
     // every frame slot is one package segment (unused ones have length 0)
@@ -1209,7 +1339,7 @@ int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
     s.frame_off = frame_off;
     s.frame_len = frame_len;
     s.scan = reinterpret_cast<ScanResult *>(scan);
-    batch_signal(e);
+    const BatchScope batch_scope(e);  // (an early return clears the pending flag)
     HIP_TRY(launch_scan_frames(s, true, e->num_cus, e->stream));
     batch_queued(e);
     return FPNN_AES_OK;
@@ -1347,6 +1477,8 @@ void batch_signal(fpnn_aes_engine *e) {
         __atomic_fetch_add(y + 16 * (e->device & 63), 1u, __ATOMIC_RELEASE);
     }
 }
+
+BatchScope::~BatchScope() { e->batch_pending.store(false, std::memory_order_release); }
 
 // Engines per device, for batch_fence.
 struct DeviceEngines {
@@ -3007,7 +3139,7 @@ int ecdh_launch(fpnn_aes_engine *e, int curve, const EccConst &c, const EcdhJob 
         return FPNN_AES_ERR_ARG;
     }
     DeviceGuard g(e->device);
-    batch_signal(e);
+    const BatchScope batch_scope(e);  // (an early return clears the pending flag)
     HIP_TRY(launch_ecdh(c, j, curve, e->stream));
     batch_queued(e);
     return FPNN_AES_OK;

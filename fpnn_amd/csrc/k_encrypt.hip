@@ -40,7 +40,9 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
     uint32_t rk_slot = ~0u;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
         const Seg g = get_seg<LAYOUT>(b, s);
-        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
+                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
+        const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
         if (KM == KEY_UNIFORM) {
             rk = rku;
         } else if (g.slot != rk_slot) {
@@ -48,13 +50,13 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             rk_slot = g.slot;
         }
         uint4 eiv = eiv_u;
-        if (kFirst && KM != KEY_UNIFORM && use_eiv) eiv = b.eiv[g.slot];
+        if (kFirst && KM != KEY_UNIFORM && use_eiv) eiv = *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
 
         uint4 iv;
         uint32_t n = 0;
         if (STREAM) {
-            iv = ld_state_iv(b.iv_state + 16 * s);
-            n = b.pos_state[s];
+            iv = ld_state_iv(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16));
+            n = *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4);
         } else {
             iv = *reinterpret_cast<const uint4 *>(key->iv);
         }
@@ -63,18 +65,19 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         uint32_t rem = g.len;
 
         if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
-            q[0] = (uint8_t)rem;
-            q[1] = (uint8_t)(rem >> 8);
-            q[2] = (uint8_t)(rem >> 16);
-            q[3] = (uint8_t)(rem >> 24);
+            uint8_t *qp = FA_RG(b, AB_OUT, q, 0, 4, a_olo, a_ohi);
+            qp[0] = (uint8_t)rem;
+            qp[1] = (uint8_t)(rem >> 8);
+            qp[2] = (uint8_t)(rem >> 16);
+            qp[3] = (uint8_t)(rem >> 24);
             q += 4;
         }
 
         if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
             const uint32_t take = rem < 16 - n ? rem : 16 - n;
             const int lo = (int)n, hi = (int)(n + take);
-            const uint4 o = load_bytes(p - n, lo, hi) ^ iv;
-            store_bytes(q - n, o, lo, hi);
+            const uint4 o = load_bytes(FA_RG(b, AB_IN, p - n, lo, hi, a_ilo, a_ihi), lo, hi) ^ iv;
+            store_bytes(FA_RG(b, AB_OUT, q - n, lo, hi, a_olo, a_ohi), o, lo, hi);
             iv = select_bytes(byte_mask(lo, hi), o, iv);
             p += take;
             q += take;
@@ -95,8 +98,9 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             uint32_t h = (mis & 15u) ? 0u : ((128u - mis) & 127u) >> 4;
             h = h < nfull ? h : nfull;
             for (; i < h; i++) {
-                iv = (use_eiv && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ load16(p);
-                store16(q, iv);
+                iv = (use_eiv && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^
+                     load16(FA_SEG(b, AB_IN, p, 16, a_ilo, a_ihi));
+                store16(FA_SEG(b, AB_OUT, q, 16, a_olo, a_ohi), iv);
                 p += 16;
                 q += 16;
             }
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
             // and the conservative waits below, measured 1.3 % slower.)
             uint4 a[C];
 #pragma unroll
-            for (int j = 0; j < C; j++) a[j] = load16(p + 16 * j);
+            for (int j = 0; j < C; j++) a[j] = load16(FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi));
             for (; i + C <= nfull; i += C) {
                 // the next chunk's loads, unconditional (the last chunk reads the first
                 // DevKey's 128+ bytes, an L2 hit, not its own chunk again: that cost C2 an
@@ -121,7 +125,8 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
                 const uint8_t *pn = more ? p + 16 * C : reinterpret_cast<const uint8_t *>(b.keys);
                 uint4 nx[C];
 #pragma unroll
-                for (int j = 0; j < C; j++) nx[j] = load16(pn + 16 * j);
+                for (int j = 0; j < C; j++)
+                    nx[j] = load16(more ? FA_SEG(b, AB_IN, pn + 16 * j, 16, a_ilo, a_ihi) : FA_AT(b, AB_KEYS, pn + 16 * j, 16));
 #pragma unroll
                 for (int j = 0; j < C; j++) {
                     uint4 ks;
@@ -133,18 +138,18 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
                     a[j] = iv;
                 }
 #pragma unroll
-                for (int j = 0; j < C; j++) store16(q + 16 * j, a[j]);
+                for (int j = 0; j < C; j++) store16(FA_SEG(b, AB_OUT, q + 16 * j, 16, a_olo, a_ohi), a[j]);
 #pragma unroll
                 for (int j = 0; j < C; j++) a[j] = nx[j];
                 p += 16 * C;
                 q += 16 * C;
             }
         }
-        uint4 pt = i < nfull ? load16(p) : make_uint4(0, 0, 0, 0);
+        uint4 pt = i < nfull ? load16(FA_SEG(b, AB_IN, p, 16, a_ilo, a_ihi)) : make_uint4(0, 0, 0, 0);
         for (; i < nfull; i++) {
-            const uint4 pn = (i + 1 < nfull) ? load16(p + 16) : make_uint4(0, 0, 0, 0);  // prefetch
+            const uint4 pn = (i + 1 < nfull) ? load16(FA_SEG(b, AB_IN, p + 16, 16, a_ilo, a_ihi)) : make_uint4(0, 0, 0, 0);  // prefetch
             iv = (use_eiv && i == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T)) ^ pt;  // C_i = P_i ^ E(C_{i-1})
-            store16(q, iv);
+            store16(FA_SEG(b, AB_OUT, q, 16, a_olo, a_ohi), iv);
             pt = pn;
             p += 16;
             q += 16;
@@ -152,14 +157,14 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
         rem &= 15u;
         if (rem) {  // partial final block: ivec = E(C) with the first rem bytes replaced
             const uint4 ks = use_eiv && nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, rk, T);
-            const uint4 o = load_bytes(p, 0, (int)rem) ^ ks;
-            store_bytes(q, o, 0, (int)rem);
+            const uint4 o = load_bytes(FA_RG(b, AB_IN, p, 0, rem, a_ilo, a_ihi), 0, (int)rem) ^ ks;
+            store_bytes(FA_RG(b, AB_OUT, q, 0, rem, a_olo, a_ohi), o, 0, (int)rem);
             iv = select_bytes(byte_mask(0, (int)rem), o, ks);
             n = rem;
         }
         if (STREAM) {
-            *reinterpret_cast<uint4 *>(b.iv_state + 16 * s) = iv;
-            b.pos_state[s] = n;
+            *reinterpret_cast<uint4 *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16)) = iv;
+            *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4) = n;
         }
     }
 }
@@ -183,9 +188,11 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 
     const uint64_t nquads = ((uint64_t)gridDim.x * blockDim.x) >> 2;
     for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; t < b.count; t += nquads) {
-        const uint64_t s = b.perm ? min(b.perm[t], (uint32_t)b.count - 1u) : t;  // longest chains first (ragged batches)
+        const uint64_t s = b.perm ? min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u) : t;  // longest chains first (ragged batches)
         const Seg g = get_seg<LAYOUT>(b, s);
-        const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+        FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
+                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
+        const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
         uint32_t rkq[NR + 1];
 #pragma unroll
         for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
@@ -197,17 +204,18 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const bool use_eiv = !STREAM && b.eiv != nullptr;
         uint32_t ew = 0;  // this lane's word of E_k(IV)
         if (STREAM) {
-            iv = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
-            n = b.pos_state[s];
+            iv = reinterpret_cast<const uint32_t *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16))[q];
+            n = *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4);
         } else {
             iv = reinterpret_cast<const uint32_t *>(key->iv)[q];
-            if (use_eiv) ew = reinterpret_cast<const uint32_t *>(b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot))[q];
+            if (use_eiv)
+                ew = reinterpret_cast<const uint32_t *>(FA_AT(b, AB_EIV, b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot), 16))[q];
         }
         const uint8_t *p = g.in;
         uint8_t *o = g.out;
         uint32_t rem = g.len;
         if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
-            if (q == 0) store_word_bytes(o, rem, 0, 4);
+            if (q == 0) store_word_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), rem, 0, 4);
             o += 4;
         }
         const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
@@ -215,8 +223,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint32_t take = rem < 16 - n ? rem : 16 - n;
             const int lo = max((int)n, wlo) - wlo, hi = min((int)(n + take), wlo + 4) - wlo;
             if (lo < hi) {
-                const uint32_t c = load_word_bytes(p - n + wlo, lo, hi) ^ iv;
-                store_word_bytes(o - n + wlo, c, lo, hi);
+                const uint32_t c = load_word_bytes(FA_RG(b, AB_IN, p - n + wlo, lo, hi, a_ilo, a_ihi), lo, hi) ^ iv;
+                store_word_bytes(FA_RG(b, AB_OUT, o - n + wlo, lo, hi, a_olo, a_ohi), c, lo, hi);
                 const uint32_t m = word_mask(lo, hi);
                 iv = (c & m) | (iv & ~m);
             }
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         if (nfull >= CH) {
             uint32_t a[CH];
 #pragma unroll
-            for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(p + 16 * j + wlo);
+            for (int j = 0; j < CH; j++) a[j] = *reinterpret_cast<const uint32_u *>(FA_SEG(b, AB_IN, p + 16 * j + wlo, 4, a_ilo, a_ihi));
             // the chain carries C ^ rk[0] (aes_chain_column: its two XORs folded into the keys)
             const uint32_t rkx = rkq[NR] ^ rkq[0];
             uint32_t sw = iv ^ rkq[0];
@@ -244,7 +252,9 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 const uint8_t *pn = (more ? p + 16 * CH : reinterpret_cast<const uint8_t *>(b.keys)) + wlo;
                 uint32_t nx[CH], c[CH];
 #pragma unroll
-                for (int j = 0; j < CH; j++) nx[j] = *reinterpret_cast<const uint32_u *>(pn + 16 * j);
+                for (int j = 0; j < CH; j++)
+                    nx[j] = *reinterpret_cast<const uint32_u *>(more ? FA_SEG(b, AB_IN, pn + 16 * j, 4, a_ilo, a_ihi)
+                                                                      : FA_AT(b, AB_KEYS, pn + 16 * j, 4));
 #pragma unroll
                 for (int j = 0; j < CH; j++) {
                     if (j == 0 && use_eiv && i == 0)  // the chain's first block (quad-uniform)
@@ -260,7 +270,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 #pragma unroll
                 for (int j = 0; j < CH; j++) asm volatile("" : "+v"(c[j]));
 #pragma unroll
-                for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(o + 16 * j + wlo) = c[j];
+                for (int j = 0; j < CH; j++) *reinterpret_cast<uint32_u *>(FA_SEG(b, AB_OUT, o + 16 * j + wlo, 4, a_olo, a_ohi)) = c[j];
                 // the loaded words are handed on here, after the rounds: without this the
                 // register allocator moved each nx[j] into a round's registers as soon as it
                 // could, waiting (vmcnt) for loads issued one block earlier
@@ -274,9 +284,9 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             }
         }
         for (; i < nfull; i++) {
-            const uint32_t pt = *reinterpret_cast<const uint32_u *>(p + wlo);
+            const uint32_t pt = *reinterpret_cast<const uint32_u *>(FA_SEG(b, AB_IN, p + wlo, 4, a_ilo, a_ihi));
             iv = (use_eiv && i == 0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T)) ^ pt;
-            *reinterpret_cast<uint32_u *>(o + wlo) = iv;
+            *reinterpret_cast<uint32_u *>(FA_SEG(b, AB_OUT, o + wlo, 4, a_olo, a_ohi)) = iv;
             p += 16;
             o += 16;
         }
@@ -285,8 +295,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint32_t ks = use_eiv && nfull == 0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T);
             const int lo = 0, hi = min((int)rem, wlo + 4) - wlo;
             if (hi > lo) {
-                const uint32_t c = load_word_bytes(p + wlo, lo, hi) ^ ks;
-                store_word_bytes(o + wlo, c, lo, hi);
+                const uint32_t c = load_word_bytes(FA_RG(b, AB_IN, p + wlo, lo, hi, a_ilo, a_ihi), lo, hi) ^ ks;
+                store_word_bytes(FA_RG(b, AB_OUT, o + wlo, lo, hi, a_olo, a_ohi), c, lo, hi);
                 const uint32_t m = word_mask(lo, hi);
                 iv = (c & m) | (ks & ~m);
             } else {
@@ -295,8 +305,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             n = rem;
         }
         if (STREAM) {
-            reinterpret_cast<uint32_t *>(b.iv_state + 16 * s)[q] = iv;
-            if (q == 0) b.pos_state[s] = n;
+            reinterpret_cast<uint32_t *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16))[q] = iv;
+            if (q == 0) *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4) = n;
         }
     }
 }

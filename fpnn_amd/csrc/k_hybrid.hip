@@ -109,6 +109,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint8_t *p = nullptr;
         uint8_t *o = nullptr;
         uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
         // SHIFT state: d = o & 15; the funnel's rotation kl, sources (fl, fh) and
         // byte offset r; pl / ph = the rotated words of the previous raw block, praw its
         // own word; pv / lo0 as in the lane session
@@ -133,23 +134,28 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 16 readable bytes
         uint8_t *const sinkw = reinterpret_cast<uint8_t *>(h.sink + 2 * ((uint64_t)blockIdx.x * (kThreads / 64) + wave));
         auto begin = [&](uint64_t t) {
-            const uint64_t s = min(b.perm[t], (uint32_t)b.count - 1u);  // (in range even from a bad block)
+            const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
-            const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+            FA_SET(a_ilo, (uintptr_t)g.in);
+            FA_SET(a_ihi, (uintptr_t)g.in + g.len);
+            FA_SET(a_olo, (uintptr_t)g.out);
+            FA_SET(a_ohi, (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
+            const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
             if (KM != KEY_UNIFORM) {
 #pragma unroll
                 for (int r = 0; r <= NR; r++) rkq[r] = key->rk[4 * r + q];
             }
             uint32_t v, pos;
             if (STREAM) {
-                v = reinterpret_cast<const uint32_t *>(b.iv_state + 16 * s)[q];
-                pos = b.pos_state[s];
+                v = reinterpret_cast<const uint32_t *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16))[q];
+                pos = *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4);
             } else {
                 v = reinterpret_cast<const uint32_t *>(key->iv)[q];
                 pos = 0;
                 at0 = true;
-                if (b.eiv) ew = reinterpret_cast<const uint32_t *>(b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot))[q];
+                if (b.eiv)
+                    ew = reinterpret_cast<const uint32_t *>(FA_AT(b, AB_EIV, b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot), 16))[q];
             }
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             uint32_t pw = 0;  // (SHIFT) this lane's word of the 16 bytes before the body
             pv = 0;
             if (!STREAM && (b.flags & F_WIRE_PREFIX)) {  // htole32(len) ‖ ciphertext (core/Encryptor.cpp:47-48)
-                if (q == 0) store_word_bytes(oo, rem, 0, 4);
+                if (q == 0) store_word_bytes(FA_RG(b, AB_OUT, oo, 0, 4, a_olo, a_ohi), rem, 0, 4);
                 oo += 4;
                 pw = q == 3 ? rem : 0u;
                 pv = 4;
@@ -166,8 +172,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 const uint32_t take = rem < 16 - pos ? rem : 16 - pos;
                 const int lo = max((int)pos, wlo) - wlo, hi = min((int)(pos + take), wlo + 4) - wlo;
                 if (lo < hi) {
-                    const uint32_t c = load_word_bytes(pp - pos + wlo, lo, hi) ^ v;
-                    store_word_bytes(oo - pos + wlo, c, lo, hi);
+                    const uint32_t c = load_word_bytes(FA_RG(b, AB_IN, pp - pos + wlo, lo, hi, a_ilo, a_ihi), lo, hi) ^ v;
+                    store_word_bytes(FA_RG(b, AB_OUT, oo - pos + wlo, lo, hi, a_olo, a_ohi), c, lo, hi);
                     const uint32_t m = word_mask(lo, hi);
                     v = (c & m) | (v & ~m);
                 }
@@ -211,20 +217,22 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 if (hv) {  // the held words of the last step
 #pragma unroll
                     for (int j = 0; j < 8; j++)
-                        if (j >= (int)jt && j < (int)hk) *reinterpret_cast<uint32_t *>(hdst + 16 * j) = held[j];
+                        if (j >= (int)jt && j < (int)hk)
+                            *FA_SEG(b, AB_OUT, reinterpret_cast<uint32_t *>(hdst + 16 * j), 4, a_olo, a_ohi) = held[j];
                     hv = false;
                 }
                 // bytes [16 - k, 16) of the last raw block end at o
                 const uint32_t k = d < pv ? d : pv;
                 const int lo = (int)(16u - k) - wlo;
-                if (k && lo < 4) store_word_bytes(o - 16 + wlo, praw, lo > 0 ? lo : 0, 4);
+                if (k && lo < 4)
+                    store_word_bytes(FA_RG(b, AB_OUT, o - 16 + wlo, lo > 0 ? lo : 0, 4, a_olo, a_ohi), praw, lo > 0 ? lo : 0, 4);
             }
             if (tail) {
                 const uint32_t ks = !STREAM && b.eiv && at0 ? ew : aes_encrypt_column<NR, NT>(iv, rkq, T);
                 const int hi = min((int)tail, wlo + 4) - wlo;
                 if (hi > 0) {
-                    const uint32_t c = load_word_bytes(p + wlo, 0, hi) ^ ks;
-                    store_word_bytes(o + wlo, c, 0, hi);
+                    const uint32_t c = load_word_bytes(FA_RG(b, AB_IN, p + wlo, 0, hi, a_ilo, a_ihi), 0, hi) ^ ks;
+                    store_word_bytes(FA_RG(b, AB_OUT, o + wlo, 0, hi, a_olo, a_ohi), c, 0, hi);
                     const uint32_t m = word_mask(0, hi);
                     iv = (c & m) | (ks & ~m);
                 } else {
@@ -233,8 +241,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 n = tail;
             }
             if (STREAM) {
-                reinterpret_cast<uint32_t *>(b.iv_state + 16 * sid)[q] = iv;
-                if (q == 0) b.pos_state[sid] = n;
+                reinterpret_cast<uint32_t *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * sid, 16))[q] = iv;
+                if (q == 0) *FA_AT(b, AB_POS_STATE, b.pos_state + sid, 4) = n;
             }
         };
         // Tickets: the wave's quads that need a chain take consecutive ones with one atomic,
@@ -259,7 +267,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             if (need) {
                 const uint32_t leader = (uint32_t)__builtin_ctzll(need);
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&h.ctr[0], (uint32_t)__builtin_popcountll(need));
+                if (lane == leader) base = atomicAdd(FA_AT(b, AB_BLOCK, &h.ctr[0], 4), (uint32_t)__builtin_popcountll(need));
                 base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
                 if (!active && !exhausted) {
                     const uint64_t below = need & ((1ull << (lane & ~3u)) - 1ull);  // needing quads before mine
@@ -287,12 +295,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             if (__builtin_amdgcn_ballot_w64(fresh) != 0) {  // chains that start: their first words
 #pragma unroll
                 for (int j = 0; j < 8; j++)
-                    if (fresh) a[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk ? p + 16 * j + wlo : dummy + wlo);
+                    if (fresh)
+                        a[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk ? FA_SEG(b, AB_IN, p + 16 * j + wlo, 4, a_ilo, a_ihi)
+                                                                                : FA_AT(b, AB_KEYS, dummy + wlo, 4));
                 __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), inside the rare branch
             }
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                nx[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk2 ? p + 16 * (kk + j) + wlo : dummy + wlo);
+                nx[j] = *reinterpret_cast<const uint32_u *>(j < (int)kk2 ? FA_SEG(b, AB_IN, p + 16 * (kk + j) + wlo, 4, a_ilo, a_ihi)
+                                                                          : FA_AT(b, AB_KEYS, dummy + wlo, 4));
             // the rounds and the stores; FUN: the in-quad funnel (wire bodies off the 4-byte
             // grid somewhere in the batch), else block words are output words
             uint8_t *const dst = o - d + wlo;
@@ -334,7 +345,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                     for (int j = 0; j < 8; j++) {
                         const bool now = j < (int)jt;
                         const bool st = now ? j < (int)kk && !(j == 0 && head) : hv && kk != 0;
-                        *reinterpret_cast<uint32_t *>(st ? (now ? dst : hdst) + 16 * j : sinkw + wlo) = now ? a[j] : held[j];
+                        *reinterpret_cast<uint32_t *>(st ? FA_SEG(b, AB_OUT, (now ? dst : hdst) + 16 * j, 4, a_olo, a_ohi)
+                                                          : FA_AT(b, AB_SINK, sinkw + wlo, 4)) = now ? a[j] : held[j];
                     }
 #pragma unroll
                     for (int j = 0; j < 8; j++) held[j] = j >= (int)jt ? a[j] : held[j];
@@ -346,14 +358,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 } else {
 #pragma unroll
                     for (int j = 0; j < 8; j++)
-                        *reinterpret_cast<uint32_u *>(j < (int)kk ? dst + 16 * j : sinkw + wlo) = a[j];
+                        *reinterpret_cast<uint32_u *>(j < (int)kk ? FA_SEG(b, AB_OUT, dst + 16 * j, 4, a_olo, a_ohi)
+                                                                  : FA_AT(b, AB_SINK, sinkw + wlo, 4)) = a[j];
                 }
             };
             if (SHIFT && !wm) body(std::true_type{});
             else body(std::false_type{});
             if (SHIFT && __builtin_amdgcn_ballot_w64(head) != 0) {
                 const int lo = (int)lo0 - wlo;
-                if (head && lo < 4) store_word_bytes(dst, a[0], lo > 0 ? lo : 0, 4);
+                if (head && lo < 4) store_word_bytes(FA_RG(b, AB_OUT, dst, lo > 0 ? lo : 0, 4, a_olo, a_ohi), a[0], lo > 0 ? lo : 0, 4);
                 __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), inside the rare branch
             }
             if (SHIFT && kk) {
@@ -382,6 +395,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         // prev that are this chain's own output (rewritable); lo0 = first byte of the
         // chain's first slot that this chain may write
         uint32_t nfull = 0, tail = 0, n = 0, d = 0, pv = 0, lo0 = 0;
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
         uint4 iv = make_uint4(0, 0, 0, 0), prev = make_uint4(0, 0, 0, 0);
         bool valid = false, exhausted = false, fresh = false;
         bool at0 = false;                     // package mode: no block of the chain ciphered yet
@@ -396,19 +410,23 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             return KM == KEY_UNIFORM ? aes_encrypt_block<NR, NT>(x, rku, T) : aes_encrypt_block<NR, NT>(x, rkl, T);
         };
         auto begin = [&](uint64_t t) {
-            const uint64_t s = min(b.perm[t], (uint32_t)b.count - 1u);  // (in range even from a bad block)
+            const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
-            const DevKey *key = b.keys + (KM == KEY_UNIFORM ? 0u : g.slot);
+            FA_SET(a_ilo, (uintptr_t)g.in);
+            FA_SET(a_ihi, (uintptr_t)g.in + g.len);
+            FA_SET(a_olo, (uintptr_t)g.out);
+            FA_SET(a_ohi, (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
+            const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
             if (KM != KEY_UNIFORM) rkl = load_round_keys<NR>(key);
             if (STREAM) {
-                iv = ld_state_iv(b.iv_state + 16 * s);
-                n = b.pos_state[s];
+                iv = ld_state_iv(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * s, 16));
+                n = *FA_AT(b, AB_POS_STATE, b.pos_state + s, 4);
             } else {
                 iv = *reinterpret_cast<const uint4 *>(key->iv);
                 n = 0;
                 at0 = true;
-                if (b.eiv) eivl = b.eiv[KM == KEY_UNIFORM ? 0u : g.slot];
+                if (b.eiv) eivl = *FA_AT(b, AB_EIV, b.eiv + (KM == KEY_UNIFORM ? 0u : g.slot), 16);
             }
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
@@ -416,15 +434,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             pv = 0;
             if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
                 prev = make_uint4(0u, 0u, 0u, rem);  // the prefix = the 4 output bytes before the body
-                store_bytes(oo - 12, prev, 12, 16);
+                store_bytes(FA_RG(b, AB_OUT, oo - 12, 12, 16, a_olo, a_ohi), prev, 12, 16);
                 oo += 4;
                 pv = 4;
             }
             if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
                 const uint32_t take = rem < 16 - n ? rem : 16 - n;
                 const int lo = (int)n, hi = (int)(n + take);
-                const uint4 c = load_bytes(pp - n, lo, hi) ^ iv;
-                store_bytes(oo - n, c, lo, hi);
+                const uint4 c = load_bytes(FA_RG(b, AB_IN, pp - n, lo, hi, a_ilo, a_ihi), lo, hi) ^ iv;
+                store_bytes(FA_RG(b, AB_OUT, oo - n, lo, hi, a_olo, a_ohi), c, lo, hi);
                 iv = select_bytes(byte_mask(lo, hi), c, iv);
                 pp += take;
                 oo += take;
@@ -457,16 +475,16 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 }
                 if (fin) {
                     const uint32_t k = d < pv ? d : pv;
-                    if (SHIFT && k) store_bytes(o - 16, prev, (int)(16 - k), 16);
+                    if (SHIFT && k) store_bytes(FA_RG(b, AB_OUT, o - 16, 16 - k, 16, a_olo, a_ohi), prev, (int)(16 - k), 16);
                     if (tail) {
-                        const uint4 c = load_bytes(p, 0, (int)tail) ^ ks;
-                        store_bytes(o, c, 0, (int)tail);
+                        const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
+                        store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
                         iv = select_bytes(byte_mask(0, (int)tail), c, ks);
                         n = tail;
                     }
                     if (STREAM) {
-                        *reinterpret_cast<uint4 *>(b.iv_state + 16 * sid) = iv;
-                        b.pos_state[sid] = n;
+                        *reinterpret_cast<uint4 *>(FA_AT(b, AB_IV_STATE, b.iv_state + 16 * sid, 16)) = iv;
+                        *FA_AT(b, AB_POS_STATE, b.pos_state + sid, 4) = n;
                     }
                     valid = false;
                 }
@@ -476,7 +494,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             if (need) {
                 const uint32_t leader = (uint32_t)__builtin_ctzll(need);
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&h.ctr[1], (uint32_t)__builtin_popcountll(need));
+                if (lane == leader) base = atomicAdd(FA_AT(b, AB_BLOCK, &h.ctr[1], 4), (uint32_t)__builtin_popcountll(need));
                 base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
                 if (!valid && !exhausted) {
                     const uint64_t t = n_long + base + lane_rank(need);
@@ -498,12 +516,12 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             constexpr bool PF = !(KM == KEY_LANE && NR >= 12);
             if (fresh || !PF) {
 #pragma unroll
-                for (int j = 0; j < CH; j++) a[j] = j < (int)kk ? load16(p + 16 * j) : a[j];
+                for (int j = 0; j < CH; j++) a[j] = j < (int)kk ? load16(FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)) : a[j];
             }
             if (PF) {
 #pragma unroll
                 for (int j = 0; j < CH; j++)
-                    if (j < (int)kk2) nx[j] = load16(p + 16 * (kk + j));
+                    if (j < (int)kk2) nx[j] = load16(FA_SEG(b, AB_IN, p + 16 * (kk + j), 16, a_ilo, a_ihi));
             }
             // every lane that ciphers a block this step is at its chain's block 0: the wave
             // takes that block's keystream from the key set (a lane at block 0 would compute
@@ -518,7 +536,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 }
 #pragma unroll
                 for (int j = 0; j < CH; j++)
-                    if (j < (int)kk) store16(o + 16 * j, a[j]);
+                    if (j < (int)kk) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
             } else {
                 // each block's output slot is assembled as soon as the block is ciphered
                 // (only the last raw block, prev, stays live), then the slots go out back
@@ -537,8 +555,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 for (int j = 0; j < CH; j++) {
                     if (j < (int)kk) {
                         uint8_t *dst = o - d + 16 * j;
-                        if (j == 0 && lo0 != 0) store_bytes(dst, a[j], (int)lo0, 16);
-                        else store16(dst, a[j]);
+                        if (j == 0 && lo0 != 0) store_bytes(FA_RG(b, AB_OUT, dst, lo0, 16, a_olo, a_ohi), a[j], (int)lo0, 16);
+                        else store16(FA_SEG(b, AB_OUT, dst, 16, a_olo, a_ohi), a[j]);
                     }
                 }
                 if (kk) {

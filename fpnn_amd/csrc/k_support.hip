@@ -289,8 +289,8 @@ __device__ __forceinline__ void tile_buckets(const KBatch &b, uint64_t tile0, ui
 #pragma unroll
     for (int i = 0; i < kBucketItems; i++) {
         const uint64_t s = tile0 + 256ull * i, sc = s < b.count ? s : b.count - 1;
-        L[i] = lens[sc];
-        P[i] = STREAM ? b.pos_snap[sc] : 0u;
+        L[i] = *FA_AT(b, AB_LEN, lens + sc, 4);
+        P[i] = STREAM ? *FA_AT(b, AB_POS_SNAP, b.pos_snap + sc, 4) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < kBucketItems; i++)
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
 #pragma unroll
         for (int i = 0; i < kBucketItems; i++) {
             const uint64_t s = tile0 + 256ull * i, sc = s < b.count ? s : b.count - 1;
-            O[i] = op ? op[sc] : sc * b.stride;
+            O[i] = op ? *FA_AT(b, b.out_off ? AB_OUT_OFF : AB_IN_OFF, op + sc, 8) : sc * b.stride;
         }
 #pragma unroll
         for (int i = 0; i < kBucketItems; i++) mis |= (uint32_t)((uintptr_t)b.out + O[i]) & 3u;
@@ -325,8 +325,8 @@ __global__ __launch_bounds__(256) void k_bucket_count(KBatch b, uint32_t *counts
     }
     if (mis) off4 = 1;
     __syncthreads();
-    if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
-    if (threadIdx.x == 0 && off4) atomicOr(&counts[kWireFlagWord], 1u);
+    if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(FA_AT(b, AB_BLOCK, &counts[threadIdx.x], 4), h[threadIdx.x]);
+    if (threadIdx.x == 0 && off4) atomicOr(FA_AT(b, AB_BLOCK, &counts[kWireFlagWord], 4), 1u);
 }
 
 __global__ __launch_bounds__(kBuckets) void k_bucket_scan(uint32_t *counts, uint32_t *cursor, uint64_t count,
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *curs
     }
     __syncthreads();
     if (threadIdx.x < kBuckets) {
-        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]) : 0u;
+        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(FA_AT(b, AB_BLOCK, &cursor[threadIdx.x], 4), cnt[threadIdx.x]) : 0u;
         cnt[threadIdx.x] = 0;
     }
     __syncthreads();
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(KBatch b, uint32_t *curs
         const uint32_t k = live ? kb[i] : 0u;
         const uint32_t slot = bucket_add(cnt, k, live);
         const uint32_t at = base[k] + slot;
-        if (live && at < b.count) perm[at] = (uint32_t)(tile0 + 256ull * i);  // (past it: a bad block, see scan)
+        if (live && at < b.count) *FA_AT(b, AB_PERM, perm + at, 4) = (uint32_t)(tile0 + 256ull * i);  // (past it: a bad block, see scan)
     }
     if (release) length_order_release(release);  // K2c follows: nothing reads the block again
 }

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "aes_common.hpp"
+#include "audit.hpp"
 
 namespace fpnn_aes {
 
@@ -45,6 +46,8 @@ struct KBatch {
     // package mode: E_k(IV) per key slot (the first keystream block of every chain of the
     // slot, fpnn_aes_keyset.d_eiv), or null (then computed)
     const uint4 *eiv;
+    // the address-audit build's extent table (audit.hpp; null in the product build)
+    AuditTable *aud;
 };
 
 // UNIFORM: segment i at i*stride, uniform_len bytes, key slot 0.  FULL: the same with

@@ -34,12 +34,12 @@ __device__ __forceinline__ Seg get_seg(const KBatch &b, uint64_t s) {
         g.len = b.uniform_len;
         g.slot = 0;
     } else {
-        const uint64_t io = b.in_off ? b.in_off[s] : s * b.stride;
-        const uint64_t oo = b.out_off ? b.out_off[s] : io;
+        const uint64_t io = b.in_off ? *FA_AT(b, AB_IN_OFF, b.in_off + s, 8) : s * b.stride;
+        const uint64_t oo = b.out_off ? *FA_AT(b, AB_OUT_OFF, b.out_off + s, 8) : io;
         g.in = b.in + io;
         g.out = b.out + oo;
-        g.len = b.len ? b.len[s] : b.uniform_len;
-        g.slot = b.key_slot ? b.key_slot[s] : 0u;
+        g.len = b.len ? *FA_AT(b, AB_LEN, b.len + s, 4) : b.uniform_len;
+        g.slot = b.key_slot ? *FA_AT(b, AB_SLOT, b.key_slot + s, 4) : 0u;
     }
     return g;
 }

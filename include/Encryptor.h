@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <stdexcept>
 #include <string>
 
@@ -53,12 +54,14 @@ protected:
     size_t _keyLen;
     uint64_t _serial;
     // EncryptorBatch bookkeeping: the subclass (1 package, 2 stream; 0 other), and this
-    // encryptor's slot in the key table tagged _batchTag (a table generation), so a flush
-    // finds a known connection's slot without a lookup; _batchSeen = the last flush that
-    // listed it (stream state hand-off)
+    // encryptor's slot in the key table of one generation (tag), so a flush finds a known
+    // connection's slot without a lookup: tag << 24 | slot in ONE atomic word, so two
+    // batches flushing the same PackageEncryptor on two threads can never pair one table's
+    // tag with the other's slot (0: none); _batchSeen = the last flush that listed it
+    // (stream state hand-off; a StreamEncryptor belongs to one thread at a time anyway)
     uint8_t _kind = 0;
-    uint32_t _batchSlot = 0;
-    uint64_t _batchTag = 0, _batchSeen = 0;
+    std::atomic<uint64_t> _batchCache{0};
+    uint64_t _batchSeen = 0;
 
 public:
     Encryptor(uint8_t *key, size_t key_len, uint8_t *iv) {
@@ -78,7 +81,8 @@ public:
             _keyLen = o._keyLen;
             encryptor_retire(_serial);
             _serial = encryptor_serial();
-            _batchTag = _batchSeen = 0;  // a new serial: no table slot yet
+            _batchCache.store(0, std::memory_order_relaxed);  // a new serial: no table slot yet
+            _batchSeen = 0;
         }
         return *this;
     }

@@ -8,6 +8,7 @@
 //   S <E|D> <key> <iv> <f1> .. <fn> -> "<out1> .. <outn>"      (StreamEncryptor)
 //   R <key> <iv> <data>            -> "<roundtrip-memcmp> <cipher>" (rijndael.h API)
 //   BP / BS ...                    as P / S, but queued on one fpnn::EncryptorBatch
+//                                  (BS E: a frame "s<hex>" / "s-" is queued as encrypt(std::string*))
 //   F                              flush the batch, then print the queued cases' lines
 // hex fields, "-" for an empty buffer.
 #include <stdio.h>
@@ -92,6 +93,13 @@ int main() {
             fpnn::Encryptor *enc = q.encs.back().get();
             std::vector<Queued::Out> outs;
             while (is >> f) {
+                if (dir == "E" && f.compare(0, 1, "s") == 0) {  // s<hex> / s-: encrypt(std::string*) (SendBuffer's form)
+                    auto data = unhex(f.substr(1));
+                    q.strs.emplace_back(new std::string((const char *)data.data(), data.size()));
+                    batch.encrypt(enc, q.strs.back().get());
+                    outs.push_back({nullptr, 0, q.strs.back().get()});
+                    continue;
+                }
                 auto data = unhex(f);
                 std::vector<uint8_t> *src = q.keep(data), *o = q.keep(data);
                 if (dir == "E")

@@ -841,6 +841,23 @@ def test_cpp_encryptor_batch_matches_reference(golden, tmp_path, oracle):
             lines.append(f"BS {'E' if enc else 'D'} {key.hex()} {iv.hex()} " + " ".join(f.hex() or "-" for f in frames))
             expect.append(" ".join(outs))
     lines.append("F")
+    # StreamEncryptor::encrypt(std::string*) of "" queued FIRST on a stream, then real frames
+    # in both forms (the empty op used to mark the encryptor as listed without
+    # grouping it, so its (iv, pos) was never staged nor taken back)
+    for conn in range(24):
+        kl = (16, 32)[conn % 2]
+        key, iv = rng.bytes(kl), rng.bytes(16)
+        frames = [b""] + [rng.bytes(int(rng.integers(1, 700))) for _ in range(int(rng.integers(1, 5)))]
+        if conn % 3 == 0:
+            frames.insert(2, b"")
+        toks, outs, st_iv, st_pos = [], [], iv, 0
+        for j, f in enumerate(frames):
+            o, st_iv, st_pos = oracle.cfb(key, True, f, st_iv, st_pos)
+            outs.append(o.hex() or "-")
+            toks.append(("s" + (f.hex() or "-")) if (j + conn) % 2 == 0 or not f else (f.hex() or "-"))
+        lines.append(f"BS E {key.hex()} {iv.hex()} " + " ".join(toks))
+        expect.append(" ".join(outs))
+    lines.append("F")
     import subprocess
     res = subprocess.run([exe], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr

@@ -11,6 +11,9 @@
 #   tests:<expr>     pytest -m gpu -k <expr>
 #   probe:<lib>:<expr>  the same against another build of the GPU library (fpnn_amd/<lib>, loaded
 #                    through FPNN_AES_GPU_LIB), e.g. a tools/probe/*.patch build
+#   guard            tests/cpp/guard_pages.cpp: ragged encrypts over arrays abutting unmapped pages
+#   guard_audit      the same through the address-audit build (libfpnn_aes_gpu_audit.so)
+#   audit:<expr>     pytest -m gpu -k <expr> through the address-audit build
 #   bench            python bench.py (the contract line)
 #   bench_driver     bench.py three times with the driver's arguments (--steps 20 --warmup 5)
 #   bench_trace      bench.py under rocprofv3 --kernel-trace --stats (profiles the line's kernels)
@@ -75,6 +78,14 @@ for step in "$@"; do
     probe:*) spec=${step#probe:}; lib=${spec%%:*}
       FPNN_AES_GPU_LIB=$PWD/fpnn_amd/$lib run "probe_${lib%.so}" 600 python -u -m pytest tests -q -m gpu \
         --timeout 300 --timeout-method thread -k "${spec#*:}" ;;
+    guard|guard_audit) [ -x "$OUT/guard_pages" ] || { gcc -O2 -fPIC -c oracle/aes_oracle.c -o "$OUT/aes_oracle.o" &&
+        g++ -std=c++14 -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tests/cpp/guard_pages.cpp "$OUT/aes_oracle.o" \
+          -o "$OUT/guard_pages" -L fpnn_amd -lfpnn_aes -Wl,-rpath,"$PWD/fpnn_amd" -L/opt/rocm/lib -lamdhip64 \
+          -Wl,-rpath,/opt/rocm/lib -pthread || exit 3; }
+      if [ "$step" = guard ]; then run guard 300 "$OUT/guard_pages"
+      else FPNN_AES_GPU_LIB=$PWD/fpnn_amd/libfpnn_aes_gpu_audit.so run guard_audit 300 "$OUT/guard_pages"; fi ;;
+    audit:*) FPNN_AES_GPU_LIB=$PWD/fpnn_amd/libfpnn_aes_gpu_audit.so run audit 900 python -u -m pytest tests -q -m gpu \
+        --timeout 300 --timeout-method thread -p no:cacheprovider -k "${step#audit:}" ;;
     bench) run bench 300 python -u bench.py ;;
     bench_driver) for i in 1 2 3; do  # the driver's own arguments (BENCH_rNN.json: --steps 20 --warmup 5)
         run "bench_driver_$i" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
