@@ -547,12 +547,13 @@ int audit_end(fpnn_aes_engine *e, int rc) {
     AuditTable t;
     HIP_TRY(hipMemcpy(&t, e->d_aud, sizeof t, hipMemcpyDeviceToHost));
     if (!t.hits) return FPNN_AES_OK;
-    char buf[512];
+    char buf[640];
     snprintf(buf, sizeof buf,
              "address audit: %u access(es) outside their extent; first: %s (%s) line %u, workgroup %u thread %u, "
-             "bytes [0x%llx, +%llu) against [0x%llx, 0x%llx)",
+             "bytes [0x%llx, +%llu) against [0x%llx, 0x%llx); segment %lld [0x%llx, 0x%llx)",
              t.hits, last_launched(), audit_buf_name(t.buf), t.site, t.block, t.thread, (unsigned long long)t.addr,
-             (unsigned long long)t.len, (unsigned long long)t.elo, (unsigned long long)t.ehi);
+             (unsigned long long)t.len, (unsigned long long)t.elo, (unsigned long long)t.ehi, (long long)t.sid,
+             (unsigned long long)t.slo, (unsigned long long)t.shi);
     g_last_error = buf;
     fprintf(stderr, "[fpnn_aes audit] %s\n", buf);
     return FPNN_AES_ERR_DEVICE;

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint8_t *p = nullptr;
         uint8_t *o = nullptr;
         uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
-        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0, a_sid = ~0ull);  // (audit build: the chain's own bytes)
         // SHIFT state: d = o & 15; the funnel's rotation kl, sources (fl, fh) and
         // byte offset r; pl / ph = the rotated words of the previous raw block, praw its
         // own word; pv / lo0 as in the lane session
@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+            FA_SET(a_sid, s);
             FA_SET(a_ilo, (uintptr_t)g.in);
             FA_SET(a_ihi, (uintptr_t)g.in + g.len);
             FA_SET(a_olo, (uintptr_t)g.out);
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         // prev that are this chain's own output (rewritable); lo0 = first byte of the
         // chain's first slot that this chain may write
         uint32_t nfull = 0, tail = 0, n = 0, d = 0, pv = 0, lo0 = 0;
-        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0, a_sid = ~0ull);  // (audit build: the chain's own bytes)
         uint4 iv = make_uint4(0, 0, 0, 0), prev = make_uint4(0, 0, 0, 0);
         bool valid = false, exhausted = false, fresh = false;
         bool at0 = false;                     // package mode: no block of the chain ciphered yet
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+            FA_SET(a_sid, s);
             FA_SET(a_ilo, (uintptr_t)g.in);
             FA_SET(a_ihi, (uintptr_t)g.in + g.len);
             FA_SET(a_olo, (uintptr_t)g.out);

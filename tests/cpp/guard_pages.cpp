@@ -16,7 +16,8 @@
 // the tests use.  With FPNN_AES_GPU_LIB pointing at libfpnn_aes_gpu_audit.so the same run
 // also checks every access of K2h / K2 / the length order against its extent (audit.hpp).
 //
-//   guard_pages [filter]     one line per (case, engine, placement); exit 0 when all pass
+//   guard_pages [--direct-copy] [--malloc] [--keep-going] [--reuse-va] [filter]
+//                one line per (case, engine, placement); exit 0 when all pass
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -42,6 +43,13 @@ namespace {
     } while (0)
 
 size_t g_gran = 0;
+bool g_direct_copy = false;  // --direct-copy: hipMemcpy of the array's bytes only (else whole mapped pages)
+bool g_malloc = false;       // --malloc: plain hipMalloc allocations of the exact size (no guard pages)
+bool g_keep_going = false;   // --keep-going: run every case after a failure
+// --reuse-va: unmap and release each case's mappings when it ends (their virtual addresses
+// come back for the next case's arrays); by default they stay mapped until the process
+// exits, so no device virtual address is ever mapped twice in one run
+bool g_reuse_va = false;
 
 // one array in a mapping of its own, an unmapped granule before and after it
 struct Guarded {
@@ -51,6 +59,10 @@ struct Guarded {
     uint8_t *ptr = nullptr;  // the array
     size_t n = 0;
     Guarded(size_t bytes, bool at_end) : n(bytes) {
+        if (g_malloc) {
+            HIPCHK(hipMalloc(reinterpret_cast<void **>(&ptr), bytes ? bytes : 1));
+            return;
+        }
         map_size = (bytes + g_gran - 1) / g_gran * g_gran;
         if (map_size == 0) map_size = g_gran;
         va_size = map_size + 2 * g_gran;
@@ -72,13 +84,41 @@ struct Guarded {
         ptr = at_end ? mid + map_size - bytes : mid;
     }
     ~Guarded() {
+        if (g_malloc) {
+            (void)hipFree(ptr);
+            return;
+        }
+        if (!g_reuse_va) return;  // (left mapped: the process exit releases it)
         uint8_t *mid = static_cast<uint8_t *>(va) + g_gran;
         (void)hipMemUnmap(mid, map_size);
         (void)hipMemRelease(h);
         (void)hipMemAddressFree(va, va_size);
     }
-    void put(const void *src) { HIPCHK(hipMemcpy(ptr, src, n, hipMemcpyHostToDevice)); }
-    void get(void *dst) const { HIPCHK(hipMemcpy(dst, ptr, n, hipMemcpyDeviceToHost)); }
+    // Copies move whole mapped pages from / to a host image (page-aligned, whole-page copies),
+    // and every upload is read back and compared, so a copy path that mishandles a
+    // destination at an odd address inside a mapping cannot pass for a kernel error.
+    uint8_t *mid() const { return static_cast<uint8_t *>(va) + g_gran; }
+    bool put(const void *src) {
+        if (g_malloc || g_direct_copy) {
+            HIPCHK(hipMemcpy(ptr, src, n, hipMemcpyHostToDevice));
+        } else {
+            std::vector<uint8_t> img(map_size, 0);
+            memcpy(&img[ptr - mid()], src, n);
+            HIPCHK(hipMemcpy(mid(), img.data(), map_size, hipMemcpyHostToDevice));
+        }
+        std::vector<uint8_t> back(n);
+        get(back.data());
+        return memcmp(back.data(), src, n) == 0;
+    }
+    void get(void *dst) const {
+        if (g_malloc || g_direct_copy) {
+            HIPCHK(hipMemcpy(dst, ptr, n, hipMemcpyDeviceToHost));
+            return;
+        }
+        std::vector<uint8_t> img(map_size);
+        HIPCHK(hipMemcpy(img.data(), mid(), map_size, hipMemcpyDeviceToHost));
+        memcpy(dst, &img[ptr - mid()], n);
+    }
     Guarded(const Guarded &) = delete;
     Guarded &operator=(const Guarded &) = delete;
 };
@@ -199,12 +239,12 @@ int run_case(const Case &c, fpnn_aes_engine *e, bool at_end, uint64_t seed, std:
     }
     Guarded g_in(in_bytes, at_end), g_out(out_bytes, at_end), g_ioff(8 * (size_t)n, at_end),
         g_ooff(8 * (size_t)n, at_end), g_len(4 * (size_t)n, at_end), g_slot(4 * (size_t)n, at_end);
-    g_in.put(plain.data());
-    g_out.put(dst0.data());
-    g_ioff.put(in_off.data());
-    g_ooff.put(out_off.data());
-    g_len.put(len.data());
-    g_slot.put(slot.data());
+    if (!g_in.put(plain.data()) || !g_out.put(dst0.data()) || !g_ioff.put(in_off.data()) ||
+        !g_ooff.put(out_off.data()) || !g_len.put(len.data()) || !g_slot.put(slot.data())) {
+        why = "upload read back differently (HIP copy path)";
+        fpnn_aes_keyset_destroy(ks);
+        return -102;
+    }
     std::unique_ptr<Guarded> g_iv, g_pos;
     fpnn_aes_batch b;
     memset(&b, 0, sizeof b);
@@ -221,8 +261,11 @@ int run_case(const Case &c, fpnn_aes_engine *e, bool at_end, uint64_t seed, std:
     if (c.kind == 2) {
         g_iv.reset(new Guarded(iv_state.size(), at_end));
         g_pos.reset(new Guarded(4 * (size_t)n, at_end));
-        g_iv->put(iv_state.data());
-        g_pos->put(pos_state.data());
+        if (!g_iv->put(iv_state.data()) || !g_pos->put(pos_state.data())) {
+            why = "upload read back differently (HIP copy path)";
+            fpnn_aes_keyset_destroy(ks);
+            return -102;
+        }
         if ((uintptr_t)g_iv->ptr & 15) {  // (iv_state must be 16-byte aligned: n * 16 bytes end on the grid)
             why = "iv_state misaligned";
             return -100;
@@ -251,8 +294,33 @@ int run_case(const Case &c, fpnn_aes_engine *e, bool at_end, uint64_t seed, std:
     }
     fpnn_aes_keyset_destroy(ks);
     if (bad) {
-        char m[128];
-        snprintf(m, sizeof m, "%zu bytes differ, first at %zu", bad, first);
+        // which frames: the first bad one's descriptor and where in it the bytes differ
+        uint32_t nbadf = 0, fi = n;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t o = out_off[i], e = o + len[i] + (wire ? 4 : 0);
+            bool fb = false;
+            for (uint64_t k = o; k < e && !fb; k++) fb = got[k] != exp[k];
+            if (fb && !nbadf++) fi = i;
+        }
+        char m[400];
+        if (fi < n) {
+            const uint64_t o = out_off[fi], e = o + len[fi] + (wire ? 4 : 0);
+            uint64_t k0 = e, k1 = o;
+            for (uint64_t k = o; k < e; k++)
+                if (got[k] != exp[k]) {
+                    k0 = std::min(k0, k);
+                    k1 = k + 1;
+                }
+            snprintf(m, sizeof m,
+                     "%zu bytes differ, first at %zu; %u frames bad, first frame %u (in_off %llu out_off %llu len %u "
+                     "slot %u): bytes [%llu, %llu) of it; in at 0x%llx out at 0x%llx",
+                     bad, first, nbadf, fi, (unsigned long long)in_off[fi], (unsigned long long)o, len[fi], slot[fi],
+                     (unsigned long long)(k0 - o), (unsigned long long)(k1 - o),
+                     (unsigned long long)(uintptr_t)(g_in.ptr + in_off[fi]), (unsigned long long)(uintptr_t)(g_out.ptr + o));
+        } else {
+            snprintf(m, sizeof m, "%zu bytes differ, first at %zu (outside every frame; state arrays: %s)", bad, first,
+                     bad >= 1000000000 ? "differ" : "equal");
+        }
         why = m;
         return -101;
     }
@@ -262,7 +330,14 @@ int run_case(const Case &c, fpnn_aes_engine *e, bool at_end, uint64_t seed, std:
 }  // namespace
 
 int main(int argc, char **argv) {
-    const char *filter = argc > 1 ? argv[1] : "";
+    const char *filter = "";
+    for (int i = 1; i < argc; i++) {
+        if (!strcmp(argv[i], "--direct-copy")) g_direct_copy = true;
+        else if (!strcmp(argv[i], "--malloc")) g_malloc = true;
+        else if (!strcmp(argv[i], "--keep-going")) g_keep_going = true;
+        else if (!strcmp(argv[i], "--reuse-va")) g_reuse_va = true;
+        else filter = argv[i];
+    }
     int vmm = 0;
     HIPCHK(hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, 0));
     if (!vmm) {
@@ -275,7 +350,9 @@ int main(int argc, char **argv) {
     prop.location.type = hipMemLocationTypeDevice;
     prop.location.id = 0;
     HIPCHK(hipMemGetAllocationGranularity(&g_gran, &prop, hipMemAllocationGranularityMinimum));
-    printf("granularity %zu B, library %s\n", g_gran, fpnn_aes_version());
+    printf("granularity %zu B, %s, library %s\n", g_gran,
+           g_malloc ? "hipMalloc arrays" : g_direct_copy ? "array-range copies" : "whole-page copies", fpnn_aes_version());
+    printf("mappings %s\n", g_reuse_va ? "released after each case (addresses reused)" : "kept until exit (no address reused)");
     int failed = 0, ran = 0;
     for (const EngineKind &k : kEngines) {
         for (const auto &kv : k.env)
@@ -299,6 +376,10 @@ int main(int argc, char **argv) {
                        r ? why.c_str() : "");
                 fflush(stdout);
                 if (r) failed++;
+                if (r && !g_keep_going) {  // one failure tells its story; the next run could start from its debris
+                    printf("stopping at the first failure (--keep-going runs on)\n");
+                    return 1;
+                }
             }
         }
         fpnn_aes_engine_destroy(e);

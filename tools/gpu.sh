@@ -78,12 +78,15 @@ for step in "$@"; do
     probe:*) spec=${step#probe:}; lib=${spec%%:*}
       FPNN_AES_GPU_LIB=$PWD/fpnn_amd/$lib run "probe_${lib%.so}" 600 python -u -m pytest tests -q -m gpu \
         --timeout 300 --timeout-method thread -k "${spec#*:}" ;;
-    guard|guard_audit) [ -x "$OUT/guard_pages" ] || { gcc -O2 -fPIC -c oracle/aes_oracle.c -o "$OUT/aes_oracle.o" &&
+    guard|guard:*|guard_audit|guard_audit:*)  # (:<args> comma-separated, e.g. guard_audit:--malloc)
+      [ -x "$OUT/guard_pages" ] || { gcc -O2 -fPIC -c oracle/aes_oracle.c -o "$OUT/aes_oracle.o" &&
         g++ -std=c++14 -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tests/cpp/guard_pages.cpp "$OUT/aes_oracle.o" \
           -o "$OUT/guard_pages" -L fpnn_amd -lfpnn_aes -Wl,-rpath,"$PWD/fpnn_amd" -L/opt/rocm/lib -lamdhip64 \
           -Wl,-rpath,/opt/rocm/lib -pthread || exit 3; }
-      if [ "$step" = guard ]; then run guard 300 "$OUT/guard_pages"
-      else FPNN_AES_GPU_LIB=$PWD/fpnn_amd/libfpnn_aes_gpu_audit.so run guard_audit 300 "$OUT/guard_pages"; fi ;;
+      gname=${step%%:*}; gargs=""; [ "$gname" != "$step" ] && gargs=${step#*:}
+      glog=$gname${gargs:+_${gargs//[^a-z]/}}
+      if [ "$gname" = guard ]; then run "$glog" 300 "$OUT/guard_pages" ${gargs//,/ }
+      else FPNN_AES_GPU_LIB=$PWD/fpnn_amd/libfpnn_aes_gpu_audit.so run "$glog" 300 "$OUT/guard_pages" ${gargs//,/ }; fi ;;
     audit:*) FPNN_AES_GPU_LIB=$PWD/fpnn_amd/libfpnn_aes_gpu_audit.so run audit 900 python -u -m pytest tests -q -m gpu \
         --timeout 300 --timeout-method thread -p no:cacheprovider -k "${step#audit:}" ;;
     bench) run bench 300 python -u bench.py ;;
