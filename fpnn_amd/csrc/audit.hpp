@@ -51,7 +51,14 @@ struct AuditTable {
 
 #if defined(FPNN_AES_BOUNDS) && defined(__HIP_DEVICE_COMPILE__)
 
-__device__ __noinline__ void audit_record(AuditTable *a, uint32_t buf, uint64_t x, uint64_t n, uint64_t lo, uint64_t hi,
+// (inlined by default: an out-of-line call makes every instrumented kernel keep a call frame
+// in scratch; -DFPNN_AES_AUDIT_CALL keeps the call, for comparison)
+#ifdef FPNN_AES_AUDIT_CALL
+#define FPNN_AUDIT_RECORD_ATTR __noinline__
+#else
+#define FPNN_AUDIT_RECORD_ATTR __forceinline__
+#endif
+__device__ FPNN_AUDIT_RECORD_ATTR void audit_record(AuditTable *a, uint32_t buf, uint64_t x, uint64_t n, uint64_t lo, uint64_t hi,
                                           uint32_t site, uint64_t slo, uint64_t shi, uint64_t sid) {
     if (atomicAdd(&a->hits, 1u) == 0u) {
         a->site = site;

@@ -17,6 +17,7 @@
 #include "../../include/Encryptor.h"
 #include "../../include/EncryptorBatch.h"
 #include "../../include/fpnn_aes.h"
+#include "fail_policy.hpp"
 #include "thread_engine.hpp"
 
 namespace {
@@ -60,10 +61,10 @@ const fpnn_aes_schedule *sched(const rijndael_context *ctx) {
     return reinterpret_cast<const fpnn_aes_schedule *>(ctx);
 }
 
-void cfb_or_throw(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *out, size_t len,
+void cfb_or_fail(const rijndael_context *ctx, bool encrypt, const uint8_t *in, uint8_t *out, size_t len,
                   uint8_t ivec[16], size_t *p_num) {
     const int rc = cfb(ctx, encrypt, in, out, len, ivec, p_num);
-    if (rc != FPNN_AES_OK) throw fpnn::EncryptorError("fpnn_aes GPU CFB failed: " + describe(rc));
+    if (rc != FPNN_AES_OK) fpnn_aes::device_failure("GPU CFB failed: " + describe(rc));  // (fail_policy.hpp)
 }
 
 }  // namespace
@@ -120,7 +121,7 @@ void PackageEncryptor::decrypt(uint8_t *dest, uint8_t *src, int len) {  // core/
     uint8_t iv[16];
     memcpy(iv, _iv, 16);
     size_t pos = 0;
-    cfb_or_throw(&_ctx, false, src, dest, (size_t)len, iv, &pos);
+    cfb_or_fail(&_ctx, false, src, dest, (size_t)len, iv, &pos);
 }
 
 void PackageEncryptor::encrypt(uint8_t *dest, uint8_t *src, int len) {  // core/Encryptor.cpp:22-32
@@ -128,7 +129,7 @@ void PackageEncryptor::encrypt(uint8_t *dest, uint8_t *src, int len) {  // core/
     uint8_t iv[16];
     memcpy(iv, _iv, 16);
     size_t pos = 0;
-    cfb_or_throw(&_ctx, true, src, dest, (size_t)len, iv, &pos);
+    cfb_or_fail(&_ctx, true, src, dest, (size_t)len, iv, &pos);
 }
 
 void PackageEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:34-51
@@ -140,7 +141,7 @@ void PackageEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:34-
         uint8_t iv[16];
         memcpy(iv, _iv, 16);
         size_t pos = 0;
-        cfb_or_throw(&_ctx, true, reinterpret_cast<const uint8_t *>(buffer->data()),
+        cfb_or_fail(&_ctx, true, reinterpret_cast<const uint8_t *>(buffer->data()),
                      reinterpret_cast<uint8_t *>(&framed[sizeof(uint32_t)]), n, iv, &pos);
     }
     buffer->swap(framed);
@@ -148,19 +149,19 @@ void PackageEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:34-
 
 void StreamEncryptor::decrypt(uint8_t *dest, uint8_t *src, int len) {  // core/Encryptor.cpp:53-56
     if (len <= 0) return;
-    cfb_or_throw(&_ctx, false, src, dest, (size_t)len, _iv, &_pos);
+    cfb_or_fail(&_ctx, false, src, dest, (size_t)len, _iv, &_pos);
 }
 
 void StreamEncryptor::encrypt(uint8_t *dest, uint8_t *src, int len) {  // core/Encryptor.cpp:58-61
     if (len <= 0) return;
-    cfb_or_throw(&_ctx, true, src, dest, (size_t)len, _iv, &_pos);
+    cfb_or_fail(&_ctx, true, src, dest, (size_t)len, _iv, &_pos);
 }
 
 void StreamEncryptor::encrypt(std::string *buffer) {  // core/Encryptor.cpp:63-70
     const size_t n = buffer->length();
     if (!n) return;
     std::string out(n, '\0');
-    cfb_or_throw(&_ctx, true, reinterpret_cast<const uint8_t *>(buffer->data()), reinterpret_cast<uint8_t *>(&out[0]),
+    cfb_or_fail(&_ctx, true, reinterpret_cast<const uint8_t *>(buffer->data()), reinterpret_cast<uint8_t *>(&out[0]),
                  n, _iv, &_pos);
     buffer->swap(out);
 }
@@ -336,7 +337,7 @@ void EncryptorBatch::flush() {
     const fpnn_aes::Lease lease = thread_engine(&rc);
     fpnn_aes_engine *e = lease.engine();
     const uint64_t eid = lease.id();
-    if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
+    if (!e) fpnn_aes::device_failure("engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
     // group by (mode, direction, wire prefix, rounds); queue order is kept inside a group
     struct Group {
         bool stream, encrypt, prefix;
@@ -396,7 +397,7 @@ void EncryptorBatch::flush() {
             if (rc != FPNN_AES_OK) {
                 delete tp;
                 tp = nullptr;
-                throw EncryptorError("EncryptorBatch: key table: " + describe(rc));
+                fpnn_aes::device_failure("EncryptorBatch: key table: " + describe(rc));
             }
         }
         KeyTable &t = *tp;
@@ -444,7 +445,7 @@ void EncryptorBatch::flush() {
                 // the slots handed out above were not uploaded: forget the table
                 delete tp;
                 tp = nullptr;
-                throw EncryptorError("EncryptorBatch: key table upload: " + describe(rc));
+                fpnn_aes::device_failure("EncryptorBatch: key table upload: " + describe(rc));
             }
             t.watch(fresh);
             break;
@@ -483,7 +484,7 @@ void EncryptorBatch::flush() {
         if (!gr.stream) {
             rc = fpnn_aes_package_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                        gr.prefix ? FPNN_AES_F_WIRE_PREFIX : 0);
-            if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: package batch: " + describe(rc));
+            if (rc != FPNN_AES_OK) fpnn_aes::device_failure("EncryptorBatch: package batch: " + describe(rc));
             if (bs.on) {
                 const double t = BatchStats::now();
                 bs.call += t - tt;
@@ -505,7 +506,7 @@ void EncryptorBatch::flush() {
             }
             rc = fpnn_aes_stream_host(e, gr.encrypt ? 1 : 0, frames.data(), (uint32_t)frames.size(), t.ks,
                                       t.iv.data(), t.pos.data());
-            if (rc != FPNN_AES_OK) throw EncryptorError("EncryptorBatch: stream batch: " + describe(rc));
+            if (rc != FPNN_AES_OK) fpnn_aes::device_failure("EncryptorBatch: stream batch: " + describe(rc));
             for (const auto &m : gr.members) {
                 const uint32_t sl = slots[m.second];
                 memcpy(m.first->_iv, &t.iv[16 * (size_t)sl], 16);

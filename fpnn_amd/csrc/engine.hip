@@ -38,6 +38,22 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// FPNN_AES_DEBUG_FAIL_CALL=N (tests only): the N-th host-data call of the process (cfb_host,
+// package_host, stream_host, stream_recv -- the calls the C++ classes make) returns
+// FPNN_AES_ERR_DEVICE as a failed device would, so the drop-in's failure contract can be
+// driven through FPNN's own IO code (fail_policy.hpp, tests/test_gpu_dropin.py).
+int debug_fail_point() {
+    static const long long at = [] {
+        const char *v = getenv("FPNN_AES_DEBUG_FAIL_CALL");
+        return v ? atoll(v) : 0ll;
+    }();
+    if (at <= 0) return 0;
+    static std::atomic<long long> calls{0};
+    if (calls.fetch_add(1, std::memory_order_relaxed) + 1 != at) return 0;
+    g_last_error = "injected device error (FPNN_AES_DEBUG_FAIL_CALL)";
+    return FPNN_AES_ERR_DEVICE;
+}
+
 int hip_fail(hipError_t err, const char *what) {
     char buf[256];
     snprintf(buf, sizeof buf, "%s: %s (%d)", what, hipGetErrorString(err), (int)err);
@@ -1274,6 +1290,7 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
                           uint64_t *frame_off, uint32_t *frame_len, fpnn_aes_frame_scan *scan) {
     int rc = check_batch(e, b);
     if (rc) return rc;
+    if ((rc = debug_fail_point())) return rc;
     if (b->out_off || b->flags) return FPNN_AES_ERR_ARG;
     if (!b->count) return FPNN_AES_OK;
     if (!frame_off || !frame_len || !scan || !max_frames) return FPNN_AES_ERR_ARG;
@@ -1321,6 +1338,7 @@ int fpnn_aes_stream_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
                          uint32_t *frame_len, fpnn_aes_frame_scan *scan) {
     int rc = check_batch(e, b);
     if (rc) return rc;
+    if ((rc = debug_fail_point())) return rc;
     if (!b->count) return FPNN_AES_OK;
     if (!frame_off || !frame_len || !scan || !max_frames) return FPNN_AES_ERR_ARG;
     if ((uint64_t)b->count * max_frames > 0xffffffffull) return FPNN_AES_ERR_RANGE;
@@ -1712,6 +1730,7 @@ int fpnn_aes_ofb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, const ui
 int fpnn_aes_cfb_host(fpnn_aes_engine *e, const fpnn_aes_schedule *ctx, int encrypt, const uint8_t *in,
                       uint8_t *out, size_t len, uint8_t ivec[16], size_t *p_num) {
     if (!e || !ctx || !ivec || !p_num || (len && (!in || !out))) return FPNN_AES_ERR_ARG;
+    if (int rc = debug_fail_point()) return rc;
     const int nr = ctx->nrounds;
     if (nr != 10 && nr != 12 && nr != 14) return FPNN_AES_ERR_KEYLEN;
     if (*p_num > 15) return FPNN_AES_ERR_ARG;
@@ -2879,6 +2898,7 @@ bool mapped_enabled() {
 int fpnn_aes_package_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                           const fpnn_aes_keyset *keys, uint32_t flags) {
     if (int rc = check_host_frames(e, frames, n, keys)) return rc;
+    if (int rc = debug_fail_point()) return rc;
     if (!encrypt && (flags & FPNN_AES_F_WIRE_PREFIX)) return FPNN_AES_ERR_ARG;
     if (flags & FPNN_AES_F_WIRE_PREFIX)
         for (uint32_t i = 0; i < n; i++)
@@ -2945,6 +2965,7 @@ int fpnn_aes_host_is_mapped(const void *ptr, size_t len) {
 int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_frame *frames, uint32_t n,
                          const fpnn_aes_keyset *keys, uint8_t *iv_state, uint32_t *pos_state) {
     if (int rc = check_host_frames(e, frames, n, keys)) return rc;
+    if (int rc = debug_fail_point()) return rc;
     if (n && (!iv_state || !pos_state)) return FPNN_AES_ERR_ARG;
     if (!n) return FPNN_AES_OK;
     if (mapped_enabled()) {  // every frame in registered host memory: the GPU moves the bytes

@@ -11,6 +11,7 @@
 
 #include "../../include/StreamReceiverBatch.h"
 #include "../../include/fpnn_aes.h"
+#include "fail_policy.hpp"
 #include "thread_engine.hpp"
 
 namespace fpnn {
@@ -25,7 +26,7 @@ std::string describe(int rc) {
 }
 
 void check(int rc, const char *what) {
-    if (rc != FPNN_AES_OK) throw EncryptorError(std::string("StreamReceiverBatch: ") + what + ": " + describe(rc));
+    if (rc != FPNN_AES_OK) fpnn_aes::device_failure(std::string("StreamReceiverBatch: ") + what + ": " + describe(rc));
 }
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
@@ -140,7 +141,7 @@ void StreamReceiverBatch::flush() {
     const fpnn_aes::Lease lease = fpnn_aes::thread_engine(&rc);
     fpnn_aes_engine *e = lease.engine();
     const uint64_t eid = lease.id();
-    if (!e) throw EncryptorError("fpnn_aes engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
+    if (!e) fpnn_aes::device_failure("engine unavailable: " + describe(rc ? rc : FPNN_AES_ERR_NODEV));
     if (!_dev) {
         _dev = new Dev();
         _dev->pe = lease.pe;

@@ -320,9 +320,13 @@ MULTI_REF = os.path.join(HERE, "_ref", "io_multi_ref")
 # SURVEY 8f row 1 inside FPNN's IO plumbing (oracle/io_multi.cpp):
 # (name, mode, keylen, conns, quests per conn, payload, window, threads).  M1 is the headline
 # shape: 1 024 connections x window 8 x 1 KiB AES-256 package frames.
+# M6 / M7: the client connections start as TCPClient's do -- the "*key"
+# quest in the clear (SendBuffer::encryptAfterFirstPackage, core/IOBuffer.cpp:36-45,
+# core/TCPClient.cpp:238-243), every later frame encrypted (io_multi's first_clear).
 MULTI_CASES = [("M1", "package", 32, 1024, 32, 1024, 8, 1), ("M2", "package", 16, 1024, 16, 1024, 8, 4),
                ("M3", "package", 24, 300, 12, 3001, 4, 2), ("M4", "stream", 32, 1024, 16, 1024, 8, 1),
-               ("M5", "stream", 16, 256, 24, 777, 4, 2)]
+               ("M5", "stream", 16, 256, 24, 777, 4, 2),
+               ("M6", "package", 32, 512, 8, 1024, 4, 2, True), ("M7", "stream", 16, 512, 8, 1024, 4, 2, True)]
 
 
 def gen_multi_cases():
@@ -332,12 +336,16 @@ def gen_multi_cases():
     stream is fixed by its key, IV and quests)."""
     import subprocess
     cases = []
-    for name, mode, kl, conns, q, plen, win, thr in MULTI_CASES:
+    for name, mode, kl, conns, q, plen, win, thr, *fc in MULTI_CASES:
+        first_clear = bool(fc and fc[0])
         out = subprocess.run([MULTI_REF, "1" if mode == "stream" else "0", str(kl), str(conns), str(q), str(plen),
-                              str(win), str(thr)], capture_output=True, text=True, check=True, timeout=600).stdout
+                              str(win), str(thr), "1", "1" if first_clear else "0"],
+                             capture_output=True, text=True, check=True, timeout=600).stdout
         d = json.loads(out.strip().splitlines()[-1])
         assert d["ok"] and d["answers_ok"], d
         c = {"name": name, "threads": thr}
+        if first_clear:
+            c["first_clear"] = True
         c.update({k: d[k] for k in ("mode", "keylen", "conns", "quests_per_conn", "payload", "window",
                                     "wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv")})
         cases.append(c)

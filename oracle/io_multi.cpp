@@ -29,8 +29,18 @@
 // wrote (write() is wrapped at link time, -Wl,--wrap=write), per connection and direction,
 // folded in connection order -- the three builds must agree byte for byte.
 //
+// With first_clear = 1 every client connection starts the way TCPClient does
+// (core/TCPClient.cpp:238-243, 464-472): its SendBuffer is told encryptAfterFirstPackage()
+// (core/IOBuffer.h:126) and its first frame is a "*key" quest that goes out in the clear
+// (SendBuffer::encryptData skips it, core/IOBuffer.cpp:36-45); every later frame is
+// encrypted.  The server reads that frame as plaintext, answers it -- encrypted, as
+// ServerIOWorker::processECDH's answer is (core/ServerIOWorker.cpp:306-309) -- and only then
+// hands the connection's bytes to its encrypted receiver.  In the batched build this runs
+// the collect patch's first-package count (collect_patch.py, NEW_REALSEND) over a cycle
+// whose collected frames start with the plaintext one.
+//
 // usage: io_multi <mode 0 package|1 stream> <keylen> <conns> <quests per conn> <payload>
-//                 <window> [threads] [tcp 1|0]
+//                 <window> [threads] [tcp 1|0] [first_clear 0|1]
 #include <arpa/inet.h>
 #include <errno.h>
 #include <execinfo.h>
@@ -121,6 +131,43 @@ struct Loopback {
     }
 };
 
+// the client's "*key" quest (core/TCPClient.cpp:469-472: {publicKey, streamMode, bits} as a
+// msgpack map), sent in the clear; its sequence number keeps its answer apart from the echoes
+constexpr uint32_t kKeySeq = 0x7fffff00u;
+std::string key_quest_raw(uint32_t conn, bool stream, int keylen) {
+    std::string m("\x83\xa9publicKey\xd9\x40", 13);
+    for (int k = 0; k < 64; k++) m += (char)(0x40 + ((conn * 7 + (uint32_t)k * 13) & 0x3f));
+    m += std::string("\xaastreamMode", 11) + (stream ? '\xc3' : '\xc2');
+    m += std::string("\xa4" "bits\xcd\x01\x00", 8);
+    if (keylen != 32) m[m.size() - 2] = '\x00', m[m.size() - 1] = '\x80';
+    FPQuest q("*key");
+    q.setSeqNum(kKeySeq);
+    q.setPayload(m);
+    q.setPayloadSize((uint32_t)m.size());
+    std::string *raw = q.raw();
+    std::string r(*raw);
+    delete raw;
+    return r;
+}
+
+// Reads one plaintext FPNN frame (12-byte header + FPMessage::BodyLen) from a non-blocking
+// fd into acc, never a byte more: 1 complete, 0 more to come, -1 closed / error.
+int read_plain_frame(int fd, std::string &acc) {
+    for (;;) {
+        const size_t want = acc.size() < 12 ? 12 - acc.size() : 12 + FPMessage::BodyLen(acc.data()) - acc.size();
+        if (want == 0) return 1;
+        char buf[4096];
+        const ssize_t r = ::read(fd, buf, std::min(want, sizeof buf));
+        if (r > 0) {
+            acc.append(buf, (size_t)r);
+            continue;
+        }
+        if (r == 0) return -1;
+        if (errno == EINTR) continue;
+        return (errno == EAGAIN || errno == EWOULDBLOCK) ? 0 : -1;
+    }
+}
+
 std::string payload_of(uint32_t conn, uint32_t i, int len) {
     std::string p((size_t)len, '\0');
     uint64_t x = 0x9E3779B97F4A7C15ull ^ ((uint64_t)i * 0xD1B54A32D192ED03ull) ^ ((uint64_t)conn << 40);
@@ -146,6 +193,10 @@ struct Conn {
     std::unique_ptr<Receiver> crecv, srecv;  // the object RecvBuffer::entryEncryptMode installs
     int crx = -1, srx = -1;                  // (batched stream mode) StreamReceiverBatch ids
     uint32_t sent = 0, answered = 0, served = 0, bad = 0;
+    // first_clear: the "*key" quest's state (client sent it / server still reading it /
+    // client got its answer) and the server's plaintext bytes of it
+    bool key_sent = false, key_pending = false, key_answered = false;
+    std::string key_acc;
 };
 
 struct Params {
@@ -154,6 +205,7 @@ struct Params {
     uint32_t quests;
     int plen;
     uint32_t window;
+    bool first_clear;
 };
 
 struct ThreadResult {
@@ -299,6 +351,43 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
         res->ok = false;
         res->err = std::string(what) + " on connection " + std::to_string(c->id);
     };
+    // an answer on the client: the "*key" answer (first_clear) or the next echo
+    auto client_answer = [&](Conn *c, const FPAnswerPtr &a) {
+        if (P.first_clear && a->seqNum() == kKeySeq && !c->key_answered) {
+            c->key_answered = true;
+            return;
+        }
+        const uint32_t i = a->seqNum() - 1;
+        if (i != c->answered || a->payload() != payload_of(c->id, i, P.plen)) c->bad++;
+        c->answered++;
+        left--;
+    };
+    // server, first_clear: the plaintext "*key" frame of each connection that still owes it,
+    // answered (encrypted) through the connection's SendBuffer; false on a broken frame
+    auto key_frames = [&]() -> bool {
+        if (!P.first_clear) return true;
+        COLLECT(batch);  // (the answers' encryption goes to the send flush)
+        for (Conn *c : conns) {
+            if (!c->key_pending) continue;
+            const int r = read_plain_frame(c->sfd, c->key_acc);
+            if (r < 0) {
+                fail("plaintext *key frame", c);
+                return false;
+            }
+            if (r == 0) continue;
+            FPQuestPtr q = Decoder::decodeQuest(c->key_acc.data(), (int)c->key_acc.size());
+            if (!q || q->method() != "*key") {
+                fail("first frame is not a plaintext *key quest", c);
+                return false;
+            }
+            FPAnswer reply(q);
+            reply.setPayload(std::string("\x80", 1));  // {} (core/ServerIOWorker.cpp:306-309)
+            reply.setPayloadSize(1);
+            c->ssend->send(c->sfd, nw, act, reply.raw());
+            c->key_pending = false;
+        }
+        return true;
+    };
     // a complete frame on receiver r: staged for decode after the flush (batched) or fetched now
     auto take = [&](Conn *c, bool server) -> bool {
         Receiver *r = server ? c->srecv.get() : c->crecv.get();
@@ -324,10 +413,7 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
             c->served++;
         } else {
             if (!a) return false;
-            const uint32_t i = a->seqNum() - 1;
-            if (i != c->answered || a->payload() != payload_of(c->id, i, P.plen)) c->bad++;
-            c->answered++;
-            left--;
+            client_answer(c, a);
         }
         return true;
     };
@@ -349,10 +435,7 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
                 p.c->served++;
             } else {
                 if (!a) return false;
-                const uint32_t i = a->seqNum() - 1;
-                if (i != p.c->answered || a->payload() != payload_of(p.c->id, i, P.plen)) p.c->bad++;
-                p.c->answered++;
-                left--;
+                client_answer(p.c, a);
             }
         }
 #endif
@@ -366,7 +449,9 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
         if (P.stream) {  // StreamReceiverBatch: read what the sockets hold, one device pass
             char buf[65536];
             std::vector<Conn *> got;
+            if (server && !key_frames()) return false;
             for (Conn *c : conns) {
+                if (server && c->key_pending) continue;  // its plaintext frame is not complete yet
                 const int fd = server ? c->sfd : c->cfd;
                 bool any = false;
                 for (;;) {
@@ -402,19 +487,18 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
                     } else {
                         FPAnswerPtr a = Decoder::decodeAnswer(m.data(), (int)m.size());
                         if (!a) return false;
-                        const uint32_t i = a->seqNum() - 1;
-                        if (i != c->answered || a->payload() != payload_of(c->id, i, P.plen)) c->bad++;
-                        c->answered++;
-                        left--;
+                        client_answer(c, a);
                     }
                 }
             }
             return true;
         }
 #endif
+        if (server && !key_frames()) return false;
         {
             COLLECT(batch);  // package mode: fetchStage queues the decrypts
             for (Conn *c : conns) {
+                if (server && c->key_pending) continue;  // its plaintext frame is not complete yet
                 Receiver *r = server ? c->srecv.get() : c->crecv.get();
                 const int fd = server ? c->sfd : c->cfd;
                 for (;;) {
@@ -454,7 +538,11 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
         res->cycles++;
         {
             COLLECT(batch);  // client: the next quests (their encryption is queued)
-            for (Conn *c : conns)
+            for (Conn *c : conns) {
+                if (P.first_clear && !c->key_sent) {  // TCPClient's "*key" quest goes first, in the clear
+                    c->csend->send(c->cfd, nw, act, new std::string(key_quest_raw(c->id, P.stream, P.keylen)));
+                    c->key_sent = true;
+                }
                 while (c->sent < P.quests && c->sent - c->answered < P.window) {
                     FPQuest q("echo");
                     q.setSeqNum(c->sent + 1);
@@ -463,6 +551,7 @@ void io_thread(std::vector<Conn *> conns, const Params P, ThreadResult *res, Sta
                     c->csend->send(c->cfd, nw, act, q.raw());
                     c->sent++;
                 }
+            }
         }
         write_out(false);
         if (!receive(true)) return;  // server: quests -> answers (queued)
@@ -506,7 +595,7 @@ int main(int argc, char **argv) {
 
 static int run(int argc, char **argv) {
     if (argc < 7) {
-        fprintf(stderr, "usage: %s mode keylen conns quests payload window [threads] [tcp]\n", argv[0]);
+        fprintf(stderr, "usage: %s mode keylen conns quests payload window [threads] [tcp] [first_clear]\n", argv[0]);
         return 2;
     }
     Params P;
@@ -518,6 +607,7 @@ static int run(int argc, char **argv) {
     P.window = (uint32_t)atoi(argv[6]);
     const uint32_t nthr = argc > 7 ? std::max(1, atoi(argv[7])) : 1u;
     bool tcp = argc > 8 ? atoi(argv[8]) != 0 : true;
+    P.first_clear = argc > 9 && atoi(argv[9]) != 0;
     Setting::set("FP.server.local.ip4", "127.0.0.1");  // FPLog never asks the cloud-metadata client
 
     rlimit rl;
@@ -555,6 +645,10 @@ static int run(int argc, char **argv) {
         if (!c->csend->entryEncryptMode(c->key, (size_t)P.keylen, c->iv, P.stream) ||
             !c->ssend->entryEncryptMode(c->key, (size_t)P.keylen, c->iv, P.stream))
             return 4;
+        if (P.first_clear) {  // TCPClient::configEncryptedConnection (core/TCPClient.cpp:238-243)
+            c->csend->encryptAfterFirstPackage();
+            c->key_pending = true;
+        }
         auto make = [&]() -> Receiver * {
             return P.stream ? (Receiver *)new EncryptedStreamReceiver(c->key, (size_t)P.keylen, c->iv)
                             : (Receiver *)new EncryptedPackageReceiver(c->key, (size_t)P.keylen, c->iv);
@@ -594,6 +688,7 @@ static int run(int argc, char **argv) {
     uint64_t h_c2s = 0xcbf29ce484222325ull, h_s2c = 0xcbf29ce484222325ull, b_c2s = 0, b_s2c = 0;
     uint32_t bad = 0, served = 0, answered = 0;
     for (auto &c : conns) {
+        if (P.first_clear && (c->key_pending || !c->key_answered)) bad++;  // the *key exchange must complete
         h_c2s = fnv(h_c2s, reinterpret_cast<const uint8_t *>(&g_fd_hash[c->cfd]), 8);
         h_s2c = fnv(h_s2c, reinterpret_cast<const uint8_t *>(&g_fd_hash[c->sfd]), 8);
         b_c2s += g_fd_bytes[c->cfd];
@@ -613,13 +708,14 @@ static int run(int argc, char **argv) {
     const char *build = "reference";
 #endif
     printf("{\"build\": \"%s\", \"transport\": \"%s\", \"mode\": \"%s\", \"keylen\": %d, \"conns\": %u, "
-           "\"quests_per_conn\": %u, \"payload\": %d, \"window\": %u, \"threads\": %u, \"ok\": %s, \"error\": \"%s\", "
+           "\"quests_per_conn\": %u, \"payload\": %d, \"window\": %u, \"threads\": %u, \"first_clear\": %s, "
+           "\"ok\": %s, \"error\": \"%s\", "
            "\"seconds\": %.4f, \"echo_per_s\": %.1f, \"us_per_echo\": %.3f, \"answers_ok\": %s, \"served\": %u, "
            "\"answered\": %u, \"cycles\": %llu, \"flushes\": %llu, \"flush_s\": %.4f, "
            "\"wire_c2s_bytes\": %llu, \"wire_c2s_fnv\": \"%016llx\", \"wire_s2c_bytes\": %llu, "
            "\"wire_s2c_fnv\": \"%016llx\"}\n",
            build, tcp ? "tcp-loopback" : "socketpair", P.stream ? "stream" : "package", P.keylen, nconn, P.quests,
-           P.plen, P.window, nthr, ok ? "true" : "false", err.c_str(), dt, echoes / dt, 1e6 * dt / echoes,
+           P.plen, P.window, nthr, P.first_clear ? "true" : "false", ok ? "true" : "false", err.c_str(), dt, echoes / dt, 1e6 * dt / echoes,
            bad == 0 && ok ? "true" : "false", served, answered, (unsigned long long)cycles,
            (unsigned long long)flushes, flush_s, (unsigned long long)b_c2s, (unsigned long long)h_c2s,
            (unsigned long long)b_s2c, (unsigned long long)h_s2c);

@@ -75,10 +75,11 @@ def _multi():
         return json.load(f)["cases"]
 
 
-def _run_multi(exe, c, threads=None, timeout=600):
+def _run_multi(exe, c, threads=None, timeout=600, env=None):
     out = subprocess.run([exe, "1" if c["mode"] == "stream" else "0", str(c["keylen"]), str(c["conns"]),
                           str(c["quests_per_conn"]), str(c["payload"]), str(c["window"]),
-                          str(threads or c["threads"])], capture_output=True, text=True, timeout=timeout)
+                          str(threads or c["threads"]), "1", "1" if c.get("first_clear") else "0"],
+                         capture_output=True, text=True, timeout=timeout, env=env)
     assert out.returncode == 0, (out.returncode, out.stderr[-3000:])
     return json.loads(out.stdout.strip().splitlines()[-1])
 
@@ -102,16 +103,64 @@ def test_collector_in_reference_io_plumbing(case):
         assert ref[k] == case[k], (k, ref[k], case[k])
 
 
-def test_percall_dropin_in_reference_io_plumbing():
+@pytest.mark.parametrize("shape", ["M3", "M6", "M7"])
+def test_percall_dropin_in_reference_io_plumbing(shape):
     """The same plumbing UNCHANGED on libfpnn_aes.so (one GPU call per frame, the drop-in
-    of INTEGRATION.md section 1) on a small many-connection case: identical wire bytes."""
-    case = dict(_multi()[2])  # M3's shape, fewer quests: per-call is slow by design
+    of INTEGRATION.md section 1) on a small many-connection case: identical wire bytes.
+    M6 / M7: the clients' first frame ("*key") in the clear, SendBuffer::encryptData's skip
+    (core/IOBuffer.cpp:36-45) -- package and stream."""
+    case = dict(next(c for c in _multi() if c["name"] == shape))  # fewer quests: per-call is slow by design
     d = _run_multi(_exe("io_multi_dropin"), dict(case, quests_per_conn=2, conns=64))
     ref = _run_multi(_exe("io_multi_ref"), dict(case, quests_per_conn=2, conns=64))
     print(json.dumps({"dropin": d, "reference": ref}))
     assert d["build"] == "dropin" and d["ok"] and d["answers_ok"], d
     for k in ("wire_c2s_bytes", "wire_c2s_fnv", "wire_s2c_bytes", "wire_s2c_fnv"):
         assert d[k] == ref[k], (k, d[k], ref[k])
+
+
+@pytest.mark.parametrize("policy", ["abort", "throw"])
+@pytest.mark.parametrize("build,fail_at", [("io_multi_dropin", 400), ("io_multi_batched", 20)])
+def test_device_error_in_reference_io_plumbing(build, fail_at, policy):
+    """a device error inside FPNN's own IO code.  The reference
+    Encryptor cannot fail, so an exception escaping EncryptedPackageReceiver::fetch or
+    SendBuffer::realSend would leave the connection with its receive / send token held and
+    the IO pool would swallow it (core/ServerIOWorker.cpp:153-182,
+    base/ParamTemplateThreadPool.h:372-375): a wedged connection, nothing logged.  The
+    drop-in's contract (fpnn_amd/csrc/fail_policy.hpp): with the
+    default FPNN_AES_ON_ERROR=abort the process prints the error and aborts; with =throw
+    fpnn::EncryptorError propagates (here it leaves the IO thread: std::terminate).  Either
+    way the run ends non-zero within its time limit and names the error -- it never hangs.
+    The error is injected at the fail_at-th host data call (FPNN_AES_DEBUG_FAIL_CALL), on
+    the per-call drop-in and on the batched collector, package and stream mode."""
+    for mode in ("package", "stream"):
+        case = dict(_multi()[2] if mode == "package" else _multi()[4], quests_per_conn=2, conns=64)
+        exe = _exe(build)
+        env = dict(os.environ, FPNN_AES_DEBUG_FAIL_CALL=str(fail_at), FPNN_AES_ON_ERROR=policy)
+        try:
+            out = subprocess.run([exe, "1" if mode == "stream" else "0", str(case["keylen"]), str(case["conns"]),
+                                  str(case["quests_per_conn"]), str(case["payload"]), str(case["window"]), "2"],
+                                 capture_output=True, text=True, timeout=120, env=env)
+        except subprocess.TimeoutExpired:
+            pytest.fail(f"{build} {mode}: hung after the injected device error ({policy})")
+        print(build, mode, policy, out.returncode, out.stderr[-600:])
+        assert out.returncode != 0, (build, mode, policy, out.stdout[-500:])
+        assert "injected device error" in out.stderr, out.stderr[-2000:]
+        if policy == "abort":
+            assert out.returncode == -6 and "FPNN_AES_ON_ERROR=abort" in out.stderr, (out.returncode, out.stderr[-2000:])
+        else:
+            assert "EncryptorError" in out.stderr, out.stderr[-2000:]
+
+
+def test_device_error_in_reference_echo_throw_policy():
+    """C1's single-threaded echo through the reference SendBuffer / receivers on the drop-in
+    (oracle/io_echo.cpp) with FPNN_AES_ON_ERROR=throw: the caller that catches
+    fpnn::EncryptorError (io_echo's main, exit 9) gets it; with the default it aborts."""
+    exe = _exe("io_echo_dropin")
+    for policy, code in (("throw", 9), ("abort", -6)):
+        env = dict(os.environ, FPNN_AES_DEBUG_FAIL_CALL="50", FPNN_AES_ON_ERROR=policy)
+        out = subprocess.run([exe, "0", "32", "100", "1024", "1"], capture_output=True, text=True, timeout=120, env=env)
+        assert out.returncode == code and "injected device error" in out.stderr, (policy, out.returncode,
+                                                                                  out.stderr[-2000:])
 
 
 def _udp():

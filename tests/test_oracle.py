@@ -305,7 +305,8 @@ def test_collect_patch_keeps_reference_wire_bytes_on_cpu(case):
     exe = _ref_exe("io_multi_cpucollect")
     out = subprocess.run([exe, "1" if case["mode"] == "stream" else "0", str(case["keylen"]), str(case["conns"]),
                           str(case["quests_per_conn"]), str(case["payload"]), str(case["window"]),
-                          str(case["threads"])], capture_output=True, text=True, timeout=300)
+                          str(case["threads"]), "1", "1" if case.get("first_clear") else "0"],
+                         capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["build"] == "cpucollect" and d["ok"] and d["answers_ok"], d
