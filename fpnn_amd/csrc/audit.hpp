@@ -45,21 +45,17 @@ struct AuditTable {
     uint32_t hits;                            // violations seen
     uint32_t site, buf, block, thread, pad;   // the first one
     uint64_t addr, len, elo, ehi;             // its bytes and the extent they left
-    uint64_t slo, shi, sid;                   // the current segment's bytes and index (payload sites)
     alignas(16) uint8_t scratch[64];          // where violating accesses go instead
 };
 
 #if defined(FPNN_AES_BOUNDS) && defined(__HIP_DEVICE_COMPILE__)
 
-// (inlined by default: an out-of-line call makes every instrumented kernel keep a call frame
-// in scratch; -DFPNN_AES_AUDIT_CALL keeps the call, for comparison)
-#ifdef FPNN_AES_AUDIT_CALL
-#define FPNN_AUDIT_RECORD_ATTR __noinline__
-#else
-#define FPNN_AUDIT_RECORD_ATTR __forceinline__
-#endif
-__device__ FPNN_AUDIT_RECORD_ATTR void audit_record(AuditTable *a, uint32_t buf, uint64_t x, uint64_t n, uint64_t lo, uint64_t hi,
-                                          uint32_t site, uint64_t slo, uint64_t shi, uint64_t sid) {
+// Out of line, and as few arguments as the record needs: the checks run at every access of
+// kernels that already hold 128 VGPRs, so each extra live value is a spill.  (Recording the
+// segment's index and bounds as well, inlined or as extra arguments, doubled the audit
+// kernels' scratch and made some of them compute wrong results -- r06c/r06d)
+__device__ __noinline__ void audit_record(AuditTable *a, uint32_t buf, uint64_t x, uint64_t n, uint64_t lo, uint64_t hi,
+                                          uint32_t site) {
     if (atomicAdd(&a->hits, 1u) == 0u) {
         a->site = site;
         a->buf = buf;
@@ -69,18 +65,15 @@ __device__ FPNN_AUDIT_RECORD_ATTR void audit_record(AuditTable *a, uint32_t buf,
         a->len = n;
         a->elo = lo;
         a->ehi = hi;
-        a->slo = slo;
-        a->shi = shi;
-        a->sid = sid;
         __threadfence();
     }
 }
 
 // [x, x + n) inside [lo, hi) (no wrap: x near 2^64 must not pass)
 __device__ __forceinline__ bool audit_ok(AuditTable *a, uint32_t buf, uint64_t x, uint64_t n, uint64_t lo, uint64_t hi,
-                                         uint32_t site, uint64_t slo = 0, uint64_t shi = 0, uint64_t sid = ~0ull) {
+                                         uint32_t site) {
     if (!a || n == 0 || hi == 0 || (x >= lo && x < hi && n <= hi - x)) return true;
-    audit_record(a, buf, x, n, lo, hi, site, slo, shi, sid);
+    audit_record(a, buf, x, n, lo, hi, site);
     return false;
 }
 
@@ -95,13 +88,12 @@ __device__ __forceinline__ T *audit_at(AuditTable *a, uint32_t buf, T *p, uint64
 // p .. p + n against the batch union AND the current segment [slo, shi)
 template <class T>
 __device__ __forceinline__ T *audit_seg(AuditTable *a, uint32_t buf, T *p, uint64_t n, uint64_t slo, uint64_t shi,
-                                        uint64_t sid, uint32_t site) {
+                                        uint32_t site) {
     if (!a) return p;
     const uint64_t x = (uint64_t)(uintptr_t)p;
-    if (!audit_ok(a, buf, x, n, a->lo[buf], a->hi[buf], site, slo, shi, sid)) return reinterpret_cast<T *>(a->scratch);
-    return audit_ok(a, buf == AB_IN ? AB_SEG_IN : AB_SEG_OUT, x, n, slo, shi, site, slo, shi, sid)
-               ? p
-               : reinterpret_cast<T *>(a->scratch);
+    if (!audit_ok(a, buf, x, n, a->lo[buf], a->hi[buf], site)) return reinterpret_cast<T *>(a->scratch);
+    return audit_ok(a, buf == AB_IN ? AB_SEG_IN : AB_SEG_OUT, x, n, slo, shi, site) ? p
+                                                                                      : reinterpret_cast<T *>(a->scratch);
 }
 
 // the bytes [lo, hi) of base (the helpers store_bytes / load_bytes / *_word_bytes touch
@@ -109,22 +101,20 @@ __device__ __forceinline__ T *audit_seg(AuditTable *a, uint32_t buf, T *p, uint6
 // base whose [lo, hi) lies in the scratch bytes
 template <class T>
 __device__ __forceinline__ T *audit_rg(AuditTable *a, uint32_t buf, T *base, int lo, int hi, uint64_t slo, uint64_t shi,
-                                       uint64_t sid, uint32_t site) {
+                                       uint32_t site) {
     if (!a || lo >= hi) return base;
     const uint64_t x = (uint64_t)(uintptr_t)base + (uint64_t)(int64_t)lo;
     const uint64_t n = (uint64_t)(hi - lo);
-    if (audit_ok(a, buf, x, n, a->lo[buf], a->hi[buf], site, slo, shi, sid) &&
-        audit_ok(a, buf == AB_IN ? AB_SEG_IN : AB_SEG_OUT, x, n, slo, shi, site, slo, shi, sid))
+    if (audit_ok(a, buf, x, n, a->lo[buf], a->hi[buf], site) &&
+        audit_ok(a, buf == AB_IN ? AB_SEG_IN : AB_SEG_OUT, x, n, slo, shi, site))
         return base;
     return reinterpret_cast<T *>(a->scratch + 16 - lo);
 }
 
 #define FA_AT(B, BUF, P, N) (::fpnn_aes::audit_at((B).aud, (BUF), (P), (uint64_t)(N), __LINE__))
-// (payload sites: the segment's index a_sid is in scope beside SLO / SHI, FA_DECL)
-#define FA_SEG(B, BUF, P, N, SLO, SHI) \
-    (::fpnn_aes::audit_seg((B).aud, (BUF), (P), (uint64_t)(N), (SLO), (SHI), a_sid, __LINE__))
+#define FA_SEG(B, BUF, P, N, SLO, SHI) (::fpnn_aes::audit_seg((B).aud, (BUF), (P), (uint64_t)(N), (SLO), (SHI), __LINE__))
 #define FA_RG(B, BUF, BASE, LO, HI, SLO, SHI) \
-    (::fpnn_aes::audit_rg((B).aud, (BUF), (BASE), (int)(LO), (int)(HI), (SLO), (SHI), a_sid, __LINE__))
+    (::fpnn_aes::audit_rg((B).aud, (BUF), (BASE), (int)(LO), (int)(HI), (SLO), (SHI), __LINE__))
 // per-lane segment extents, declared and set only in the audit build
 #define FA_DECL(...) uint64_t __VA_ARGS__
 #define FA_SET(X, V) ((X) = (uint64_t)(V))

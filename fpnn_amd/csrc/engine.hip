@@ -234,8 +234,6 @@ struct fpnn_aes_engine {
     // general-layout scratch
     uint64_t *d_bstart = nullptr;
     uint64_t cap_bstart = 0;
-    uint64_t *d_wgsums = nullptr;
-    uint64_t cap_wgsums = 0;
     uint4 *d_boundary = nullptr;
     uint64_t cap_boundary = 0;
     uint4 *d_snap_iv = nullptr;  // stream-decrypt state snapshot
@@ -469,7 +467,7 @@ KBatch make_kbatch(const fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *i
     k.iv_state = iv_state;
     k.pos_state = pos_state;
     k.t0le = t0le_of(e);
-    k.eiv = e->variant.eiv ? b->keys->d_eiv : nullptr;
+    k.eiv = b->keys->d_eiv;
     return k;
 }
 
@@ -566,10 +564,9 @@ int audit_end(fpnn_aes_engine *e, int rc) {
     char buf[640];
     snprintf(buf, sizeof buf,
              "address audit: %u access(es) outside their extent; first: %s (%s) line %u, workgroup %u thread %u, "
-             "bytes [0x%llx, +%llu) against [0x%llx, 0x%llx); segment %lld [0x%llx, 0x%llx)",
+             "bytes [0x%llx, +%llu) against [0x%llx, 0x%llx)",
              t.hits, last_launched(), audit_buf_name(t.buf), t.site, t.block, t.thread, (unsigned long long)t.addr,
-             (unsigned long long)t.len, (unsigned long long)t.elo, (unsigned long long)t.ehi, (long long)t.sid,
-             (unsigned long long)t.slo, (unsigned long long)t.shi);
+             (unsigned long long)t.len, (unsigned long long)t.elo, (unsigned long long)t.ehi);
     g_last_error = buf;
     fprintf(stderr, "[fpnn_aes audit] %s\n", buf);
     return FPNN_AES_ERR_DEVICE;
@@ -604,17 +601,16 @@ int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_s
     // Few chains (fewer than the lanes of a full chip) or ragged lengths: one quad per
     // chain (K2c); otherwise one lane per chain with 8-block chunks (K2).
     const uint64_t full_chip = (uint64_t)e->num_cus * kThreads;
-    const uint64_t coop_below = e->variant.coop_below < 0 ? full_chip : (uint64_t)e->variant.coop_below;
+
     // Ragged package batches of many short frames (the caller's max_len bound): one lane
     // per chain in grid-stride order (K2) -- Q1, 2 M x 145-B quests of 16 384 keyed
     // connections: 705 against K2h's 343 GiB/s (its work-queue atomics and length-order
     // indirection per chain; profiles/r05/ab_k2_short, ab_k2_align), from one chain per
-    // GPU lane on (Variant::k2_short_min).  Without a bound K2h, which also balances
+    // GPU lane on (Q1h, 2 per lane: K2 767-770 against K2h 182-184 GiB/s,
+    // profiles/r05/ab_k2_short_min).  Without a bound K2h, which also balances
     // Zipf-like lengths (C4 on K2: 88 GiB/s).
-    const bool k2_ragged = b->len && !stream &&
-                           ((e->variant.k2_ragged && b->count >= full_chip) ||
-                            (e->variant.k2_short && b->max_len && b->max_len <= 2048 && b->count >= (uint64_t)e->variant.k2_short_min * full_chip));
-    if ((b->count < coop_below || b->len != nullptr) && !k2_ragged) {
+    const bool k2_ragged = b->len && !stream && b->max_len && b->max_len <= 2048 && b->count >= full_chip;
+    if ((b->count < full_chip || b->len != nullptr) && !k2_ragged) {
         const uint64_t lanes = 4 * b->count;
         int threads = 64;
         while (threads < kThreads && (uint64_t)threads * e->num_cus < lanes) threads *= 2;
@@ -658,9 +654,9 @@ int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_s
             h.long_bucket = length_bucket_of((uint64_t)e->variant.hyb_long);
             h.quad_waves = (uint32_t)e->variant.hyb_quad_waves;
             h.sink = e->d_sink;
-            if ((b->flags & FPNN_AES_F_WIRE_PREFIX) && !e->variant.hyb_wire_lanes) {
-                // wire frames (htole32(len) || C): every chain on quads -- the lane session's
-                // funnel-shifted, line-aligned steps measured 653 vs 800 GiB/s on R1
+            if (b->flags & FPNN_AES_F_WIRE_PREFIX) {
+                // wire frames (htole32(len) || C): every chain on quads (k_hybrid.hip's
+                // launcher takes the quads-only kernel for them)
                 h.long_bucket = 127;
                 h.quad_waves = 16;
             }
@@ -681,12 +677,10 @@ int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_s
     const int grid = (int)(want < slots ? (want ? want : 1) : slots);
     // (not for ragged batches by default, Variant::k2_align_ragged: a few 16-B aligned
     // frames per wave made the whole wave run their singles)
-    if (b->len ? e->variant.k2_align_ragged : e->variant.k2_align) k.flags |= F_ALIGN_CHUNKS;
+    if (!b->len) k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream,
-                                  (e->variant.k2_fence ? kEncFenceGeneral : 0u) |
-                                      (e->variant.k2_lane_c4 ? kEncLaneChunk4 : 0u)));
+    HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
     return timing_end(e, ev, FPNN_AES_K_ENCRYPT);
 }
 
@@ -746,16 +740,14 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
     if (layout == LAYOUT_GENERAL) {
         // K1r: block-map scan, per-wave plan and decrypt all on the device; the host
         // never learns the block total, so nothing here waits for the GPU
-        const uint64_t nwg = (b->count + 1023) / 1024;
         if ((rc = grow(e, e->d_bstart, e->cap_bstart, b->count + 1))) return rc;
-        if ((rc = grow(e, e->d_wgsums, e->cap_wgsums, nwg + 1))) return rc;
         const int grid = e->num_cus;
         if ((rc = grow(e, e->d_plan, e->cap_plan, (uint64_t)grid * (kThreads / 64)))) return rc;
         if ((rc = grow(e, e->d_sink, e->cap_sink, 2ull * grid * (kThreads / 64)))) return rc;
         if (small_map)
             HIP_TRY(launch_block_map_small(k, stream, iv_state, pos_state, e->d_snap_iv, e->d_snap_pos, e->d_bstart,
                                            e->d_total, e->stream));
-        else if (e->variant.onepass) {
+        else {
             const uint64_t words = block_map_onepass_words(b->count);
             if (words > e->cap_lookback) {  // the kernel expects zeros on first use
                 if ((rc = grow(e, e->d_lookback, e->cap_lookback, words))) return rc;
@@ -763,8 +755,7 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             }
             HIP_TRY(launch_block_map_onepass(k, stream, e->d_bstart, e->d_lookback, e->cap_lookback, e->d_fault,
                                              e->d_total, e->stream));
-        } else
-            HIP_TRY(launch_block_map_scan(k, stream, e->d_bstart, e->d_wgsums, e->d_total, e->stream));
+        }
         k.bstart = e->d_bstart;
         if (!k.in_off || !k.len) {  // K1r reads descriptor arrays: materialize the missing ones
             if (!k.in_off && (rc = grow(e, e->d_desc_off, e->cap_desc_off, b->count))) return rc;
@@ -867,20 +858,9 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     // K2h split (tests set these so that small batches exercise each session)
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
-    if (const char *v = getenv("FPNN_AES_HYB_WIRE_LANES")) e->variant.hyb_wire_lanes = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_HYB_FORCE")) e->variant.hyb_force = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_COOP_BELOW")) e->variant.coop_below = atoll(v);
-    if (const char *v = getenv("FPNN_AES_EIV")) e->variant.eiv = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_RAGGED")) e->variant.k2_ragged = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_SHORT")) e->variant.k2_short = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_SHORT_MIN")) e->variant.k2_short_min = std::max(1, atoi(v));
-    if (const char *v = getenv("FPNN_AES_K2_FENCE")) e->variant.k2_fence = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_LANE_C4")) e->variant.k2_lane_c4 = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_ALIGN_RAGGED")) e->variant.k2_align_ragged = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_K2_ALIGN")) e->variant.k2_align = atoi(v) != 0;
     if (const char *v = getenv("FPNN_AES_DEBUG_POISON_ORDER")) e->variant.poison_order = std::max(0, atoi(v));
     if (const char *v = getenv("FPNN_AES_K1R_RUNS")) e->variant.k1r_runs = atoi(v) != 0;
-    if (const char *v = getenv("FPNN_AES_ONEPASS")) e->variant.onepass = atoi(v) != 0;
     {  // stream-ordered scratch allocation from a pool of the engine's own: it keeps freed
        // memory for reuse (release threshold: never) without changing the device's
        // default pool, which other code in the process allocates from
@@ -943,7 +923,7 @@ int fpnn_aes_engine_destroy(fpnn_aes_engine *e) {
     DeviceGuard g(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     (void)hipFree(e->d_tables);
-    for (void *p : {(void *)e->d_bstart, (void *)e->d_wgsums, (void *)e->d_boundary, (void *)e->d_snap_iv,
+    for (void *p : {(void *)e->d_bstart, (void *)e->d_boundary, (void *)e->d_snap_iv,
                     (void *)e->d_snap_pos, (void *)e->d_perm, (void *)e->d_buckets,
                     (void *)e->d_fr_off, (void *)e->d_fr_slot, (void *)e->d_plan, (void *)e->d_sink,
                     (void *)e->d_desc_off, (void *)e->d_desc_len, (void *)e->d_ecdh, (void *)e->d_sstate,
@@ -1045,7 +1025,6 @@ int fpnn_aes_engine_reserve(fpnn_aes_engine *e, uint64_t max_segments, uint64_t 
     DeviceGuard g(e->device);
     int rc;
     if ((rc = grow(e, e->d_bstart, e->cap_bstart, max_segments + 1))) return rc;
-    if ((rc = grow(e, e->d_wgsums, e->cap_wgsums, (max_segments + 1023) / 1024 + 1))) return rc;
     if (block_map_onepass_words(max_segments) > e->cap_lookback) {
         if ((rc = grow(e, e->d_lookback, e->cap_lookback, block_map_onepass_words(max_segments)))) return rc;
         HIP_TRY(hipMemsetAsync(e->d_lookback, 0, e->cap_lookback * sizeof(uint64_t), e->stream));
@@ -1805,10 +1784,9 @@ HostPool *pool_of(fpnn_aes_engine *e) {
 
 // parts for `bytes` of copying: about 1 MiB per thread at least
 unsigned copy_parts(fpnn_aes_engine *e, uint64_t bytes) {
-    static const int grain = [] {  // bytes per copy thread: 2^grain (FPNN_AES_COPY_GRAIN, A/B)
-        const char *v = getenv("FPNN_AES_COPY_GRAIN");
-        return v ? std::max(12, std::min(30, atoi(v))) : 20;
-    }();
+    // 1 MiB per copy thread (256 KiB / 64 KiB grains measured within run-to-run spread on
+    // the IO-plumbing echo, profiles/r05/io_multi/r05cg_*; the A/B switch was removed in round 6)
+    constexpr int grain = 20;
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pool_of(e)->parts(), bytes >> grain));
 }
 

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
         const Seg g = get_seg<LAYOUT>(b, s);
         FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
-                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u), a_sid = s);
+                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
         const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
         if (KM == KEY_UNIFORM) {
             rk = rku;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         const uint64_t s = b.perm ? min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u) : t;  // longest chains first (ragged batches)
         const Seg g = get_seg<LAYOUT>(b, s);
         FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
-                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u), a_sid = s);
+                a_ohi = (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
         const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
         uint32_t rkq[NR + 1];
 #pragma unroll
@@ -314,41 +314,30 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 // ---------------------------------------------------------------------------
 // Launchers (runtime -> template dispatch)
 
-// The C2 shape (uniform layout, package mode) runs the fenced round (every lookup of a
-// round issued before any fold); the other layouts hold more live registers per lane and
-// keep the plain round.
+// Which K2 runs (the other sides of these choices were measured slower and removed in
+// round 6, their A/B switches with them):
+//   * package batches run the fenced round (every lookup of a round issued before any
+//     fold): C2 and, on ragged batches, R1's wire send 919-930 -> 966-975 GiB/s, Q1 +1 %
+//     (profiles/r05/ab_k2_fence_c4);
+//   * per-lane AES-128/192 keys on ragged package batches take 4-block chunks (8-block
+//     chunks spilled 14-26 VGPRs): Q1s 559-560 -> 636-638 GiB/s (same profile);
+//   * stream batches keep the plain round (more live registers per lane).
 template <int NR>
-static void enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, unsigned opts, int grid, int threads,
-                   hipStream_t st) {
-#define FPNN_ENC(L, K, S) hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, 4, 8>), dim3(grid), dim3(threads), 0, st, b)
-    const bool fence_general = opts & kEncFenceGeneral;
-    if (layout != LAYOUT_UNIFORM && km == KEY_LANE && !stream && (opts & kEncLaneChunk4) && NR != 14) {
-        // per-lane AES-128/192 round keys beside 8-block chunks spill VGPRs: 4-block chunks
-        // (measured on package batches, Q1s; stream batches keep 8)
-        if (fence_general)
-            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 4, true>), dim3(grid),
-                               dim3(threads), 0, st, b);
-        else
-            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 4>), dim3(grid),
-                               dim3(threads), 0, st, b);
-        return;
-    }
-    if (layout == LAYOUT_UNIFORM && !stream) {
-        hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_UNIFORM, KEY_UNIFORM, false, 4, 8, true>), dim3(grid),
-                           dim3(threads), 0, st, b);
-    } else if (layout == LAYOUT_UNIFORM) {
-        FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true);
-    } else if (!stream && fence_general) {  // (Variant::k2_fence: ragged package batches, A/B)
-        if (km == KEY_UNIFORM)
-            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_UNIFORM, false, 4, 8, true>), dim3(grid),
-                               dim3(threads), 0, st, b);
-        else
-            hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, LAYOUT_GENERAL, KEY_LANE, false, 4, 8, true>), dim3(grid),
-                               dim3(threads), 0, st, b);
+static void enc_nr(const KBatch &b, Layout layout, KeyMode km, bool stream, int grid, int threads, hipStream_t st) {
+#define FPNN_ENC(L, K, S, CH, F) \
+    hipLaunchKernelGGL((k_cfb_encrypt_chains<NR, L, K, S, 4, CH, F>), dim3(grid), dim3(threads), 0, st, b)
+    if (layout == LAYOUT_UNIFORM) {
+        if (stream) FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, true, 8, false);
+        else FPNN_ENC(LAYOUT_UNIFORM, KEY_UNIFORM, false, 8, true);
+    } else if (stream) {
+        if (km == KEY_UNIFORM) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true, 8, false);
+        else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true, 8, false);
     } else if (km == KEY_UNIFORM) {
-        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false);
+        FPNN_ENC(LAYOUT_GENERAL, KEY_UNIFORM, false, 8, true);
+    } else if (NR != 14) {
+        FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false, 4, true);
     } else {
-        if (stream) FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, true); else FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false);
+        FPNN_ENC(LAYOUT_GENERAL, KEY_LANE, false, 8, true);  // (AES-256 per-lane keys chunk by 4 anyway)
     }
 #undef FPNN_ENC
 }
@@ -386,12 +375,12 @@ const char *last_launched() { return g_launched; }
 void set_launched(const char *name) { g_launched = name; }
 
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
-                                 int threads, hipStream_t st, unsigned opts) {
+                                 int threads, hipStream_t st) {
     set_launched("cfb_encrypt_chains");
     switch (nrounds) {
-        case 10: enc_nr<10>(b, layout, km, stream, opts, grid, threads, st); break;
-        case 12: enc_nr<12>(b, layout, km, stream, opts, grid, threads, st); break;
-        case 14: enc_nr<14>(b, layout, km, stream, opts, grid, threads, st); break;
+        case 10: enc_nr<10>(b, layout, km, stream, grid, threads, st); break;
+        case 12: enc_nr<12>(b, layout, km, stream, grid, threads, st); break;
+        case 14: enc_nr<14>(b, layout, km, stream, grid, threads, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -16,29 +16,15 @@
 // start in the quad session, the rest in the lane session; a wave whose queue runs dry
 // joins the other one.
 //
-// Lane-session output is written in whole 128-byte lines: steps end on line boundaries
-// of the OUTPUT, and when the output is not 16-byte aligned with the blocks (the
-// htole32(len) prefix of the wire form, core/Encryptor.cpp:34-51, shifts every frame by 4)
-// each 16-byte slot is assembled from the tails and heads of two consecutive cipher blocks
-// (a funnel shift by d = out & 15 bytes, the d-byte remainder carried to the next step).
-// Only a chain's first and last slot are partial stores.
+// Lane-session steps end on 128-byte line boundaries of the OUTPUT.  Wire frames (the
+// htole32(len) prefix of core/Encryptor.cpp:34-51 puts every body 4 bytes off its blocks)
+// run on quads alone: each 16-byte output slot is assembled inside the quad from the tails
+// and heads of two consecutive cipher blocks (a funnel shift by d = out & 15 bytes).  The
+// lane session's own funnel (FPNN_AES_HYB_WIRE_LANES) was slower and was removed in round 6
+// together with its knob; it was the variant running when session r05x faulted.
 #include "coop.hpp"
 
 namespace fpnn_aes {
-
-// Bytes [16 - d, 32 - d) of the 32-byte sequence prev ‖ cur (d in 1..15): the output slot
-// whose first d bytes end the previous block.  c1/c2 = bits 0/1 of the word offset
-// (16 - d) >> 2, r = (16 - d) & 3.  20 VALU.
-__device__ __forceinline__ uint4 funnel_slot(const uint4 &prev, const uint4 &cur, bool c1, bool c2, uint32_t r) {
-    const uint32_t y[8] = {prev.x, prev.y, prev.z, prev.w, cur.x, cur.y, cur.z, cur.w};
-    uint32_t z1[7], z2[5];
-#pragma unroll
-    for (int m = 0; m < 7; m++) z1[m] = c1 ? y[m + 1] : y[m];
-#pragma unroll
-    for (int m = 0; m < 5; m++) z2[m] = c2 ? z1[m + 2] : z1[m];
-    return make_uint4(__builtin_amdgcn_alignbyte(z2[1], z2[0], r), __builtin_amdgcn_alignbyte(z2[2], z2[1], r),
-                      __builtin_amdgcn_alignbyte(z2[3], z2[2], r), __builtin_amdgcn_alignbyte(z2[4], z2[3], r));
-}
 
 // component-wise select (a ternary on uint4 makes the compiler pick a stack slot by address)
 __device__ __forceinline__ uint4 sel4(bool c, const uint4 &x, const uint4 &y) {
@@ -65,6 +51,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of m
 
 template <int NR, int KM, bool STREAM, int NT, int CH, bool SHIFT, bool FENCE, bool LANES = true>
 __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_cfb_encrypt_hybrid(KBatch b, HybridArgs h) {
+    static_assert(!(SHIFT && LANES), "wire frames run on quads alone");
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -100,16 +87,16 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     auto quad_session = [&](bool first) {
         const int q = (int)(lane & 3u);
         const int wlo = 4 * q;  // block bytes [wlo, wlo + 4) belong to this lane
+        // (per-lane keys: zero until the quad's first chain -- every lane runs the rounds,
+        // and a quad without a chain must not run them on undefined values)
         uint32_t rkq[NR + 1];
-        if (KM == KEY_UNIFORM) {
 #pragma unroll
-            for (int r = 0; r <= NR; r++) rkq[r] = b.keys[0].rk[4 * r + q];
-        }
+        for (int r = 0; r <= NR; r++) rkq[r] = KM == KEY_UNIFORM ? b.keys[0].rk[4 * r + q] : 0u;
         uint64_t sid = 0;
         const uint8_t *p = nullptr;
         uint8_t *o = nullptr;
         uint32_t nfull = 0, tail = 0, n = 0, iv = 0;
-        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0, a_sid = ~0ull);  // (audit build: the chain's own bytes)
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
         // SHIFT state: d = o & 15; the funnel's rotation kl, sources (fl, fh) and
         // byte offset r; pl / ph = the rotated words of the previous raw block, praw its
         // own word; pv / lo0 as in the lane session
@@ -137,7 +124,6 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
-            FA_SET(a_sid, s);
             FA_SET(a_ilo, (uintptr_t)g.in);
             FA_SET(a_ihi, (uintptr_t)g.in + g.len);
             FA_SET(a_olo, (uintptr_t)g.out);
@@ -386,18 +372,21 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
     };
 
     // ---------------- lane session: K2's cipher over perm[n_long, count) ----------------
+    // (never for wire frames: their outputs sit 4 bytes off the blocks, and they run on
+    // quads alone, whose in-quad funnel stores whole slots -- hybrid_nr)
     auto lane_session = [&]() {
-        RoundKeys<NR> rkl;
+        RoundKeys<NR> rkl;  // (per-lane keys: zero until the lane's first chain, as rkq above)
+        if (KM != KEY_UNIFORM) {
+#pragma unroll
+            for (int i = 0; i < 4 * (NR + 1); i++) rkl.k[i] = 0u;
+        }
         uint64_t sid = 0;
         const uint8_t *p = nullptr;
         uint8_t *o = nullptr;
-        // nfull/tail: whole blocks / bytes of the partial final block left; n: stream
-        // position; d = o & 15 (output shift against the blocks); pv = trailing bytes of
-        // prev that are this chain's own output (rewritable); lo0 = first byte of the
-        // chain's first slot that this chain may write
-        uint32_t nfull = 0, tail = 0, n = 0, d = 0, pv = 0, lo0 = 0;
-        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0, a_sid = ~0ull);  // (audit build: the chain's own bytes)
-        uint4 iv = make_uint4(0, 0, 0, 0), prev = make_uint4(0, 0, 0, 0);
+        // nfull/tail: whole blocks / bytes of the partial final block left; n: stream position
+        uint32_t nfull = 0, tail = 0, n = 0;
+        FA_DECL(a_ilo = 0, a_ihi = 0, a_olo = 0, a_ohi = 0);  // (audit build: the chain's own bytes)
+        uint4 iv = make_uint4(0, 0, 0, 0);
         bool valid = false, exhausted = false, fresh = false;
         bool at0 = false;                     // package mode: no block of the chain ciphered yet
         uint4 eivl = make_uint4(0, 0, 0, 0);  // the slot's E_k(IV) (KBatch::eiv)
@@ -405,7 +394,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
 #pragma unroll
         for (int j = 0; j < CH; j++) a[j] = nx[j] = make_uint4(0, 0, 0, 0);
         auto enc = [&](const uint4 &x) {
-            if (SHIFT || FENCE)  // (the funnel's live registers make the compiler serialize the lookups)
+            if (FENCE)
                 return KM == KEY_UNIFORM ? aes_encrypt_block_fenced<NR, NT>(x, rku, T)
                                          : aes_encrypt_block_fenced<NR, NT>(x, rkl, T);
             return KM == KEY_UNIFORM ? aes_encrypt_block<NR, NT>(x, rku, T) : aes_encrypt_block<NR, NT>(x, rkl, T);
@@ -414,11 +403,10 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint64_t s = min(*FA_AT(b, AB_PERM, b.perm + t, 4), (uint32_t)b.count - 1u);  // (in range even from a bad block)
             sid = s;
             const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
-            FA_SET(a_sid, s);
             FA_SET(a_ilo, (uintptr_t)g.in);
             FA_SET(a_ihi, (uintptr_t)g.in + g.len);
             FA_SET(a_olo, (uintptr_t)g.out);
-            FA_SET(a_ohi, (uintptr_t)g.out + g.len + ((b.flags & F_WIRE_PREFIX) ? 4u : 0u));
+            FA_SET(a_ohi, (uintptr_t)g.out + g.len);
             const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
             if (KM != KEY_UNIFORM) rkl = load_round_keys<NR>(key);
             if (STREAM) {
@@ -433,13 +421,6 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             const uint8_t *pp = g.in;
             uint8_t *oo = g.out;
             uint32_t rem = g.len;
-            pv = 0;
-            if (!STREAM && (b.flags & F_WIRE_PREFIX)) {
-                prev = make_uint4(0u, 0u, 0u, rem);  // the prefix = the 4 output bytes before the body
-                store_bytes(FA_RG(b, AB_OUT, oo - 12, 12, 16, a_olo, a_ohi), prev, 12, 16);
-                oo += 4;
-                pv = 4;
-            }
             if (STREAM && n != 0 && rem != 0) {  // finish the partially consumed keystream block
                 const uint32_t take = rem < 16 - n ? rem : 16 - n;
                 const int lo = (int)n, hi = (int)(n + take);
@@ -450,21 +431,16 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                 oo += take;
                 rem -= take;
                 n = (n + take) & 15u;
-                prev = c;
-                pv = n == 0 ? take : 0u;  // c's last `take` bytes precede oo only if the block is used up
             }
             p = pp;
             o = oo;
             nfull = rem >> 4;
             tail = rem & 15u;
-            d = (uint32_t)(uintptr_t)oo & 15u;
-            lo0 = d > pv ? d - pv : 0u;
             valid = true;
             fresh = true;
         };
         for (;;) {
-            // chains whose whole blocks are done: the shifted remainder, the partial final
-            // block, the stream state
+            // chains whose whole blocks are done: the partial final block, the stream state
             const bool fin = valid && nfull == 0;
             if (__builtin_amdgcn_ballot_w64(fin)) {
                 uint4 ks = make_uint4(0, 0, 0, 0);
@@ -476,8 +452,6 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
                         ks = enc(iv);
                 }
                 if (fin) {
-                    const uint32_t k = d < pv ? d : pv;
-                    if (SHIFT && k) store_bytes(FA_RG(b, AB_OUT, o - 16, 16 - k, 16, a_olo, a_ohi), prev, (int)(16 - k), 16);
                     if (tail) {
                         const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
                         store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
@@ -507,8 +481,8 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             if (__builtin_amdgcn_ballot_w64(valid) == 0) break;
             if (__builtin_amdgcn_ballot_w64(valid && nfull != 0) == 0) continue;  // only sub-block chains
 
-            // one step: up to CH blocks, ending on a CH*16-byte boundary of the output slots
-            const uint32_t slot0 = (uint32_t)((uintptr_t)(o - d) >> 4);
+            // one step: up to CH blocks, ending on a CH*16-byte boundary of the output
+            const uint32_t slot0 = (uint32_t)((uintptr_t)o >> 4);
             const uint32_t lim = (uint32_t)CH - (slot0 & (uint32_t)(CH - 1));
             const uint32_t kk = valid ? (nfull < lim ? nfull : lim) : 0u;
             const uint32_t rest = valid ? nfull - kk : 0u;
@@ -529,43 +503,15 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
             // takes that block's keystream from the key set (a lane at block 0 would compute
             // the same E_k(IV))
             const bool all0 = !STREAM && b.eiv && __builtin_amdgcn_ballot_w64(kk != 0 && !at0) == 0;
-            if (!SHIFT) {
 #pragma unroll
-                for (int j = 0; j < CH; j++) {
-                    const uint4 c = (j == 0 && all0 ? eivl : enc(iv)) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
-                    iv = sel4(j < (int)kk, c, iv);
-                    a[j] = c;
-                }
-#pragma unroll
-                for (int j = 0; j < CH; j++)
-                    if (j < (int)kk) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
-            } else {
-                // each block's output slot is assembled as soon as the block is ciphered
-                // (only the last raw block, prev, stays live), then the slots go out back
-                // to back; lanes with d == 0 store the blocks themselves
-                const uint32_t t = 16u - d;
-                const bool c1 = (t >> 2) & 1u, c2 = (t >> 3) & 1u;
-                const uint32_t r = t & 3u;
-#pragma unroll
-                for (int j = 0; j < CH; j++) {
-                    const uint4 c = (j == 0 && all0 ? eivl : enc(iv)) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
-                    iv = sel4(j < (int)kk, c, iv);
-                    a[j] = sel4(d != 0, funnel_slot(prev, c, c1, c2, r), c);
-                    prev = sel4(j < (int)kk, c, prev);
-                }
-#pragma unroll
-                for (int j = 0; j < CH; j++) {
-                    if (j < (int)kk) {
-                        uint8_t *dst = o - d + 16 * j;
-                        if (j == 0 && lo0 != 0) store_bytes(FA_RG(b, AB_OUT, dst, lo0, 16, a_olo, a_ohi), a[j], (int)lo0, 16);
-                        else store16(FA_SEG(b, AB_OUT, dst, 16, a_olo, a_ohi), a[j]);
-                    }
-                }
-                if (kk) {
-                    lo0 = 0;
-                    pv = 16;
-                }
+            for (int j = 0; j < CH; j++) {
+                const uint4 c = (j == 0 && all0 ? eivl : enc(iv)) ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                iv = sel4(j < (int)kk, c, iv);
+                a[j] = c;
             }
+#pragma unroll
+            for (int j = 0; j < CH; j++)
+                if (j < (int)kk) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
             if (kk) at0 = false;
             p += 16 * kk;
             o += 16 * kk;
@@ -578,7 +524,7 @@ __global__ __launch_bounds__(kThreads, 4) __attribute__((amdgpu_waves_per_eu(4, 
         }
     };
 
-    if (!LANES) {  // every chain on quads (the host routes here with quad_waves = 16)
+    if constexpr (!LANES) {  // every chain on quads (wire frames: the host routes them here)
         quad_session(true);
     } else {
         if (wave < h.quad_waves) quad_session(true);
@@ -593,19 +539,18 @@ template <int NR>
 static void hybrid_nr(const KBatch &b, const HybridArgs &h, KeyMode km, bool stream, int grid, hipStream_t st) {
 #define FPNN_HYB(K, STR, CH, SH, LN) \
     hipLaunchKernelGGL((k_cfb_encrypt_hybrid<NR, K, STR, 4, CH, SH, true, LN>), dim3(grid), dim3(kThreads), 0, st, b, h)
-    // the funnel-shifted whole-slot stores only where outputs sit off the block grid by
-    // construction (the wire prefix); other ragged outputs are stored as they fall
+    // wire frames (outputs off the block grid by construction, the 4-byte prefix): every
+    // chain on quads, whose funnel stores whole 16-byte slots -- the lane session's funnel
+    // measured 653 vs 800 GiB/s on R1 (profiles/r03/ab_r1.json) and was removed in round 6;
+    // other ragged outputs are stored as they fall
     const bool shift = !stream && (b.flags & F_WIRE_PREFIX);
-    const bool quads = shift && h.quad_waves >= 16 && h.long_bucket >= 127;  // no lane session
     if (km == KEY_UNIFORM) {
         if (stream) FPNN_HYB(KEY_UNIFORM, true, 8, false, true);
-        else if (quads) FPNN_HYB(KEY_UNIFORM, false, 8, true, false);
-        else if (shift) FPNN_HYB(KEY_UNIFORM, false, 8, true, true);
+        else if (shift) FPNN_HYB(KEY_UNIFORM, false, 8, true, false);
         else FPNN_HYB(KEY_UNIFORM, false, 8, false, true);
     } else {  // per-lane round keys (up to 60 VGPRs): half-line steps
         if (stream) FPNN_HYB(KEY_LANE, true, 4, false, true);
-        else if (quads) FPNN_HYB(KEY_LANE, false, 4, true, false);
-        else if (shift) FPNN_HYB(KEY_LANE, false, 4, true, true);
+        else if (shift) FPNN_HYB(KEY_LANE, false, 4, true, false);
         else FPNN_HYB(KEY_LANE, false, 4, false, true);
     }
 #undef FPNN_HYB

@@ -9,8 +9,6 @@ namespace fpnn_aes {
 // General-layout block map: exclusive scan of per-segment block counts.
 
 constexpr int kScanThreads = 256;
-constexpr int kScanItems = 4;
-constexpr int kScanTile = kScanThreads * kScanItems;
 
 template <bool STREAM>
 __device__ __forceinline__ uint64_t nblocks_of(const KBatch &b, uint64_t s) {
@@ -35,52 +33,9 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *s
     return incl - v;
 }
 
-template <bool STREAM>
-__global__ __launch_bounds__(kScanThreads) void k_scan_local(KBatch b, uint64_t *bstart, uint64_t *wg_sums) {
-    __shared__ uint64_t sh[kScanThreads];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-    uint64_t v[kScanItems], sum = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; k++) {
-        v[k] = nblocks_of<STREAM>(b, base + k);
-        sum += v[k];
-    }
-    uint64_t total;
-    uint64_t run = block_exclusive_scan(sum, sh, total);
-#pragma unroll
-    for (int k = 0; k < kScanItems; k++) {
-        if (base + k < b.count) bstart[base + k] = run;
-        run += v[k];
-    }
-    if (threadIdx.x == 0) wg_sums[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_scan_sums(uint64_t *wg_sums, uint64_t nwg, uint64_t *bstart,
-                                                            uint64_t count, uint64_t *total_out) {
-    __shared__ uint64_t sh[kScanThreads];
-    uint64_t carry = 0;
-    for (uint64_t base = 0; base < nwg; base += kScanThreads) {
-        const uint64_t i = base + threadIdx.x;
-        const uint64_t v = i < nwg ? wg_sums[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_exclusive_scan(v, sh, tot);
-        if (i < nwg) wg_sums[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) {
-        bstart[count] = carry;
-        *total_out = carry;
-    }
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_scan_add(uint64_t *bstart, const uint64_t *wg_sums, uint64_t count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) bstart[i] += wg_sums[i / kScanTile];
-}
-
 // Batches of up to kSmallScanMax segments (C3's 4 096 streams, R1's 16 384 connections):
 // the whole block map in ONE workgroup -- and, for stream batches, the (iv, pos) snapshot
-// the decrypt kernels read -- instead of three scan launches plus two copies; a framed
+// the decrypt kernels read -- instead of a look-back launch plus two copies; a framed
 // call is launch-bound, so this is most of its fixed cost.  The snapshot is written
 // here but the block counts read the live state (nothing has changed it yet).
 constexpr int kSmallScanThreads = 1024;
@@ -583,22 +538,6 @@ hipError_t launch_block_map_onepass(const KBatch &b, bool stream, uint64_t *bsta
     else
         hipLaunchKernelGGL((k_scan_onepass<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, lb, nwg,
                            lb_words, fault, total);
-    return hipGetLastError();
-}
-
-hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums, uint64_t *total,
-                                 hipStream_t st) {
-    const uint64_t nwg = (b.count + kScanTile - 1) / kScanTile;
-    if (nwg) {
-        if (stream)
-            hipLaunchKernelGGL((k_scan_local<true>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
-        else
-            hipLaunchKernelGGL((k_scan_local<false>), dim3((unsigned)nwg), dim3(kScanThreads), 0, st, b, bstart, wg_sums);
-    }
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kScanThreads), 0, st, wg_sums, nwg, bstart, b.count, total);
-    if (b.count)
-        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((b.count + kScanThreads - 1) / kScanThreads)),
-                           dim3(kScanThreads), 0, st, bstart, wg_sums, b.count);
     return hipGetLastError();
 }
 

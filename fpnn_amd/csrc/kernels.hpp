@@ -59,46 +59,27 @@ struct KBatch {
 enum Layout { LAYOUT_UNIFORM = 0, LAYOUT_GENERAL = 1, LAYOUT_FULL = 2 };
 enum KeyMode { KEY_UNIFORM = 0, KEY_LANE = 1 };
 
-// Per-engine dispatch settings.  Round 4 removed the measured-and-rejected kernel
-// variants (2-table LDS image, 1/4-block encrypt chunks, unfenced rounds, K2q, K1 on dense
-// batches, the separate K1r plan launch for out-of-place batches); what is left are the
-// K2h split parameters, settable per engine so that small test batches exercise each of
-// its sessions (tests/conftest.py).
+// Per-engine dispatch settings that tests set (tests/conftest.py) so that small batches
+// reach every session of the shipped kernels.  Round 4 removed the measured-and-rejected
+// kernel variants (2-table LDS image, 1/4-block encrypt chunks, unfenced rounds, K2q, K1 on
+// dense batches, the separate K1r plan launch for out-of-place batches); round 6 the A/B
+// switches whose other side was measured slower (K2h's lane-session wire funnel, the K2c
+// threshold, E_k(IV) off, K2's ragged / short-frame / fence / 4-block-chunk / line-
+// alignment switches, the three-launch block map) -- their numbers stay in DESIGN.md.
 struct Variant {
     // K2h: chains of at least hyb_long blocks (bucket-rounded) go to quads; hyb_quad_waves
     // of a workgroup's 16 waves start on them.  Round-3 sweep on C4 (profiles/r03/
     // sweep_c4_r03x.json): 1024 / 12 at 790-799 GiB/s against 738 for 512 / 8.
     int hyb_long = 1024;
     int hyb_quad_waves = 12;
-    int hyb_wire_lanes = 0;  // wire-prefix batches also use the lane session (else all quads)
-    int hyb_force = 0;       // every ragged batch of more than one chain takes K2h (tests)
-    int64_t coop_below = -1;  // uniform batches of fewer chains take K2c (-1: a full chip's lanes)
-    int eiv = 1;              // package encrypts take block 0's keystream from the key set's E_k(IV)
-    int k2_ragged = 0;        // ragged batches of a full chip's chains or more on K2 (lane per chain, grid stride)
-    int k2_short = 1;         // ... when the caller bounds the lengths (fpnn_aes_batch.max_len <= 2048)
-    // ... and the batch holds at least this many chains per GPU lane (4 until round 5's K2
-    // changes; Q1h, 2 per lane: K2h 182-184 vs K2 767-770 GiB/s, profiles/r05/ab_k2_short_min)
-    int k2_short_min = 1;
-    // K2 on ragged package batches with the fenced round (C2's): R1 wire send 919-930 -> 966-975,
-    // Q1 +1 % (profiles/r05/ab_k2_fence_c4)
-    int k2_fence = 1;
-    // K2 with per-lane AES-128/192 keys in 4-block chunks (8-block chunks spill 14-26 VGPRs):
-    // Q1s encrypt 559-560 -> 636-638 GiB/s (profiles/r05/ab_k2_fence_c4)
-    int k2_lane_c4 = 1;
-    // K2 on ragged batches: line-alignment single blocks before the chunks.  Off: the few
-    // 16-B aligned frames of a wave made all its lanes wait out their singles -- Q1 encrypt
-    // 503-504 -> 705, Q1s 642-644 -> 741-753, R1 send equal (profiles/r05/ab_k2_align)
-    int k2_align_ragged = 0;
-    int k2_align = 1;  // the same for batches without per-frame lengths (U1's 1472-B datagrams, A/B)
+    int hyb_force = 0;  // every ragged batch of more than one chain takes K2h (tests)
     // tests only: the next poison_order ragged encrypts find their length-order block's
     // counts dirty (FPNN_AES_DEBUG_POISON_ORDER), to check that the device reports it
     int poison_order = 0;
     // K1r: chunks inside one segment's interior take the lean loop (k_ragged.hip); 0 runs
-    // every chunk through the general path (FPNN_AES_K1R_RUNS=0, same-box A/B and tests)
+    // every chunk through the general path (FPNN_AES_K1R_RUNS=0: tests reach the general
+    // path at every chunk position)
     int k1r_runs = 1;
-    // large ragged block maps in one decoupled look-back launch (0: the three-launch scan;
-    // FPNN_AES_ONEPASS, same-box A/B and tests)
-    int onepass = 1;
 };
 
 // Base name ("cfb_decrypt_dense", ...) of the main kernel the last launch_* call on this
@@ -135,10 +116,7 @@ struct KScan {
 
 hipError_t launch_scan_frames(const KScan &s, bool stream, int num_cus, hipStream_t st);
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
-                                 int threads, hipStream_t st, unsigned opts = 0);
-// launch_encrypt_chains opts: the fenced round on ragged package batches (Variant::k2_fence);
-// 4-block chunks for per-lane AES-128/192 keys (Variant::k2_lane_c4)
-constexpr unsigned kEncFenceGeneral = 1u, kEncLaneChunk4 = 2u;
+                                 int threads, hipStream_t st);
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st);
@@ -181,7 +159,7 @@ hipError_t launch_length_order(const KBatch &b, bool stream, uint32_t *perm, uin
 hipError_t launch_decrypt_blocks(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool inplace, int grid,
                                  hipStream_t st);
 // K1r (k_ragged.hip): ragged decrypt with no host round trip.  b.bstart[0..count] from
-// launch_block_map_scan (bstart[count] = total blocks, device only); plan: one entry per
+// launch_block_map_onepass / _small (bstart[count] = total blocks, device only); plan: one entry per
 // wave of the grid (grid * kThreads / 64), filled by the plan kernel queued first.
 struct RaggedPlan {
     uint64_t s0;  // segment holding the wave's first block
@@ -197,11 +175,9 @@ hipError_t launch_ragged_desc(uint64_t count, uint64_t stride, uint32_t uniform_
                               hipStream_t st);
 // In-place K1 / K1d: save the ciphertext block before every 64-block chunk.
 hipError_t launch_boundary_save(const KBatch &b, uint4 *boundary, uint64_t nchunks, hipStream_t st);
-// General-layout block map: bstart[0..count] (bstart[count] = *total = total blocks, both
-// device); wg_sums scratch of ceil(count/1024) entries.
-hipError_t launch_block_map_scan(const KBatch &b, bool stream, uint64_t *bstart, uint64_t *wg_sums,
-                                 uint64_t *total, hipStream_t st);
-// The same in one launch (decoupled look-back); lb = block_map_onepass_words(count) words
+// General-layout block map: bstart[0..count], the exclusive scan of per-segment block counts
+// (bstart[count] = *total = total blocks, both device), in one launch (decoupled
+// look-back); lb = block_map_onepass_words(count) words
 // (lb_words = the buffer's capacity), zero when first used.  Everything the next launch
 // needs is kept by the kernel itself -- tickets reset and the tile-status epoch advanced by
 // its last workgroup -- so a launch captured in a graph and replayed stays correct.

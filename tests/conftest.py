@@ -85,11 +85,11 @@ def _env_engine(env):
 # of waves that start on quads set so that small test batches exercise each session:
 #   hybrid_engine       chains of >= 64 blocks on quads, 3 quad waves per workgroup
 #   hybrid_lane_engine  every chain one lane (no quad queue)
-# (both with wire-prefix batches in the lane session too; by default those go to quads)
 #   hybrid_quad_engine  every chain on quads, no quad waves at start (lane waves join)
+# (wire-prefix batches run on quads alone in every setting, as in the product)
 HYBRID_ENGINES = {
-    "hybrid_engine": {"FPNN_AES_HYB_LONG": "64", "FPNN_AES_HYB_QW": "3", "FPNN_AES_HYB_WIRE_LANES": "1"},
-    "hybrid_lane_engine": {"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2", "FPNN_AES_HYB_WIRE_LANES": "1"},
+    "hybrid_engine": {"FPNN_AES_HYB_LONG": "64", "FPNN_AES_HYB_QW": "3"},
+    "hybrid_lane_engine": {"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2"},
     "hybrid_quad_engine": {"FPNN_AES_HYB_LONG": "1", "FPNN_AES_HYB_QW": "0"},
 }
 

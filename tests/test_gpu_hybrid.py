@@ -154,7 +154,7 @@ def test_many_stream_segments(request, oracle, eng_kind, keylen):
         assert np.array_equal(_host(pos_d).astype(np.uint32), pos_h), call
 
 
-@pytest.mark.parametrize("path,wire", [("k2c", False), ("k2h", False), ("k2h", True), ("k2h_lanes", True)])
+@pytest.mark.parametrize("path,wire", [("k2c", False), ("k2h", False), ("k2h", True), ("k2h_lanes", False)])
 def test_dirty_length_order_block_reported(oracle, path, wire):
     """The length-order block must be zero when a ragged encrypt starts (kernels.hpp).  With
     its bucket counts dirtied on purpose (FPNN_AES_DEBUG_POISON_ORDER: once, before the call)
@@ -167,7 +167,7 @@ def test_dirty_length_order_block_reported(oracle, path, wire):
     if path != "k2c":
         env["FPNN_AES_HYB_FORCE"] = "1"
     if path == "k2h_lanes":
-        env.update({"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2", "FPNN_AES_HYB_WIRE_LANES": "1"})
+        env.update({"FPNN_AES_HYB_LONG": "1000000000", "FPNN_AES_HYB_QW": "2"})
     eng = _env_engine(env)
     try:
         rng = np.random.default_rng(5150 + len(path) + wire)
