@@ -7,8 +7,11 @@
  *
  * Every call runs the CFB cipher on the MI355X through the C-ABI in fpnn_aes.h
  * (per calling thread: one engine, one HIP stream, pinned staging).  Results are
- * byte-identical to the reference's.  A GPU failure throws fpnn::EncryptorError;
- * there is no CPU fallback.
+ * byte-identical to the reference's.  There is no CPU fallback.  A GPU failure aborts the
+ * process with a message (FPNN_AES_ON_ERROR=abort, the default: the reference's callers
+ * cannot fail, and an exception escaping them would leave the connection wedged with its
+ * token held); FPNN_AES_ON_ERROR=throw raises fpnn::EncryptorError instead, for callers
+ * that catch it.
  *
  * For throughput, frames should be submitted in batches (fpnn_aes_package_* /
  * fpnn_aes_stream_* in fpnn_aes.h): one GPU round trip per 1 KiB frame costs more
