@@ -170,6 +170,97 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 }
 
 // ---------------------------------------------------------------------------
+// K2s: short frames (FPNN's quests: 145-B frames from many keyed connections, the caller's
+// max_len <= kFrameMaxBytes), one lane per chain in grid-stride order like K2, but a
+// chain's whole frame is loaded at once, ciphered in registers and stored at once.
+// K2 steps through a frame in 4-block chunks; adjacent lanes' frames share their first and
+// last 128-byte lines, and with 1024 lanes per CU of ~145-B frames in flight the lines a
+// chunk touches left L2 before the chunk that needed their other half came: Q1 moved 2.35x
+// its algorithmic HBM bytes (reads 2.52x, writes 2.16x; profiles/r05/Q1s_final, VERDICT r05
+// item 3).  Here a wave's 64 frames -- one contiguous span for a collector's flush -- are
+// read by back-to-back loads and written by back-to-back stores, so every line is read
+// once and written whole while L2 still holds it.
+
+template <int NR, int KM, bool WIRE>
+__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
+    // (per-lane AES-256 round keys hold 60 VGPRs: 9 blocks a pass -- a 145-B quest is still
+    // one pass, its 1-byte tail apart -- where 10 spilled 4 VGPRs to scratch)
+    constexpr int NT = 4, MAXB = (KM == KEY_LANE && NR == 14) ? kFrameMaxBlocks - 1 : kFrameMaxBlocks;
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+
+    RoundKeys<NR> rku;
+    uint4 eiv_u = make_uint4(0, 0, 0, 0);
+    if (KM == KEY_UNIFORM) {
+        rku = load_round_keys<NR>(b.keys);
+        eiv_u = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
+    }
+    const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 272 readable bytes
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    RoundKeys<NR> rk;  // per-lane keys: kept while the lane's next chain has the same slot
+    if (KM != KEY_UNIFORM) {
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
+    }
+    uint32_t rk_slot = ~0u;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
+        const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+        FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
+                a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
+        const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
+        if (KM != KEY_UNIFORM && g.slot != rk_slot) {
+            rk = load_round_keys<NR>(key);
+            rk_slot = g.slot;
+        }
+        const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
+        uint4 iv = *reinterpret_cast<const uint4 *>(key->iv);
+        const uint8_t *p = g.in;
+        uint8_t *o = g.out;
+        const uint32_t nfull = g.len >> 4, tail = g.len & 15u;
+        if (WIRE) {  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
+            store_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
+            o += 4;
+        }
+        // MAXB blocks at a time -- a frame within the caller's bound is ONE pass: its blocks
+        // loaded back to back (lanes past their frame's blocks re-read the key table),
+        // ciphered in registers, stored back to back
+        uint32_t done = 0;
+        do {
+            const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
+            uint4 a[MAXB];
+#pragma unroll
+            for (int j = 0; j < MAXB; j++)
+                a[j] = load16(j < (int)nb ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
+                                          : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
+            // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
+            // chain here together (point 3)
+#pragma unroll
+            for (int j = 0; j < MAXB; j++) {
+                if (j < (int)nb) {
+                    const uint4 ks =
+                        j == 0 && done == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
+                    iv = ks ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                    a[j] = iv;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < MAXB; j++)
+                if (j < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
+            p += 16 * nb;
+            o += 16 * nb;
+            done += nb;
+        } while (done < nfull);
+        if (tail) {  // partial final block: its keystream from the last whole block (or E_k(IV))
+            const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
+            const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
+            store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K2c: encryption, one lane QUAD per chain.  Lane q of the quad owns state column q:
 // per round it does the 4 T-table lookups of its own 4 bytes and the quad sums the
 // contributions with DPP quad_perm (VALU only; aes_encrypt_column below).  A chain
@@ -363,6 +454,29 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
         case 10: coop_nr<10>(b, layout, km, stream, grid, threads, st); break;
         case 12: coop_nr<12>(b, layout, km, stream, grid, threads, st); break;
         case 14: coop_nr<14>(b, layout, km, stream, grid, threads, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int NR>
+static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int threads, hipStream_t st) {
+#define FPNN_FR(K, W) hipLaunchKernelGGL((k_cfb_encrypt_frames<NR, K, W>), dim3(grid), dim3(threads), 0, st, b)
+    if (km == KEY_UNIFORM) {
+        if (wire) FPNN_FR(KEY_UNIFORM, true); else FPNN_FR(KEY_UNIFORM, false);
+    } else {
+        if (wire) FPNN_FR(KEY_LANE, true); else FPNN_FR(KEY_LANE, false);
+    }
+#undef FPNN_FR
+}
+
+hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, int threads,
+                                 hipStream_t st) {
+    set_launched("cfb_encrypt_frames");
+    switch (nrounds) {
+        case 10: frames_nr<10>(b, km, wire, grid, threads, st); break;
+        case 12: frames_nr<12>(b, km, wire, grid, threads, st); break;
+        case 14: frames_nr<14>(b, km, wire, grid, threads, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

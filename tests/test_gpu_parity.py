@@ -287,9 +287,10 @@ def test_random_package_batch(request, oracle, keylen, nkeys, inplace, eng_kind)
 
 @pytest.mark.parametrize("keylen,nk", [(16, 1000), (32, 1000), (32, 1)])
 def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keylen, nk):
-    """fpnn_aes_batch.max_len: a ragged per-key package encrypt of >= 4 chains per GPU lane
+    """fpnn_aes_batch.max_len: a ragged per-key package encrypt of >= 1 chain per GPU lane
     whose lengths the caller bounds by <= 2048 bytes runs one lane per chain in grid-stride
-    order (K2) instead of the length-ordered hybrid (Q1: 491 vs 343 GiB/s).  1.1 M frames of
+    order (K2) instead of the length-ordered hybrid (Q1: 491 vs 343 GiB/s; bounds of <= 175
+    bytes take K2s, test_short_frames_whole_frame_passes).  1.1 M frames of
     1-300 bytes (sub-block, block-aligned and ragged tails) from 1000 keyed connections,
     the ciphertext against the oracle (and from one key: R1's send side); the same batch
     without the bound takes K2h and must give the same bytes."""
@@ -329,6 +330,57 @@ def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keyle
             o, ln = int(wout[i]), int(lens[i])
             assert np.array_equal(got[o:o + 4 + ln], np.concatenate(
                 [np.frombuffer(ln.to_bytes(4, "little"), np.uint8), exp[int(offs[i]):int(offs[i]) + ln]])), (bound, i)
+
+
+@pytest.mark.parametrize("keylen,nk", [(16, 1000), (24, 7), (32, 1000), (32, 1)])
+@pytest.mark.parametrize("wire", [False, True])
+def test_short_frames_whole_frame_passes(engine, oracle, keylen, nk, wire):
+    """K2s (k_cfb_encrypt_frames, round 6): ragged package encrypts whose caller bounds every
+    length by <= 175 bytes (fpnn_aes_batch.max_len; FPNN's 145-B quests) with at least one
+    chain per GPU lane load each frame whole, cipher it in registers and store it whole.
+    300 000 frames of 0-175 bytes (FPNN's 145, whole blocks, 1-15-byte tails, empty) at
+    unaligned offsets, one key or keyed connections, plain and wire frames
+    (htole32(len) || C, core/Encryptor.cpp:34-51) against the oracle -- and a few frames past
+    the bound (up to 400 B) still come out right, in several passes."""
+    import fpnn_amd
+    rng = np.random.default_rng(7700 + keylen + nk + 3 * wire)
+    n = 300_000
+    lens = rng.integers(0, 176, n).astype(np.int64)
+    pick = rng.random(n)
+    lens[pick < 0.3] = 145
+    lens[(pick >= 0.3) & (pick < 0.4)] = 16 * rng.integers(0, 11, int(((pick >= 0.3) & (pick < 0.4)).sum()))
+    over = rng.integers(0, n, 40)
+    lens[over] = rng.integers(176, 401, 40)  # (past the caller's bound)
+    gaps = rng.integers(0, 3, n)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])]).astype(np.int64) + 1
+    keys = rng.integers(0, 256, nk * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nk * 16, dtype=np.uint8)
+    slots = rng.integers(0, nk, n).astype(np.int32)
+    ks = keyset(engine, keys, keylen, ivs)
+    total = int(offs[-1] + lens[-1] + 16)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+    if nk > 1:
+        kw["key_slot"] = to_dev(slots)
+    if not wire:
+        exp = inp.copy()
+        oracle.package_batch(True, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                             key_slot=slots.astype(np.uint32) if nk > 1 else None, keys=keys, keylen=keylen, ivs=ivs,
+                             threads=8)
+        dst = to_dev(inp)
+        engine.package_encrypt(to_dev(inp), dst, n, ks, max_len=175, **kw)
+    else:
+        wout = (offs + 4 * np.arange(n) + rng.integers(0, 2, n)).astype(np.int64)
+        dst0 = rng.integers(0, 256, int(wout[-1] + lens[-1] + 4 + 16), dtype=np.uint8)
+        from test_gpu_hybrid import _wire_expected
+        exp = _wire_expected(oracle, inp, dst0, n, offs, wout, lens, slots if nk > 1 else None, keys, keylen, ivs)
+        dst = to_dev(dst0)
+        engine.package_encrypt(to_dev(inp), dst, n, ks, wire_prefix=True, max_len=175, out_off=to_dev(wout), **kw)
+    torch.cuda.synchronize()
+    assert engine.last_kernel(fpnn_amd.K_ENCRYPT) == "cfb_encrypt_frames"
+    got = to_host(dst)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
 
 
 @pytest.mark.parametrize("keylen", [16, 32])

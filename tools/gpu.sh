@@ -28,6 +28,7 @@
 #   iomulti          tools/bench_io_multi.py (echoes/s through FPNN's IO plumbing: reference vs batched)
 #   ldsprobe         tools/probe/lds_ceiling (compute-only LDS ceilings: b32 vs b64 images, bare loops)
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
+#   abframes         tools/ab_frames.py (short-frame encrypt: K2s vs K2 on Q1 / Q1s / Q1w, alternating)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
 #   trace:<cfg>      rocprofv3 kernel trace (no counters) of one bench_configs config
@@ -111,6 +112,7 @@ for step in "$@"; do
         echo "   $var=$v #$i: $(grep -h '^{"configs"' "$OUT/ab_${var}_${v}_$i.log" | cut -c1-700)"
       done; done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
+    abframes) run abframes 600 python -u tools/ab_frames.py ;;
     ldsprobe) run lds_ceiling 300 tools/probe/lds_ceiling ;;
     iomulti) run iomulti 600 python -u tools/bench_io_multi.py ;;
     k0s) run k0s 600 python -u tools/bench_k0s.py ;;  # (built on the CPU side: hipcc ... lds_ceiling.hip)
