@@ -183,9 +183,16 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
 template <int NR, int KM, bool WIRE>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
-    // (per-lane AES-256 round keys hold 60 VGPRs: 9 blocks a pass -- a 145-B quest is still
-    // one pass, its 1-byte tail apart -- where 10 spilled 4 VGPRs to scratch)
-    constexpr int NT = 4, MAXB = (KM == KEY_LANE && NR == 14) ? kFrameMaxBlocks - 1 : kFrameMaxBlocks;
+    // PF: the next chain's descriptor is loaded during this chain (below).  Per-lane round
+    // keys hold 4(NR+1) VGPRs: AES-192/256 have no room for the 6 it costs (they spilled 44 and
+    // 60 B/lane), AES-128 has with 9 blocks a pass -- a 145-B quest is still one pass, its
+    // 1-byte tail apart -- and so has AES-256 without PF (10 blocks spilled 4 VGPRs).
+#ifdef FPNN_AES_K2S_NOPF
+    constexpr bool PF = false;  // (probe build: tools/ab_frames.py A/B)
+#else
+    constexpr bool PF = !(KM == KEY_LANE && NR > 10);
+#endif
+    constexpr int NT = 4, MAXB = (KM == KEY_LANE && (NR == 14 || PF)) ? kFrameMaxBlocks - 1 : kFrameMaxBlocks;
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -205,17 +212,27 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
     }
     uint32_t rk_slot = ~0u;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
-        const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+    // With PF the next chain's descriptor is loaded during this chain, right behind this
+    // frame's loads, so a chain starts with one round trip (its frame, its E_k(IV) and -- on a
+    // slot change -- its round keys, all issued together), not two (descriptor, then the
+    // rest).  (Holding the next E_k(IV) as well costs 4 more VGPRs.)  The IV itself is never
+    // needed: block 0's keystream is E_k(IV), every later one comes from the ciphertext.
+    const uint64_t s0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t last = b.count - 1;
+    Seg gn;
+    if constexpr (PF) gn = get_seg<LAYOUT_GENERAL>(b, s0 < b.count ? s0 : last);
+    for (uint64_t s = s0; s < b.count; s += nthreads) {
+        Seg g;
+        if constexpr (PF) g = gn;
+        else g = get_seg<LAYOUT_GENERAL>(b, s);
+        const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
         FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
                 a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
-        const DevKey *key = FA_AT(b, AB_KEYS, b.keys + (KM == KEY_UNIFORM ? 0u : g.slot), sizeof(DevKey));
         if (KM != KEY_UNIFORM && g.slot != rk_slot) {
-            rk = load_round_keys<NR>(key);
+            rk = load_round_keys<NR>(FA_AT(b, AB_KEYS, b.keys + g.slot, sizeof(DevKey)));
             rk_slot = g.slot;
         }
-        const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
-        uint4 iv = *reinterpret_cast<const uint4 *>(key->iv);
+        uint4 iv = make_uint4(0, 0, 0, 0);
         const uint8_t *p = g.in;
         uint8_t *o = g.out;
         const uint32_t nfull = g.len >> 4, tail = g.len & 15u;
@@ -227,6 +244,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         // loaded back to back (lanes past their frame's blocks re-read the key table),
         // ciphered in registers, stored back to back
         uint32_t done = 0;
+        bool first = true;
         do {
             const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
             uint4 a[MAXB];
@@ -234,6 +252,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
             for (int j = 0; j < MAXB; j++)
                 a[j] = load16(j < (int)nb ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
                                           : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
+            if (PF && first) {  // the next chain's descriptor (the last chain re-reads its own)
+                const uint64_t sn = s + nthreads;
+                gn = get_seg<LAYOUT_GENERAL>(b, sn < b.count ? sn : last);
+            }
             // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
             // chain here together (point 3)
 #pragma unroll
@@ -251,6 +273,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
             p += 16 * nb;
             o += 16 * nb;
             done += nb;
+            first = false;
         } while (done < nfull);
         if (tail) {  // partial final block: its keystream from the last whole block (or E_k(IV))
             const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);

@@ -370,7 +370,7 @@ def test_short_frames_whole_frame_passes(engine, oracle, keylen, nk, wire):
         dst = to_dev(inp)
         engine.package_encrypt(to_dev(inp), dst, n, ks, max_len=175, **kw)
     else:
-        wout = (offs + 4 * np.arange(n) + rng.integers(0, 2, n)).astype(np.int64)
+        wout = (offs + 4 * np.arange(n) + np.cumsum(rng.integers(0, 2, n))).astype(np.int64)  # (never overlapping)
         dst0 = rng.integers(0, 256, int(wout[-1] + lens[-1] + 4 + 16), dtype=np.uint8)
         from test_gpu_hybrid import _wire_expected
         exp = _wire_expected(oracle, inp, dst0, n, offs, wout, lens, slots if nk > 1 else None, keys, keylen, ivs)

@@ -17,7 +17,7 @@
 #   bench            python bench.py (the contract line)
 #   bench_driver     bench.py three times with the driver's arguments (--steps 20 --warmup 5)
 #   bench_trace      bench.py under rocprofv3 --kernel-trace --stats (profiles the line's kernels)
-#   bench_pmc        bench.py under the four PMC passes (HBM bytes, LDS, VALU, waits)
+#   bench_pmc        bench.py under the five PMC passes (HBM bytes, LDS, VALU, waits, EA read sizes)
 #   configs          tools/bench_configs.py --no-host, every device config (steady-state medians)
 #   configs:<list>   the same for a comma list, e.g. configs:C4,R1
 #   host             tools/bench_configs.py --configs C2,S1 with the host / PCIe legs
@@ -28,11 +28,12 @@
 #   iomulti          tools/bench_io_multi.py (echoes/s through FPNN's IO plumbing: reference vs batched)
 #   ldsprobe         tools/probe/lds_ceiling (compute-only LDS ceilings: b32 vs b64 images, bare loops)
 #   timer            tools/timer_probe.py (bench.py vs bench_configs timing loops, one process)
-#   abframes         tools/ab_frames.py (short-frame encrypt: K2s vs K2 on Q1 / Q1s / Q1w, alternating)
+#   abframes[:<lib>] tools/ab_frames.py (short-frame encrypt: K2s vs K2 on Q1 / Q1s / Q1w, alternating),
+#                    optionally through another build of the GPU library (fpnn_amd/<lib>)
 #   percall          tools/bench_percall.py (C1's shape: per-call drop-in vs the reference)
 #   percall_trace    rocprofv3 kernel + HIP API trace of 1000 per-call encrypts + decrypts
 #   trace:<cfg>      rocprofv3 kernel trace (no counters) of one bench_configs config
-#   prof:<cfg>       rocprofv3 trace + 4 PMC passes of one bench_configs config (or ECDH)
+#   prof:<cfg>       rocprofv3 trace + 5 PMC passes of one bench_configs config (or ECDH)
 #   ecdh             tools/bench_ecdh.py
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -40,7 +41,7 @@ export TMPDIR=/tmp
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-PASSES="FETCH_SIZE|WRITE_SIZE|SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_LDS,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES|SQ_WAIT_INST_LDS,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,GRBM_GUI_ACTIVE"
+PASSES="FETCH_SIZE|WRITE_SIZE|SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_INSTS_LDS,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES|SQ_WAIT_INST_LDS,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,GRBM_GUI_ACTIVE|TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum"
 
 run() {  # run <name> <seconds> <cmd...>
   local name=$1 t=$2; shift 2
@@ -113,6 +114,7 @@ for step in "$@"; do
       done; done ;;
     timer) run timer 300 python -u tools/timer_probe.py ;;
     abframes) run abframes 600 python -u tools/ab_frames.py ;;
+    abframes:*) lib=${step#abframes:}; FPNN_AES_GPU_LIB=$PWD/fpnn_amd/$lib run "abframes_${lib%.so}" 600 python -u tools/ab_frames.py ;;
     ldsprobe) run lds_ceiling 300 tools/probe/lds_ceiling ;;
     iomulti) run iomulti 600 python -u tools/bench_io_multi.py ;;
     k0s) run k0s 600 python -u tools/bench_k0s.py ;;  # (built on the CPU side: hipcc ... lds_ceiling.hip)

@@ -3,7 +3,10 @@
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reads exactly half of the bytes of a wide coalesced streaming
-read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Each pass was
+read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  The doubling is
+calibrated on wide streaming reads only; when the fifth pass (TCC_EA0_RDREQ by request size:
+32, 64 and 128 B, gfx950 events 43-45) is present its byte count is reported as
+hbm_read_bytes_by_size and used for hbm_bytes_per_launch -- it needs no calibration.  Each pass was
 its own rocprofv3 run, so counters are averaged per kernel over that pass's
 dispatches.  Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.
 
@@ -58,6 +61,13 @@ def main():
             wr = avg["WRITE_SIZE"] * 1024
             d["hbm_read_bytes_corrected"] = rd
             d["hbm_write_bytes"] = wr
+            sized = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+            if all(c in avg for c in sized):
+                n32, n64, n128 = (avg[c] for c in sized)
+                rd = 32 * n32 + 64 * n64 + 128 * n128
+                d["hbm_read_bytes_by_size"] = rd
+                d["hbm_read_requests"] = {"32B": n32, "64B": n64, "128B": n128,
+                                          "all": avg.get("TCC_EA0_RDREQ_sum")}
             d["hbm_bytes_per_launch"] = rd + wr
             if dur:
                 d["hbm_GBs"] = round((rd + wr) / statistics.mean(dur), 1)
