@@ -100,6 +100,7 @@ SIGNATURES = {
     "fpnn_aes_pinned_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
     "fpnn_aes_pinned_free": (C.c_int, [_vp, _vp]),
     "fpnn_aes_copy_async": (C.c_int, [_vp, _vp, _vp, C.c_size_t]),
+    "fpnn_aes_engine_numa": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "fpnn_aes_engine_reserve": (C.c_int, [_vp, C.c_uint64, C.c_uint64]),
     "fpnn_aes_keyset_create": (C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int, C.POINTER(_vp)]),
     "fpnn_aes_keyset_from_schedules": (C.c_int, [_vp, C.c_uint32, C.POINTER(Schedule), _vp, C.POINTER(_vp)]),

@@ -29,6 +29,7 @@
 #include "../../include/fpnn_ecdh.h"
 #include "ecc.hpp"
 #include "hostcopy.hpp"
+#include "numa_place.hpp"
 #include "aes_common.hpp"
 #include "kernels.hpp"
 
@@ -78,6 +79,14 @@ struct CopyJob {
     uint64_t n;
 };
 
+// Pinned host memory on `node` (the engine's NUMA placement; < 0: the runtime's default).
+// hipHostMallocNumaUser makes the allocation follow the calling thread's memory policy,
+// which NumaPreferScope points at the node for the call.
+hipError_t pinned_host_alloc(int node, void **p, size_t n) {
+    fpnn_aes::NumaPreferScope prefer(node);
+    return hipHostMalloc(p, n, prefer.active() ? hipHostMallocNumaUser : 0u);
+}
+
 // One slot of the host-frame pipeline (fpnn_aes_package_host / fpnn_aes_stream_host):
 // pinned + device staging and its own stream, so the copies of one chunk overlap the
 // kernel of the other.
@@ -120,7 +129,8 @@ struct MapSlot {
 // thread start-up.  run(k, fn) calls fn(0..k-1) across the caller and k-1 workers.
 class HostPool {
 public:
-    explicit HostPool(unsigned workers) {
+    // workers run on the engine's NUMA placement (numa_place.hpp: the GPU's node's CPUs)
+    HostPool(unsigned workers, const fpnn_aes::NumaPlacement &pl) : pl_(pl) {
         for (unsigned t = 0; t < workers; t++) th_.emplace_back([this, t] { loop(t + 1); });
     }
     ~HostPool() {
@@ -186,6 +196,7 @@ public:
 
 private:
     void loop(unsigned me) {
+        (void)fpnn_aes::numa_pin_thread(pl_);
         uint64_t seen = 0;
         for (;;) {
             std::unique_lock<std::mutex> lk(mu_);
@@ -201,6 +212,7 @@ private:
         }
     }
 
+    const fpnn_aes::NumaPlacement pl_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
@@ -299,6 +311,7 @@ struct fpnn_aes_engine {
     hipStream_t map_stream = nullptr;  // host-mapped moves (both PCIe directions in one launch)
     const char *host_path = "";  // "host_staged" / "host_mapped": the last host-frame call's path
     std::unique_ptr<HostPool> pool;  // created on first use
+    fpnn_aes::NumaPlacement numa;    // where the pinned arenas and the pool's threads live
     // the address-audit build (audit.hpp): the extent table kernels check against
     AuditTable *d_aud = nullptr;
     // instrumentation
@@ -312,7 +325,7 @@ struct fpnn_aes_keyset {
     fpnn_aes_engine *e = nullptr;  // creating engine (may be destroyed before the key set)
     int device = 0;
     DevKey *d_keys = nullptr;
-    uint4 *d_eiv = nullptr;  // E_k(IV) per slot (launch_slot_eiv after every write), or null
+    uint4 *d_eiv = nullptr;  // E_k(IV) per slot (launch_slot_eiv after every write)
     uint32_t count = 0;
     int nrounds = 0;
     uint32_t keylen = 0;
@@ -859,6 +872,10 @@ int fpnn_aes_engine_create(int device, void *hip_stream, fpnn_aes_engine **out) 
     fpnn_aes_engine *e = new fpnn_aes_engine();
     e->device = device;
     e->num_cus = prop.multiProcessorCount;
+    {  // the GPU's NUMA node: pinned arenas and copy threads go there (numa_place.hpp)
+        char bdf[64] = {0};
+        e->numa = fpnn_aes::numa_placement(hipDeviceGetPCIBusId(bdf, sizeof bdf, device) == hipSuccess ? bdf : nullptr);
+    }
     // K2h split (tests set these so that small batches exercise each session)
     if (const char *v = getenv("FPNN_AES_HYB_LONG")) e->variant.hyb_long = std::max(1, atoi(v));
     if (const char *v = getenv("FPNN_AES_HYB_QW")) e->variant.hyb_quad_waves = std::min(16, std::max(0, atoi(v)));
@@ -1363,7 +1380,7 @@ int stage_reserve(fpnn_aes_engine *e, uint64_t need) {
     e->h_stage = nullptr;
     e->d_stage = nullptr;
     e->cap_stage = 0;
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_stage), n, 0));
+    HIP_TRY(pinned_host_alloc(e->numa.node, reinterpret_cast<void **>(&e->h_stage), n));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stage), n));
     e->cap_stage = n;
     return FPNN_AES_OK;
@@ -1780,7 +1797,7 @@ unsigned host_threads() {
 
 HostPool *pool_of(fpnn_aes_engine *e) {
     if (!e->pool) {
-        e->pool.reset(new HostPool(host_threads() - 1));
+        e->pool.reset(new HostPool(host_threads() - 1, e->numa));
         e->pool->set_device(e->device);
     }
     return e->pool.get();
@@ -1798,7 +1815,7 @@ void parallel_copy(fpnn_aes_engine *e, const std::vector<CopyJob> &jobs, uint64_
     pool_of(e)->copy(jobs, total, copy_parts(e, total));
 }
 
-int slot_reserve(HostSlot &s, int device, uint64_t need) {
+int slot_reserve(HostSlot &s, int node, uint64_t need) {
     if (!s.st) {
         HIP_TRY(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -1813,10 +1830,9 @@ int slot_reserve(HostSlot &s, int device, uint64_t need) {
     s.h = nullptr;
     s.d = nullptr;
     s.cap = 0;
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h), n, 0));
+    HIP_TRY(pinned_host_alloc(node, reinterpret_cast<void **>(&s.h), n));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d), n));
     s.cap = n;
-    (void)device;
     return FPNN_AES_OK;
 }
 
@@ -1883,7 +1899,7 @@ int sstate_reserve(fpnn_aes_engine *e, uint64_t bytes) {
         if (e->h_sstate) (void)hipHostFree(e->h_sstate);
         e->h_sstate = nullptr;
         e->cap_hsstate = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&e->h_sstate), c, 0));
+        HIP_TRY(pinned_host_alloc(e->numa.node, reinterpret_cast<void **>(&e->h_sstate), c));
         e->cap_hsstate = c;
     }
     return FPNN_AES_OK;
@@ -1967,7 +1983,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
     hipStream_t main_stream = e->stream;
     // order the slot streams after work already queued on the engine stream
     for (auto &sl : e->hs)
-        if (int rc = slot_reserve(sl, e->device, 0)) return rc;
+        if (int rc = slot_reserve(sl, e->numa.node, 0)) return rc;
     HIP_TRY(hipEventRecord(e->hs[0].kdone, main_stream));
     for (auto &sl : e->hs) HIP_TRY(hipStreamWaitEvent(sl.st, e->hs[0].kdone, 0));
     // ---- stream state: compact (iv, pos) of the touched streams on the device ----------
@@ -2049,7 +2065,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             out_pad = (out_b + 15) & ~15ull;
             arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
             out_at = in_pad + ((arr + 15) & ~15ull);
-            if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
+            if ((rc = slot_reserve(s, e->numa.node, in_pad + out_pad + arr + 64))) break;
             uint64_t *in_off = reinterpret_cast<uint64_t *>(s.h + in_pad);
             uint64_t *out_off = in_off + cnt;
             uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
@@ -2141,7 +2157,7 @@ int host_pipeline(fpnn_aes_engine *e, bool encrypt, bool stream, const fpnn_aes_
             out_pad = in_pad;
             arr = (uint64_t)cnt * (8 + 8 + 4 + 4);
             out_at = in_pad + ((arr + 15) & ~15ull);
-            if ((rc = slot_reserve(s, e->device, in_pad + out_pad + arr + 64))) break;
+            if ((rc = slot_reserve(s, e->numa.node, in_pad + out_pad + arr + 64))) break;
             uint64_t *in_off = reinterpret_cast<uint64_t *>(s.h + in_pad);
             uint64_t *out_off = in_off + cnt;
             uint32_t *lens = reinterpret_cast<uint32_t *>(out_off + cnt);
@@ -2287,7 +2303,7 @@ int map_view(int device, MapView &v) {
     return FPNN_AES_OK;
 }
 
-int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
+int mslot_reserve(MapSlot &m, int node, uint64_t dneed, uint64_t hneed) {
     if (!m.gathered) {
         HIP_TRY(hipEventCreateWithFlags(&m.gathered, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&m.ciphered, hipEventDisableTiming));
@@ -2308,7 +2324,7 @@ int mslot_reserve(MapSlot &m, uint64_t dneed, uint64_t hneed) {
         if (m.h) (void)hipHostFree(m.h);
         m.h = nullptr;
         m.hcap = 0;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&m.h), c, 0));
+        HIP_TRY(pinned_host_alloc(node, reinterpret_cast<void **>(&m.h), c));
         m.hcap = c;
     }
     return FPNN_AES_OK;
@@ -2339,7 +2355,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
     const double t_call = hst.on ? HostStats::now() : 0;
     DeviceGuard g(e->device);
     for (auto &m : e->ms)
-        if (int rc = mslot_reserve(m, 0, 0)) return rc;
+        if (int rc = mslot_reserve(m, e->numa.node, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
     // the move stream starts after work already queued on the engine stream
@@ -2429,7 +2445,7 @@ int mapped_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host_frame 
                 rc = hip_fail(err, "hipStreamSynchronize");
                 return false;
             }
-            if ((rc = mslot_reserve(m, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
+            if ((rc = mslot_reserve(m, e->numa.node, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
         }
         // descriptor block (same layout in h and at d + desc_at):
         //   src u64 | so u64 | dst u64 | oo u64 | len u32 | slot u32   (cnt entries each)
@@ -2605,7 +2621,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
     const double t_sorted = hst.on ? HostStats::now() : 0;
     DeviceGuard g(e->device);
     for (auto &m : e->ms)
-        if (int rc = mslot_reserve(m, 0, 0)) return rc;
+        if (int rc = mslot_reserve(m, e->numa.node, 0, 0)) return rc;
     if (!e->map_stream) HIP_TRY(hipStreamCreateWithFlags(&e->map_stream, hipStreamNonBlocking));
     hipStream_t ms = e->map_stream;
     // ---- the streams' (iv, pos), compact, on the device (engine stream) ----
@@ -2717,7 +2733,7 @@ int mapped_stream_pipeline(fpnn_aes_engine *e, bool encrypt, const fpnn_aes_host
                 rc = hip_fail(err, "hipStreamSynchronize");
                 return false;
             }
-            if ((rc = mslot_reserve(m, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
+            if ((rc = mslot_reserve(m, e->numa.node, c.desc_at + c.desc_b + 64, c.desc_b + 64))) return false;
         }
         uint64_t *h_src = reinterpret_cast<uint64_t *>(m.h);
         uint64_t *h_so = h_src + np, *h_dst = h_so + np, *h_oo = h_dst + np;
@@ -3060,7 +3076,16 @@ int fpnn_aes_pinned_alloc(fpnn_aes_engine *e, size_t bytes, void **out) {
     if (!e || !out) return FPNN_AES_ERR_ARG;
     *out = nullptr;
     DeviceGuard g(e->device);
-    HIP_TRY(hipHostMalloc(out, bytes ? bytes : 1, 0));
+    HIP_TRY(pinned_host_alloc(e->numa.node, out, bytes ? bytes : 1));
+    return FPNN_AES_OK;
+}
+
+int fpnn_aes_engine_numa(fpnn_aes_engine *e, int *node, int *device_node, int *ncpus) {
+    if (!e) return FPNN_AES_ERR_ARG;
+    if (node) *node = e->numa.node;
+    if (device_node) *device_node = e->numa.device_node;
+    if (ncpus) *ncpus = e->numa.ncpus;
+    g_last_error = e->numa.why;
     return FPNN_AES_OK;
 }
 

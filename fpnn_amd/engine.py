@@ -138,6 +138,14 @@ class Engine:
         """Base name of the kernel variant the last call queued for that direction."""
         return lib.fpnn_aes_engine_last_kernel(self._h, which).decode()
 
+    def numa(self) -> dict:
+        """The engine's NUMA placement (fpnn_aes_engine_numa): node of its pinned arenas and
+        copy threads, the GPU's node from sysfs, CPUs the threads are pinned to, and why."""
+        node, dnode, ncpus = C.c_int(), C.c_int(), C.c_int()
+        check(lib.fpnn_aes_engine_numa(self._h, C.byref(node), C.byref(dnode), C.byref(ncpus)), "engine_numa")
+        return {"node": node.value, "device_node": dnode.value, "ncpus": ncpus.value,
+                "why": lib.fpnn_aes_last_error().decode()}
+
     # -- synthetic data ------------------------------------------------------------------
     def fill_synthetic(self, dst: torch.Tensor, seed: int, byte_offset: int = 0, nbytes: Optional[int] = None):
         n = dst.numel() * dst.element_size() if nbytes is None else nbytes

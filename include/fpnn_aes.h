@@ -311,6 +311,13 @@ int fpnn_aes_pinned_alloc(fpnn_aes_engine *e, size_t bytes, void **out);
 int fpnn_aes_pinned_free(fpnn_aes_engine *e, void *p);
 int fpnn_aes_copy_async(fpnn_aes_engine *e, void *dst, const void *src, size_t bytes);
 
+/* NUMA placement of the engine's host side: `node` the node its pinned
+ * arenas (pinned_alloc, the host-frame staging) are allocated on and its copy threads run
+ * on (-1: none); `device_node` the GPU's node from sysfs (-1: unknown); `ncpus` the node's
+ * CPUs the copy threads are pinned to (0: unpinned).  fpnn_aes_last_error() then holds one
+ * line saying how the placement was chosen.  FPNN_AES_NUMA=auto|off|<node>. */
+int fpnn_aes_engine_numa(fpnn_aes_engine *e, int *node, int *device_node, int *ncpus);
+
 /* ---- synthetic data (bench/tests utility, not part of the cipher) ------------------ */
 /* dst[k] = byte (off+k)&7 of splitmix64((off+k)>>3 + seed*0xD1B54A32D192ED03), LE. */
 int fpnn_aes_fill_synthetic(fpnn_aes_engine *e, uint8_t *dst, uint64_t nbytes, uint64_t seed,
