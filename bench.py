@@ -36,12 +36,16 @@ import torch  # noqa: E402
 import workloads as W  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+# LDS: ds_read_b32 serves a wave's 64 lanes in 2 LDS cycles = 32 T-table lookups per clock
+# per CU (MI355X_MICROARCH.md, LDS table); the clock is the kernel's effective one from PMC
+LDS_PEAK_LOOKUPS = 32
+NOMINAL_CLOCK_GHZ = 2.4
 METRIC = "AES-256 GiB/s on device-resident packet batch; 1/2/4/8-GPU scaling"  # BASELINE.json "metric"
 # newest committed PMC summary of the bench command (tools/pmc_summary.py output), per workload
 # (C2: this bench command under the PMC passes, `tools/gpu.sh <tag> bench_pmc`; C4 / C5:
 # `tools/gpu.sh <tag> prof:C4` -- the same kernels on the same batches through tools/bench_configs.py)
-PMC_SUMMARIES = {"C2": "profiles/r05/bench/pmc_summary.json", "C4": "profiles/r04/C4/pmc_summary.json",
-                 "C5": "profiles/r05/C5/pmc_summary.json"}
+PMC_SUMMARIES = {"C2": ["profiles/r06/bench/pmc_summary.json", "profiles/r05/bench/pmc_summary.json"],
+                 "C4": ["profiles/r04/C4/pmc_summary.json"], "C5": ["profiles/r05/C5/pmc_summary.json"]}
 
 
 def parse():
@@ -149,20 +153,49 @@ def barrier(world):
         dist.barrier()
 
 
-def load_traffic(kernel: str, workload: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this
-    workload's bench command, and which file that was (None, None if there is none)."""
-    rel = PMC_SUMMARIES.get(workload)
-    for path in ([rel] if rel else []) + (["profiles/r01/r01h/pmc_summary.json"] if workload == "C2" else []):
+def load_pmc(kernel: str, workload: str):
+    """The newest committed PMC summary (tools/pmc_summary.py) of this workload's bench
+    command that holds `kernel`: (its per-kernel record, the file), or (None, None)."""
+    for path in PMC_SUMMARIES.get(workload, []):
         try:
             with open(os.path.join(ROOT, path)) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        v = d.get(kernel, {}).get("hbm_bytes_per_launch")
-        if v is not None:
-            return v, path
+        entry = d.get(kernel)
+        if entry and entry.get("hbm_bytes_per_launch") is not None:
+            rec = dict(d.get("kernels", {}).get(entry.get("variant"), {}))
+            rec["hbm_bytes_per_launch"] = entry["hbm_bytes_per_launch"]
+            return rec, path
     return None, None
+
+
+def lds_roofline(avg_s: float, lookups: int, num_cus: int, pmc, pmc_path) -> dict:
+    """The LDS side of the dominant kernel: T-table lookups per clock per CU against the
+    32/clk/CU ds_read_b32 peak, and the LDS-array busy fraction (SQ_LDS_IDX_ACTIVE per CU over
+    active cycles).  Clocks come from the committed PMC summary of this command (the same
+    kernel on the same batch): its GRBM_GUI_ACTIVE cycles per launch give lookups per cycle,
+    and those cycles over this run's HIP-event time give the clock this run implies.  With no
+    summary the live rate is priced at the nominal 2.4 GHz."""
+    grbm = ((pmc or {}).get("counters_avg_per_dispatch") or {}).get("GRBM_GUI_ACTIVE")
+    live_nominal = lookups / avg_s / num_cus / (NOMINAL_CLOCK_GHZ * 1e9)
+    out = {"bound": "lds", "peak": LDS_PEAK_LOOKUPS, "unit": "lookups/clk/CU", "lookups_per_launch": lookups,
+           "lookups_formula": "NR * 16 per block ciphered: decrypt kernels every 16-B block (block 0's "
+                              "keystream E_k(IV) included), encrypt kernels every block but each packet's "
+                              "first (the key set's precomputed E_k(IV))",
+           "num_cus": num_cus, "frac_at_nominal_clock": round(live_nominal / LDS_PEAK_LOOKUPS, 4)}
+    if grbm:
+        cycles = grbm / 8  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        per_clk = lookups / cycles / num_cus
+        out.update({"achieved": round(per_clk, 2), "frac": round(per_clk / LDS_PEAK_LOOKUPS, 4),
+                    "cycles_per_launch": round(cycles), "effective_clock_GHz": round(cycles / avg_s / 1e9, 3),
+                    "pmc_run_clock_GHz": pmc.get("effective_clock_GHz"),
+                    "lds_array_busy_frac": pmc.get("lds_array_busy_frac"), "source": pmc_path})
+    else:
+        out.update({"achieved": round(live_nominal, 2), "frac": round(live_nominal / LDS_PEAK_LOOKUPS, 4),
+                    "effective_clock_GHz": None, "lds_array_busy_frac": None,
+                    "source": f"nominal {NOMINAL_CLOCK_GHZ} GHz (no PMC summary of this kernel)"})
+    return out
 
 
 def _cpu_model():
@@ -338,7 +371,7 @@ def setup_c2(args, eng, world, rank):
     desc = {"workload": "C2: 1M x 1 KiB AES-256 package-mode CFB encrypt+decrypt per GPU",
             "packets_per_gpu": P, "payload_bytes": L, "key_bits": 256, "mode": "package",
             "global_packets": P * world, "parallelism": f"packet-shard x{world}"}
-    return dict(plain=plain, ks=ks, kw=kw, P=P, nkeys=1, scaling="weak", config=desc,
+    return dict(plain=plain, ks=ks, kw=kw, P=P, nkeys=1, scaling="weak", config=desc, blocks=P * ((L + 15) // 16),
                 data="synthetic (counter splitmix64 payload, seed 2; key/IV from seed 1002)",
                 key=key, iv=iv, L=L, uniform=True)
 
@@ -364,6 +397,7 @@ def setup_c4(args, eng, world, rank):
             "packets_this_rank": last - first, "global_packets": len(sizes), "global_bytes": int(sizes.sum()),
             "key_bits": 256, "mode": "package", "parallelism": f"byte-balanced packet-shard x{world}"}
     return dict(plain=plain[:nbytes], ks=ks, kw=kw, P=last - first, nkeys=1, scaling="strong", config=desc,
+                blocks=int(((sizes[first:last] + 15) // 16).sum()),
                 data="synthetic (splitmix64 payload seed 4, Zipf sizes seed 4004, key/IV seed 1004)",
                 key=key, iv=iv, L=None, uniform=False)
 
@@ -387,6 +421,7 @@ def setup_c5(args, eng, world, rank):
             "packets_this_rank": P, "global_packets": Pg, "payload_bytes": L, "key_bits": 256, "mode": "package",
             "parallelism": f"packet-shard x{world} (key table replicated)"}
     return dict(plain=plain[:P * L], ks=ks, kw=kw, P=P, nkeys=Pg, scaling="strong", config=desc,
+                blocks=P * ((L + 15) // 16),
                 data="synthetic (splitmix64 payload seed 5; keys/IVs seed 1005)", key=None, iv=None, L=L,
                 uniform=False)
 
@@ -531,11 +566,22 @@ def main():
                              "payload_GiBs": round(nbytes / avg_s / 2**30, 2)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     ach = kernels[dom]["achieved_GBs"]
-    traffic, traffic_src = load_traffic(dom, args.workload)
+    pmc, pmc_src = load_pmc(dom, args.workload)
+    avg_s = kernels[dom]["avg_ms"] / 1e3
+    # SURVEY.md 8(d)'s 28*P term prices descriptor arrays; alg_bytes counts only the arrays
+    # the call passes (C2 passes none: stride + uniform length, the kernels read none)
+    desc_term = 28 * P
+    with_desc = alg_bytes + (0 if kw.get("in_off") is not None else desc_term)
     roofline = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None, "traffic_source": pmc_src,
                 "kernel": dom, "alg_bytes_per_launch": alg_bytes,
-                "alg_bytes_formula": "2*payload + descriptor arrays passed per packet + 272*keys", "kernels": kernels}
+                "alg_bytes_formula": "2*payload + descriptor arrays passed per packet + 272*keys",
+                "descriptor_28P": {"counted": kw.get("in_off") is not None, "bytes": desc_term,
+                                   "frac_if_counted": round(with_desc / avg_s / 1e9 / HBM_PEAK_GBS, 4)},
+                "lds": lds_roofline(avg_s, (job["blocks"] - (0 if "decrypt" in dom else P)) * ks.nrounds * 16,
+                                    torch.cuda.get_device_properties(local).multi_processor_count, pmc, pmc_src),
+                "kernels": kernels}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and job["uniform"]:
