@@ -2976,14 +2976,16 @@ int fpnn_aes_stream_host(fpnn_aes_engine *e, int encrypt, const fpnn_aes_host_fr
 }
 
 // ---- one host batch over several engines (GPUs) ------------------------------------------
-// Each engine runs its share through its own host_pipeline in its own thread; errors are
-// collected and the first one (by engine index) is returned, with its message.
-static int run_multi(int n_engines, const std::function<int(int)> &fn) {
+// Each engine runs its share through its own host_pipeline in its own thread (engine 0's in
+// the caller's), on that engine's NUMA node; errors are collected and the first one (by
+// engine index) is returned, with its message.
+static int run_multi(fpnn_aes_engine *const *engines, int n_engines, const std::function<int(int)> &fn) {
     std::vector<int> rc(n_engines, FPNN_AES_OK);
     std::vector<std::string> msg(n_engines);
     std::vector<std::thread> th;
     for (int k = 1; k < n_engines; k++)
         th.emplace_back([&, k] {
+            (void)fpnn_aes::numa_pin_thread(engines[k]->numa);
             rc[k] = fn(k);
             if (rc[k]) msg[k] = g_last_error;
         });
@@ -3016,7 +3018,7 @@ int fpnn_aes_package_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_
         acc += frames[i].len;
         while (p < n_engines && acc * n_engines >= total * p) cut[p++] = i + 1;
     }
-    return run_multi(n_engines, [&](int k) {
+    return run_multi(engines, n_engines, [&](int k) {
         return fpnn_aes_package_host(engines[k], encrypt, frames + cut[k], cut[k + 1] - cut[k], keys[k], flags);
     });
 }
@@ -3050,7 +3052,7 @@ int fpnn_aes_stream_host_multi(fpnn_aes_engine *const *engines, const fpnn_aes_k
     }
     std::vector<std::vector<fpnn_aes_host_frame>> part(n_engines);
     for (uint32_t i = 0; i < n; i++) part[owner[frames[i].key_slot]].push_back(frames[i]);
-    return run_multi(n_engines, [&](int k) {
+    return run_multi(engines, n_engines, [&](int k) {
         return fpnn_aes_stream_host(engines[k], encrypt, part[k].data(), (uint32_t)part[k].size(), keys[k], iv_state,
                                     pos_state);
     });
