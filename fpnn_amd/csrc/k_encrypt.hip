@@ -183,20 +183,34 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
 template <int NR, int KM, bool WIRE>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
-    // PF: the next chain's descriptor is loaded during this chain (below).  Per-lane round
-    // keys hold 4(NR+1) VGPRs: AES-192/256 have no room for the 6 it costs (they spilled 44 and
-    // 60 B/lane), AES-128 has with 9 blocks a pass -- a 145-B quest is still one pass, its
-    // 1-byte tail apart -- and so has AES-256 without PF (10 blocks spilled 4 VGPRs).
-#ifdef FPNN_AES_K2S_NOPF
-    constexpr bool PF = false;  // (probe build: tools/ab_frames.py A/B)
+    // Per-lane AES-256 round keys hold 60 VGPRs: 9 blocks a pass there (10 spilled 4 VGPRs),
+    // so a 145-B quest is one pass plus its tail; elsewhere 10, and (but for AES-192 lane
+    // keys) the tail rides along in the pass.
+#ifdef FPNN_AES_K2S_LANE14_MAXB
+    constexpr int kLane14 = FPNN_AES_K2S_LANE14_MAXB;  // (probe build: tools/ab_frames.py)
 #else
-    constexpr bool PF = !(KM == KEY_LANE && NR > 10);
+    constexpr int kLane14 = kFrameMaxBlocks - 1;
 #endif
-    constexpr int NT = 4, MAXB = (KM == KEY_LANE && (NR == 14 || PF)) ? kFrameMaxBlocks - 1 : kFrameMaxBlocks;
+#ifdef FPNN_AES_K2S_NO_TAILSLOT
+    constexpr bool kTailSlot = false;  // (probe build)
+#else
+    constexpr bool kTailSlot = !(KM == KEY_LANE && NR > 10);  // (AES-192/256 lane keys: it spilled 32-56 B)
+#endif
+    constexpr int NT = 4, MAXB = (KM == KEY_LANE && NR == 14) ? kLane14 : kFrameMaxBlocks;
+#ifdef FPNN_AES_K2S_SPLIT
+    constexpr int H = MAXB / 2;  // (probe build) second half's loads issued behind block 0
+#else
+    constexpr int H = MAXB;
+#endif
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
     const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+#ifdef FPNN_AES_K2S_STAGGER
+    // (probe build) wave w of the CU starts w steps late, a step being about one wave's
+    // 10-block chain at the full LDS rate, so the chains' load and store bursts spread out
+    for (uint32_t i = 0; i < (threadIdx.x >> 6); i++) __builtin_amdgcn_s_sleep(NR * 5);
+#endif
 
     RoundKeys<NR> rku;
     uint4 eiv_u = make_uint4(0, 0, 0, 0);
@@ -212,19 +226,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
     }
     uint32_t rk_slot = ~0u;
-    // With PF the next chain's descriptor is loaded during this chain, right behind this
-    // frame's loads, so a chain starts with one round trip (its frame, its E_k(IV) and -- on a
-    // slot change -- its round keys, all issued together), not two (descriptor, then the
-    // rest).  (Holding the next E_k(IV) as well costs 4 more VGPRs.)  The IV itself is never
-    // needed: block 0's keystream is E_k(IV), every later one comes from the ciphertext.
-    const uint64_t s0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t last = b.count - 1;
-    Seg gn;
-    if constexpr (PF) gn = get_seg<LAYOUT_GENERAL>(b, s0 < b.count ? s0 : last);
-    for (uint64_t s = s0; s < b.count; s += nthreads) {
-        Seg g;
-        if constexpr (PF) g = gn;
-        else g = get_seg<LAYOUT_GENERAL>(b, s);
+    // (Loading the next chain's descriptor during this chain measured 5 % slower on Q1s and
+    // Q1w, r06g; the IV itself is never needed: block 0's keystream is E_k(IV), every later
+    // one comes from the ciphertext.)
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
+        const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
         const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
         FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
                 a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
@@ -242,40 +248,62 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         }
         // MAXB blocks at a time -- a frame within the caller's bound is ONE pass: its blocks
         // loaded back to back (lanes past their frame's blocks re-read the key table),
-        // ciphered in registers, stored back to back
+        // ciphered in registers, stored back to back.  A partial final block takes the next
+        // free slot of its pass: loaded with the rest as the frame's LAST 16 bytes (inside
+        // the frame, shifted down), so it costs no round trip of its own.
         uint32_t done = 0;
-        bool first = true;
+        bool tail_done = !tail;
         do {
             const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
+            const bool tin = kTailSlot && !tail_done && nfull > 0 && done + nb == nfull && nb < (uint32_t)MAXB;
             uint4 a[MAXB];
+            auto load_slot = [&](int j) {
+                return load16(j < (int)nb               ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
+                              : (tin && j == (int)nb) ? FA_SEG(b, AB_IN, p + 16 * j + tail - 16, 16, a_ilo, a_ihi)
+                                                      : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
+            };
 #pragma unroll
-            for (int j = 0; j < MAXB; j++)
-                a[j] = load16(j < (int)nb ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
-                                          : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
-            if (PF && first) {  // the next chain's descriptor (the last chain re-reads its own)
-                const uint64_t sn = s + nthreads;
-                gn = get_seg<LAYOUT_GENERAL>(b, sn < b.count ? sn : last);
-            }
+            for (int j = 0; j < H; j++) a[j] = load_slot(j);
             // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
             // chain here together (point 3)
 #pragma unroll
             for (int j = 0; j < MAXB; j++) {
+                if (H < MAXB && j == 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int k = H; k < MAXB; k++) a[k] = load_slot(k);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 if (j < (int)nb) {
                     const uint4 ks =
                         j == 0 && done == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
                     iv = ks ^ a[j];  // C_i = P_i ^ E(C_{i-1})
                     a[j] = iv;
                 }
+                if (H < MAXB && j == H - 1) {
+#pragma unroll
+                    for (int k = 0; k < H; k++)
+                        if (k < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * k, 16, a_olo, a_ohi), a[k]);
+                }
+            }
+            uint4 t = make_uint4(0, 0, 0, 0);
+            if (tin) {  // (slot nb picked by selects: one AES pass, not one per slot)
+#pragma unroll
+                for (int j = 1; j < MAXB; j++)
+                    if (j == (int)nb) t = a[j];
+                t = shr_bytes(t, 16 - (int)tail) ^ aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
             }
 #pragma unroll
-            for (int j = 0; j < MAXB; j++)
+            for (int j = H < MAXB ? H : 0; j < MAXB; j++)
                 if (j < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
+            if (tin) store_bytes(FA_RG(b, AB_OUT, o + 16 * nb, 0, tail, a_olo, a_ohi), t, 0, (int)tail);
             p += 16 * nb;
             o += 16 * nb;
             done += nb;
-            first = false;
+            tail_done |= tin;
         } while (done < nfull);
-        if (tail) {  // partial final block: its keystream from the last whole block (or E_k(IV))
+        if (!tail_done) {  // partial final block after a full pass (or a frame under 16 B):
+                           // keystream from the last whole block, or E_k(IV)
             const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
             const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
             store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
