@@ -194,14 +194,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
 #ifdef FPNN_AES_K2S_NO_TAILSLOT
     constexpr bool kTailSlot = false;  // (probe build)
 #else
-    constexpr bool kTailSlot = !(KM == KEY_LANE && NR > 10);  // (AES-192/256 lane keys: it spilled 32-56 B)
+    constexpr bool kTailSlot = true;
 #endif
     constexpr int NT = 4, MAXB = (KM == KEY_LANE && NR == 14) ? kLane14 : kFrameMaxBlocks;
-#ifdef FPNN_AES_K2S_SPLIT
-    constexpr int H = MAXB / 2;  // (probe build) second half's loads issued behind block 0
-#else
-    constexpr int H = MAXB;
-#endif
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
@@ -249,52 +244,42 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         // MAXB blocks at a time -- a frame within the caller's bound is ONE pass: its blocks
         // loaded back to back (lanes past their frame's blocks re-read the key table),
         // ciphered in registers, stored back to back.  A partial final block takes the next
-        // free slot of its pass: loaded with the rest as the frame's LAST 16 bytes (inside
-        // the frame, shifted down), so it costs no round trip of its own.
+        // free slot of its pass as a whole 16-byte block when those 16 bytes lie in one
+        // 4 KiB page (the page of its first byte, which the frame's own bytes map): it is
+        // then ciphered like the others and costs no round trip of its own (Q1s +17 %,
+        // r06h).  The bytes past the frame are read, never used or written.
         uint32_t done = 0;
         bool tail_done = !tail;
         do {
             const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
-            const bool tin = kTailSlot && !tail_done && nfull > 0 && done + nb == nfull && nb < (uint32_t)MAXB;
+            const uint64_t ta = (uint64_t)(uintptr_t)(p + 16 * nb);
+            const bool tin = kTailSlot && !tail_done && done + nb == nfull && nb < (uint32_t)MAXB &&
+                             ((ta ^ (ta + 15)) >> 12) == 0;
             uint4 a[MAXB];
             auto load_slot = [&](int j) {
                 return load16(j < (int)nb               ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
-                              : (tin && j == (int)nb) ? FA_SEG(b, AB_IN, p + 16 * j + tail - 16, 16, a_ilo, a_ihi)
+                              : (tin && j == (int)nb) ? FA_SEG(b, AB_IN, p + 16 * j, tail, a_ilo, a_ihi)
                                                       : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
             };
 #pragma unroll
-            for (int j = 0; j < H; j++) a[j] = load_slot(j);
+            for (int j = 0; j < MAXB; j++) a[j] = load_slot(j);
             // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
             // chain here together (point 3)
 #pragma unroll
             for (int j = 0; j < MAXB; j++) {
-                if (H < MAXB && j == 1) {
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int k = H; k < MAXB; k++) a[k] = load_slot(k);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (j < (int)nb) {
+                if (j < (int)nb || (tin && j == (int)nb)) {
                     const uint4 ks =
                         j == 0 && done == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
                     iv = ks ^ a[j];  // C_i = P_i ^ E(C_{i-1})
                     a[j] = iv;
                 }
-                if (H < MAXB && j == H - 1) {
-#pragma unroll
-                    for (int k = 0; k < H; k++)
-                        if (k < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * k, 16, a_olo, a_ohi), a[k]);
-                }
             }
-            uint4 t = make_uint4(0, 0, 0, 0);
-            if (tin) {  // (slot nb picked by selects: one AES pass, not one per slot)
+            uint4 t = a[0];  // the partial block's slot, picked by selects
 #pragma unroll
-                for (int j = 1; j < MAXB; j++)
-                    if (j == (int)nb) t = a[j];
-                t = shr_bytes(t, 16 - (int)tail) ^ aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
-            }
+            for (int j = 1; j < MAXB; j++)
+                if (j == (int)nb) t = a[j];
 #pragma unroll
-            for (int j = H < MAXB ? H : 0; j < MAXB; j++)
+            for (int j = 0; j < MAXB; j++)
                 if (j < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
             if (tin) store_bytes(FA_RG(b, AB_OUT, o + 16 * nb, 0, tail, a_olo, a_ohi), t, 0, (int)tail);
             p += 16 * nb;

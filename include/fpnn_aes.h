@@ -156,7 +156,9 @@ typedef struct {
     uint32_t max_len;           /* optional: an upper bound on every len_i in bytes, 0 = unknown.
                                    Ragged package encrypts of many short frames (max_len <=
                                    2048, count >= 1 chain per GPU lane, i.e. 256 CUs x 1024)
-                                   then run one lane per chain in grid-stride order (K2);
+                                   then run one lane per chain in grid-stride order (K2;
+                                   with max_len <= 175, FPNN's quests, K2s: each frame
+                                   loaded, ciphered and stored whole in one pass);
                                    without the bound, or with fewer chains, the
                                    length-ordered hybrid (K2h), whose work queue also balances
                                    Zipf-like lengths.  (Was `reserved`, 0: same layout.) */
