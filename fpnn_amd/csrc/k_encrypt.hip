@@ -183,29 +183,20 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 
 template <int NR, int KM, bool WIRE>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
-    // Per-lane AES-256 round keys hold 60 VGPRs: 9 blocks a pass there (10 spilled 4 VGPRs),
-    // so a 145-B quest is one pass plus its tail; elsewhere 10, and (but for AES-192 lane
-    // keys) the tail rides along in the pass.
-#ifdef FPNN_AES_K2S_LANE14_MAXB
-    constexpr int kLane14 = FPNN_AES_K2S_LANE14_MAXB;  // (probe build: tools/ab_frames.py)
-#else
-    constexpr int kLane14 = kFrameMaxBlocks - 1;
-#endif
+    // 10 blocks a pass: a 145-B quest's 9 whole blocks and its partial one.  (Per-lane
+    // AES-256 round keys hold 60 VGPRs, and 10 slots spill 3 VGPRs (12 B/lane) there; 9
+    // slots and a separate round trip for the tail measured 746 against 781-786 GiB/s on
+    // Q1, r06i.)
 #ifdef FPNN_AES_K2S_NO_TAILSLOT
-    constexpr bool kTailSlot = false;  // (probe build)
+    constexpr bool kTailSlot = false;  // (probe build: tools/probe/build_variant.sh)
 #else
     constexpr bool kTailSlot = true;
 #endif
-    constexpr int NT = 4, MAXB = (KM == KEY_LANE && NR == 14) ? kLane14 : kFrameMaxBlocks;
+    constexpr int NT = 4, MAXB = kFrameMaxBlocks;
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
     __syncthreads();
     const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
-#ifdef FPNN_AES_K2S_STAGGER
-    // (probe build) wave w of the CU starts w steps late, a step being about one wave's
-    // 10-block chain at the full LDS rate, so the chains' load and store bursts spread out
-    for (uint32_t i = 0; i < (threadIdx.x >> 6); i++) __builtin_amdgcn_s_sleep(NR * 5);
-#endif
 
     RoundKeys<NR> rku;
     uint4 eiv_u = make_uint4(0, 0, 0, 0);
@@ -221,9 +212,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
         for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
     }
     uint32_t rk_slot = ~0u;
-    // (Loading the next chain's descriptor during this chain measured 5 % slower on Q1s and
-    // Q1w, r06g; the IV itself is never needed: block 0's keystream is E_k(IV), every later
-    // one comes from the ciphertext.)
+    // The IV itself is never needed: block 0's keystream is E_k(IV), every later one comes
+    // from the ciphertext.  (Measured and not kept, tools/ab_frames.py: loading the next
+    // chain's descriptor during this chain, -5 % on Q1s / Q1w (r06g); the second half of a
+    // pass loaded behind block 0, -8 % (r06h); waves of a CU starting one chain-step apart,
+    // +1 % Q1s / -1 % Q1 / -3 % Q1w (r06h, r06i).)
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
         const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
         const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
