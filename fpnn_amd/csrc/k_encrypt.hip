@@ -181,17 +181,86 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 // read by back-to-back loads and written by back-to-back stores, so every line is read
 // once and written whole while L2 still holds it.
 
+// One chain of K2s: MAXB-block passes (see k_cfb_encrypt_frames).
+template <int NR, int KM, bool WIRE, int MAXB>
+__device__ __forceinline__ void frame_passes(const KBatch &b, const Seg &g, const uint4 &eiv, const RoundKeys<NR> &key,
+                                             const Tables4<4> &T, const uint8_t *dummy) {
+#ifdef FPNN_AES_K2S_NO_TAILSLOT
+    constexpr bool kTailSlot = false;  // (probe build: tools/probe/build_variant.sh)
+#else
+    constexpr bool kTailSlot = true;
+#endif
+    constexpr int NT = 4;
+    FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
+            a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
+    uint4 iv = make_uint4(0, 0, 0, 0);
+    const uint8_t *p = g.in;
+    uint8_t *o = g.out;
+    const uint32_t nfull = g.len >> 4, tail = g.len & 15u;
+    if (WIRE) {  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
+        store_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
+        o += 4;
+    }
+    // MAXB blocks at a time -- a frame within the caller's bound is ONE pass: its blocks
+    // loaded back to back (lanes past their frame's blocks re-read the key table),
+    // ciphered in registers, stored back to back.  A partial final block takes the next
+    // free slot of its pass as a whole 16-byte block when those 16 bytes lie in one
+    // 4 KiB page (the page of its first byte, which the frame's own bytes map): it is
+    // then ciphered like the others and costs no round trip of its own (Q1s +17 %,
+    // r06h).  The bytes past the frame are read, never used or written.
+    uint32_t done = 0;
+    bool tail_done = !tail;
+    do {
+        const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
+        const uint64_t ta = (uint64_t)(uintptr_t)(p + 16 * nb);
+        const bool tin = kTailSlot && !tail_done && done + nb == nfull && nb < (uint32_t)MAXB &&
+                         ((ta ^ (ta + 15)) >> 12) == 0;
+        uint4 a[MAXB];
+        auto load_slot = [&](int j) {
+            return load16(j < (int)nb               ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
+                          : (tin && j == (int)nb) ? FA_SEG(b, AB_IN, p + 16 * j, tail, a_ilo, a_ihi)
+                                                  : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
+        };
+#pragma unroll
+        for (int j = 0; j < MAXB; j++) a[j] = load_slot(j);
+        // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
+        // chain here together (point 3)
+#pragma unroll
+        for (int j = 0; j < MAXB; j++) {
+            if (j < (int)nb || (tin && j == (int)nb)) {
+                const uint4 ks =
+                    j == 0 && done == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, key, T);
+                iv = ks ^ a[j];  // C_i = P_i ^ E(C_{i-1})
+                a[j] = iv;
+            }
+        }
+        uint4 t = a[0];  // the partial block's slot, picked by selects
+#pragma unroll
+        for (int j = 1; j < MAXB; j++)
+            if (j == (int)nb) t = a[j];
+#pragma unroll
+        for (int j = 0; j < MAXB; j++)
+            if (j < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
+        if (tin) store_bytes(FA_RG(b, AB_OUT, o + 16 * nb, 0, tail, a_olo, a_ohi), t, 0, (int)tail);
+        p += 16 * nb;
+        o += 16 * nb;
+        done += nb;
+        tail_done |= tin;
+    } while (done < nfull);
+    if (!tail_done) {  // partial final block after a full pass (or a frame under 16 B):
+                       // keystream from the last whole block, or E_k(IV)
+        const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, key, T);
+        const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
+        store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
+    }
+}
+
 template <int NR, int KM, bool WIRE>
 __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
     // 10 blocks a pass: a 145-B quest's 9 whole blocks and its partial one.  (Per-lane
     // AES-256 round keys hold 60 VGPRs, and 10 slots spill 3 VGPRs (12 B/lane) there; 9
     // slots and a separate round trip for the tail measured 746 against 781-786 GiB/s on
     // Q1, r06i.)
-#ifdef FPNN_AES_K2S_NO_TAILSLOT
-    constexpr bool kTailSlot = false;  // (probe build: tools/probe/build_variant.sh)
-#else
-    constexpr bool kTailSlot = true;
-#endif
     constexpr int NT = 4, MAXB = kFrameMaxBlocks;
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
     lds_fill_tables<NT>(lds4, b.t0le);
@@ -220,72 +289,139 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
         const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
         const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
-        FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
-                a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
         if (KM != KEY_UNIFORM && g.slot != rk_slot) {
             rk = load_round_keys<NR>(FA_AT(b, AB_KEYS, b.keys + g.slot, sizeof(DevKey)));
             rk_slot = g.slot;
         }
-        uint4 iv = make_uint4(0, 0, 0, 0);
-        const uint8_t *p = g.in;
-        uint8_t *o = g.out;
-        const uint32_t nfull = g.len >> 4, tail = g.len & 15u;
-        if (WIRE) {  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
-            store_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
-            o += 4;
-        }
-        // MAXB blocks at a time -- a frame within the caller's bound is ONE pass: its blocks
-        // loaded back to back (lanes past their frame's blocks re-read the key table),
-        // ciphered in registers, stored back to back.  A partial final block takes the next
-        // free slot of its pass as a whole 16-byte block when those 16 bytes lie in one
-        // 4 KiB page (the page of its first byte, which the frame's own bytes map): it is
-        // then ciphered like the others and costs no round trip of its own (Q1s +17 %,
-        // r06h).  The bytes past the frame are read, never used or written.
-        uint32_t done = 0;
-        bool tail_done = !tail;
-        do {
-            const uint32_t nb = nfull - done < (uint32_t)MAXB ? nfull - done : (uint32_t)MAXB;
-            const uint64_t ta = (uint64_t)(uintptr_t)(p + 16 * nb);
-            const bool tin = kTailSlot && !tail_done && done + nb == nfull && nb < (uint32_t)MAXB &&
-                             ((ta ^ (ta + 15)) >> 12) == 0;
-            uint4 a[MAXB];
-            auto load_slot = [&](int j) {
-                return load16(j < (int)nb               ? FA_SEG(b, AB_IN, p + 16 * j, 16, a_ilo, a_ihi)
-                              : (tin && j == (int)nb) ? FA_SEG(b, AB_IN, p + 16 * j, tail, a_ilo, a_ihi)
-                                                      : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
-            };
+        frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2s-DB: K2s with the next chain's frame in flight while this one is ciphered.  In K2s every
+// chain starts with the same two round trips (descriptor, then frame), and the waves of a CU
+// start their chains together: at Q1's 10 blocks per chain the CU's LDS idles while 1024
+// lanes wait on 160 KiB of loads (0.61 busy, SQ_WAIT_ANY 0.51, profiles/r06/Q1).  Here the
+// next chain's descriptor is read at the top of the chain, its frame and E_k(IV) behind this
+// chain's block 1, so they land while the rounds run.  Two frames of registers per lane
+// (2 x 40 VGPRs) do not fit at 4 waves per SIMD with per-lane round keys: the kernel runs
+// OCC waves per SIMD (256 * OCC threads a workgroup, one workgroup per CU).
+//
+// A frame "fits" when its whole blocks and partial block take at most MAXB slots; its
+// partial block is then loaded as the frame's LAST 16 bytes (inside the frame) and shifted
+// down.  Frames past the caller's bound and frames under 16 B take the K2s passes.
+
+struct FrameShape {
+    uint32_t nfull, tail;
+    bool fit;
+};
+
+__device__ __forceinline__ FrameShape frame_shape(const Seg &g, int maxb) {
+    FrameShape f;
+    f.nfull = g.len >> 4;
+    f.tail = g.len & 15u;
+    f.fit = f.nfull + (f.tail ? 1u : 0u) <= (uint32_t)maxb && (f.nfull > 0 || f.tail == 0);
+    return f;
+}
+
+template <int MAXB>
+__device__ __forceinline__ void frame_issue(const KBatch &b, const Seg &g, const FrameShape &f, uint4 (&x)[MAXB],
+                                            const uint8_t *dummy) {
+    FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len);
 #pragma unroll
-            for (int j = 0; j < MAXB; j++) a[j] = load_slot(j);
-            // block 0's keystream is the slot's E_k(IV): every lane of the wave starts its
-            // chain here together (point 3)
+    for (int j = 0; j < MAXB; j++)
+        x[j] = load16(j < (int)f.nfull                   ? FA_SEG(b, AB_IN, g.in + 16 * j, 16, a_ilo, a_ihi)
+                      : (f.tail && j == (int)f.nfull) ? FA_SEG(b, AB_IN, g.in + g.len - 16, 16, a_ilo, a_ihi)
+                                                      : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
+}
+
+template <int NR, int KM, bool WIRE, int OCC>
+__global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_cfb_encrypt_frames_db(
+    KBatch b) {
+    constexpr int NT = 4, MAXB = kFrameMaxBlocks;
+    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
+    lds_fill_tables<NT>(lds4, b.t0le);
+    __syncthreads();
+    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
+
+    RoundKeys<NR> rku;
+    uint4 eiv_u = make_uint4(0, 0, 0, 0);
+    if (KM == KEY_UNIFORM) {
+        rku = load_round_keys<NR>(b.keys);
+        eiv_u = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
+    }
+    const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 272 readable bytes
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    RoundKeys<NR> rk;
+    if (KM != KEY_UNIFORM) {
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
+    }
+    uint32_t rk_slot = ~0u;
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= b.count) return;  // (no barrier below)
+    Seg g = get_seg<LAYOUT_GENERAL>(b, s);
+    FrameShape fa = frame_shape(g, MAXB);
+    uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
+    uint4 A[MAXB], B[MAXB];
+    if (fa.fit) frame_issue<MAXB>(b, g, fa, A, dummy);
+    for (;;) {
+        const uint64_t sn = s + nthreads;
+        const bool more = sn < b.count;
+        const Seg gn = get_seg<LAYOUT_GENERAL>(b, more ? sn : s);  // (read now, used behind block 1)
+        if (KM != KEY_UNIFORM && g.slot != rk_slot) {
+            rk = load_round_keys<NR>(FA_AT(b, AB_KEYS, b.keys + g.slot, sizeof(DevKey)));
+            rk_slot = g.slot;
+        }
+        FrameShape fb;
+        fb.fit = false;
+        uint4 eivn = eiv_u;
+        if (fa.fit) {
+            FA_DECL(a_olo = (uintptr_t)g.out, a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
+            uint4 iv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < MAXB; j++) {
-                if (j < (int)nb || (tin && j == (int)nb)) {
-                    const uint4 ks =
-                        j == 0 && done == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
-                    iv = ks ^ a[j];  // C_i = P_i ^ E(C_{i-1})
-                    a[j] = iv;
+                if (j == 2) {  // the next chain's frame and E_k(IV), behind this chain's block 1
+                    fb = frame_shape(gn, MAXB);
+                    fb.fit = fb.fit && more;
+                    if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
+                    if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
+                }
+                if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
+                    const uint4 ks = j == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
+                    const uint4 x = j == (int)fa.nfull ? shr_bytes(A[j], 16 - (int)fa.tail) : A[j];
+                    iv = ks ^ x;  // C_i = P_i ^ E(C_{i-1})
+                    A[j] = iv;
                 }
             }
-            uint4 t = a[0];  // the partial block's slot, picked by selects
+            uint8_t *o = g.out;
+            if (WIRE) {  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
+                store_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
+                o += 4;
+            }
+            uint4 t = A[0];  // the partial block's slot, picked by selects
 #pragma unroll
             for (int j = 1; j < MAXB; j++)
-                if (j == (int)nb) t = a[j];
+                if (j == (int)fa.nfull) t = A[j];
 #pragma unroll
             for (int j = 0; j < MAXB; j++)
-                if (j < (int)nb) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), a[j]);
-            if (tin) store_bytes(FA_RG(b, AB_OUT, o + 16 * nb, 0, tail, a_olo, a_ohi), t, 0, (int)tail);
-            p += 16 * nb;
-            o += 16 * nb;
-            done += nb;
-            tail_done |= tin;
-        } while (done < nfull);
-        if (!tail_done) {  // partial final block after a full pass (or a frame under 16 B):
-                           // keystream from the last whole block, or E_k(IV)
-            const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
-            const uint4 c = load_bytes(FA_RG(b, AB_IN, p, 0, tail, a_ilo, a_ihi), 0, (int)tail) ^ ks;
-            store_bytes(FA_RG(b, AB_OUT, o, 0, tail, a_olo, a_ohi), c, 0, (int)tail);
+                if (j < (int)fa.nfull) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), A[j]);
+            if (fa.tail)
+                store_bytes(FA_RG(b, AB_OUT, o + 16 * fa.nfull, 0, fa.tail, a_olo, a_ohi), t, 0, (int)fa.tail);
+        } else {
+            frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
+            fb = frame_shape(gn, MAXB);
+            fb.fit = fb.fit && more;
+            if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
+            if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
         }
+        if (!more) break;
+        s = sn;
+        g = gn;
+        fa = fb;
+        eiv = eivn;
+#pragma unroll
+        for (int j = 0; j < MAXB; j++) A[j] = B[j];
     }
 }
 
@@ -488,9 +624,21 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
     return hipGetLastError();
 }
 
+// K2s-DB's waves per SIMD (0: K2s; the probe builds of tools/probe/build_variant.sh set it)
+#ifndef FPNN_AES_K2S_DB_OCC
+#define FPNN_AES_K2S_DB_OCC 3
+#endif
+
 template <int NR>
 static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int threads, hipStream_t st) {
+#if FPNN_AES_K2S_DB_OCC
+    (void)threads;  // one workgroup of 256 * OCC threads per CU
+#define FPNN_FR(K, W)                                                                                          \
+    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, W, FPNN_AES_K2S_DB_OCC>), dim3(grid),                   \
+                       dim3(256 * FPNN_AES_K2S_DB_OCC), 0, st, b)
+#else
 #define FPNN_FR(K, W) hipLaunchKernelGGL((k_cfb_encrypt_frames<NR, K, W>), dim3(grid), dim3(threads), 0, st, b)
+#endif
     if (km == KEY_UNIFORM) {
         if (wire) FPNN_FR(KEY_UNIFORM, true); else FPNN_FR(KEY_UNIFORM, false);
     } else {
