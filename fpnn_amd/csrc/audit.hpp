@@ -115,9 +115,11 @@ __device__ __forceinline__ T *audit_rg(AuditTable *a, uint32_t buf, T *base, int
 #define FA_SEG(B, BUF, P, N, SLO, SHI) (::fpnn_aes::audit_seg((B).aud, (BUF), (P), (uint64_t)(N), (SLO), (SHI), __LINE__))
 #define FA_RG(B, BUF, BASE, LO, HI, SLO, SHI) \
     (::fpnn_aes::audit_rg((B).aud, (BUF), (BASE), (int)(LO), (int)(HI), (SLO), (SHI), __LINE__))
-// per-lane segment extents, declared and set only in the audit build
+// per-lane segment extents, declared and set only in the audit build (FA_ARGS passes two of
+// them to a helper)
 #define FA_DECL(...) uint64_t __VA_ARGS__
 #define FA_SET(X, V) ((X) = (uint64_t)(V))
+#define FA_ARGS(...) __VA_ARGS__
 #define FA_ON 1
 
 #else
@@ -127,6 +129,7 @@ __device__ __forceinline__ T *audit_rg(AuditTable *a, uint32_t buf, T *base, int
 #define FA_RG(B, BUF, BASE, LO, HI, SLO, SHI) (BASE)
 #define FA_DECL(...)
 #define FA_SET(X, V) ((void)0)
+#define FA_ARGS(...) 0, 0  // (extent arguments of helpers: unused in the product build)
 #define FA_ON 0
 
 #endif

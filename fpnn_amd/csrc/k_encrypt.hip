@@ -324,18 +324,36 @@ __device__ __forceinline__ FrameShape frame_shape(const Seg &g, int maxb) {
     return f;
 }
 
-template <int MAXB>
+template <int MAXB, int LO = 0, int HI = MAXB>
 __device__ __forceinline__ void frame_issue(const KBatch &b, const Seg &g, const FrameShape &f, uint4 (&x)[MAXB],
                                             const uint8_t *dummy) {
     FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len);
 #pragma unroll
-    for (int j = 0; j < MAXB; j++)
+    for (int j = LO; j < HI; j++)
         x[j] = load16(j < (int)f.nfull                   ? FA_SEG(b, AB_IN, g.in + 16 * j, 16, a_ilo, a_ihi)
                       : (f.tail && j == (int)f.nfull) ? FA_SEG(b, AB_IN, g.in + g.len - 16, 16, a_ilo, a_ihi)
                                                       : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
 }
 
-template <int NR, int KM, bool WIRE, int OCC>
+// Store slots [LO, HI) of a fitted frame: its whole blocks there, and its partial block if
+// that block's slot is there.
+template <int LO, int HI, int MAXB>
+__device__ __forceinline__ void frame_store(const KBatch &b, const uint4 (&A)[MAXB], const FrameShape &f, uint8_t *o,
+                                            uint64_t a_olo, uint64_t a_ohi) {
+    (void)a_olo;
+    (void)a_ohi;
+    uint4 t = A[LO];  // the partial block's slot, picked by selects
+#pragma unroll
+    for (int j = LO + 1; j < HI; j++)
+        if (j == (int)f.nfull) t = A[j];
+#pragma unroll
+    for (int j = LO; j < HI; j++)
+        if (j < (int)f.nfull) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), A[j]);
+    if (f.tail && (int)f.nfull >= LO && (int)f.nfull < HI)
+        store_bytes(FA_RG(b, AB_OUT, o + 16 * f.nfull, 0, f.tail, a_olo, a_ohi), t, 0, (int)f.tail);
+}
+
+template <int NR, int KM, bool WIRE, int OCC, int HS, bool RING>
 __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_cfb_encrypt_frames_db(
     KBatch b) {
     constexpr int NT = 4, MAXB = kFrameMaxBlocks;
@@ -378,13 +396,22 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
         uint4 eivn = eiv_u;
         if (fa.fit) {
             FA_DECL(a_olo = (uintptr_t)g.out, a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
+            uint8_t *const o = g.out + (WIRE ? 4 : 0);
+            if (WIRE)  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
+                store_bytes(FA_RG(b, AB_OUT, g.out, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
             uint4 iv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < MAXB; j++) {
-                if (j == 2) {  // the next chain's frame and E_k(IV), behind this chain's block 1
+                if (j == (HS ? HS : 2)) {
+                    // HS: slots [0, HS) are stored first and the next chain's frame loads into
+                    // them (one frame of registers less in flight); else it loads behind block 1
+                    if (HS) frame_store<0, HS, MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));
                     fb = frame_shape(gn, MAXB);
                     fb.fit = fb.fit && more;
-                    if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
+                    if (fb.fit) {
+                        if (RING) frame_issue<MAXB, 0, HS>(b, gn, fb, A, dummy);  // into the stored slots
+                        else frame_issue<MAXB>(b, gn, fb, B, dummy);
+                    }
                     if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
                 }
                 if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
@@ -394,25 +421,13 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
                     A[j] = iv;
                 }
             }
-            uint8_t *o = g.out;
-            if (WIRE) {  // htole32(len) || ciphertext (core/Encryptor.cpp:47-48)
-                store_bytes(FA_RG(b, AB_OUT, o, 0, 4, a_olo, a_ohi), make_uint4(g.len, 0u, 0u, 0u), 0, 4);
-                o += 4;
-            }
-            uint4 t = A[0];  // the partial block's slot, picked by selects
-#pragma unroll
-            for (int j = 1; j < MAXB; j++)
-                if (j == (int)fa.nfull) t = A[j];
-#pragma unroll
-            for (int j = 0; j < MAXB; j++)
-                if (j < (int)fa.nfull) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), A[j]);
-            if (fa.tail)
-                store_bytes(FA_RG(b, AB_OUT, o + 16 * fa.nfull, 0, fa.tail, a_olo, a_ohi), t, 0, (int)fa.tail);
+            frame_store<HS, MAXB, MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));
+            if (RING && fb.fit) frame_issue<MAXB, HS, MAXB>(b, gn, fb, A, dummy);  // the rest of the next frame
         } else {
             frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
             fb = frame_shape(gn, MAXB);
             fb.fit = fb.fit && more;
-            if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
+            if (fb.fit) frame_issue<MAXB>(b, gn, fb, RING ? A : B, dummy);
             if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
         }
         if (!more) break;
@@ -420,8 +435,10 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
         g = gn;
         fa = fb;
         eiv = eivn;
+        if (!RING) {
 #pragma unroll
-        for (int j = 0; j < MAXB; j++) A[j] = B[j];
+            for (int j = 0; j < MAXB; j++) A[j] = B[j];
+        }
     }
 }
 
@@ -626,7 +643,13 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
 
 // K2s-DB's waves per SIMD (0: K2s; the probe builds of tools/probe/build_variant.sh set it)
 #ifndef FPNN_AES_K2S_DB_OCC
-#define FPNN_AES_K2S_DB_OCC 3
+#define FPNN_AES_K2S_DB_OCC 2
+#endif
+#ifndef FPNN_AES_K2S_DB_HS
+#define FPNN_AES_K2S_DB_HS 0
+#endif
+#ifndef FPNN_AES_K2S_DB_RING
+#define FPNN_AES_K2S_DB_RING 0
 #endif
 
 template <int NR>
@@ -634,7 +657,7 @@ static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int thre
 #if FPNN_AES_K2S_DB_OCC
     (void)threads;  // one workgroup of 256 * OCC threads per CU
 #define FPNN_FR(K, W)                                                                                          \
-    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, W, FPNN_AES_K2S_DB_OCC>), dim3(grid),                   \
+    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, W, FPNN_AES_K2S_DB_OCC, FPNN_AES_K2S_DB_HS, FPNN_AES_K2S_DB_RING>), dim3(grid), \
                        dim3(256 * FPNN_AES_K2S_DB_OCC), 0, st, b)
 #else
 #define FPNN_FR(K, W) hipLaunchKernelGGL((k_cfb_encrypt_frames<NR, K, W>), dim3(grid), dim3(threads), 0, st, b)
