@@ -754,6 +754,16 @@ int run_decrypt(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_state, 
             k.magic = magic_for((uint32_t)nb);
         }
     }
+    // Ragged package batches of FPNN's quests (the caller's max_len bound, at least one frame
+    // per GPU lane): one lane per frame, its blocks decrypted as independent AES passes from
+    // registers (D2s).  K1r's 64-block chunks span ~7 frames and key slots there.
+    if (layout == LAYOUT_GENERAL && !stream && b->len && b->max_len && b->max_len <= kFrameMaxBytes &&
+        b->count >= (uint64_t)e->num_cus * kThreads) {
+        EventPair *ev = nullptr;
+        if ((rc = timing_begin(e, FPNN_AES_K_DECRYPT, &ev))) return rc;
+        HIP_TRY(launch_decrypt_frames(k, b->keys->nrounds, km, e->num_cus, e->stream));
+        return timing_end(e, ev, FPNN_AES_K_DECRYPT);
+    }
     if (layout == LAYOUT_GENERAL) {
         // K1r: block-map scan, per-wave plan and decrypt all on the device; the host
         // never learns the block total, so nothing here waits for the GPU

@@ -353,7 +353,31 @@ __device__ __forceinline__ void frame_store(const KBatch &b, const uint4 (&A)[MA
         store_bytes(FA_RG(b, AB_OUT, o + 16 * f.nfull, 0, f.tail, a_olo, a_ohi), t, 0, (int)f.tail);
 }
 
-template <int NR, int KM, bool WIRE, int OCC, int HS, bool RING>
+// One chain of a decrypt past the bound (or under 16 B): block by block.  P_i = C_i ^
+// E(C_{i-1}), P_0 = C_0 ^ E_k(IV).
+template <int NR>
+__device__ __forceinline__ void frame_decrypt_blocks(const KBatch &b, const Seg &g, const uint4 &eiv,
+                                                     const RoundKeys<NR> &key, const Tables4<4> &T) {
+    FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
+            a_ohi = (uintptr_t)g.out + g.len);
+    const uint32_t nfull = g.len >> 4, tail = g.len & 15u;
+    uint4 prev = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = 0; i < nfull; i++) {
+        const uint4 c = load16(FA_SEG(b, AB_IN, g.in + 16 * i, 16, a_ilo, a_ihi));
+        const uint4 ks = i == 0 ? eiv : aes_encrypt_block<NR, 4>(prev, key, T);
+        store16(FA_SEG(b, AB_OUT, g.out + 16 * i, 16, a_olo, a_ohi), c ^ ks);
+        prev = c;
+    }
+    if (tail) {
+        const uint4 ks = nfull == 0 ? eiv : aes_encrypt_block<NR, 4>(prev, key, T);
+        const uint4 c = load_bytes(FA_RG(b, AB_IN, g.in + 16 * nfull, 0, tail, a_ilo, a_ihi), 0, (int)tail);
+        store_bytes(FA_RG(b, AB_OUT, g.out + 16 * nfull, 0, tail, a_olo, a_ohi), c ^ ks, 0, (int)tail);
+    }
+}
+
+// DEC: the same pipeline decrypts (D2s): block j's keystream is E(C_{j-1}), the ciphertext
+// just loaded, so a lane's AES passes are independent of each other.
+template <int NR, int KM, bool WIRE, int OCC, int HS, bool RING, bool DEC = false>
 __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_cfb_encrypt_frames_db(
     KBatch b) {
     constexpr int NT = 4, MAXB = kFrameMaxBlocks;
@@ -417,14 +441,20 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
                 if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
                     const uint4 ks = j == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
                     const uint4 x = j == (int)fa.nfull ? shr_bytes(A[j], 16 - (int)fa.tail) : A[j];
-                    iv = ks ^ x;  // C_i = P_i ^ E(C_{i-1})
-                    A[j] = iv;
+                    if (DEC) {  // P_i = C_i ^ E(C_{i-1}); iv carries the ciphertext
+                        A[j] = x ^ ks;
+                        iv = x;
+                    } else {  // C_i = P_i ^ E(C_{i-1})
+                        iv = ks ^ x;
+                        A[j] = iv;
+                    }
                 }
             }
             frame_store<HS, MAXB, MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));
             if (RING && fb.fit) frame_issue<MAXB, HS, MAXB>(b, gn, fb, A, dummy);  // the rest of the next frame
         } else {
-            frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
+            if (DEC) frame_decrypt_blocks<NR>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T);
+            else frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
             fb = frame_shape(gn, MAXB);
             fb.fit = fb.fit && more;
             if (fb.fit) frame_issue<MAXB>(b, gn, fb, RING ? A : B, dummy);
@@ -651,6 +681,10 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
 #ifndef FPNN_AES_K2S_DB_RING
 #define FPNN_AES_K2S_DB_RING 0
 #endif
+// D2s's waves per SIMD (probe builds set it)
+#ifndef FPNN_AES_D2S_OCC
+#define FPNN_AES_D2S_OCC 2
+#endif
 
 template <int NR>
 static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int threads, hipStream_t st) {
@@ -668,6 +702,27 @@ static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int thre
         if (wire) FPNN_FR(KEY_LANE, true); else FPNN_FR(KEY_LANE, false);
     }
 #undef FPNN_FR
+}
+
+template <int NR>
+static void dframes_nr(const KBatch &b, KeyMode km, int grid, hipStream_t st) {
+#define FPNN_DF(K)                                                                                               \
+    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, false, FPNN_AES_D2S_OCC, 0, false, true>), dim3(grid),   \
+                       dim3(256 * FPNN_AES_D2S_OCC), 0, st, b)
+    if (km == KEY_UNIFORM) FPNN_DF(KEY_UNIFORM);
+    else FPNN_DF(KEY_LANE);
+#undef FPNN_DF
+}
+
+hipError_t launch_decrypt_frames(const KBatch &b, int nrounds, KeyMode km, int grid, hipStream_t st) {
+    set_launched("cfb_decrypt_frames");
+    switch (nrounds) {
+        case 10: dframes_nr<10>(b, km, grid, st); break;
+        case 12: dframes_nr<12>(b, km, grid, st); break;
+        case 14: dframes_nr<14>(b, km, grid, st); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, int threads,

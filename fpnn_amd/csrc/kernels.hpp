@@ -124,6 +124,9 @@ constexpr int kFrameMaxBlocks = 10;
 constexpr uint32_t kFrameMaxBytes = 16u * kFrameMaxBlocks + 15u;  // 175: FPNN's 145-B quests and shorter
 hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, int threads,
                                  hipStream_t st);
+// D2s: the same pipeline for package decrypts of short frames (one lane per frame, its
+// blocks' AES passes independent of each other); grid = one workgroup per CU
+hipError_t launch_decrypt_frames(const KBatch &b, int nrounds, KeyMode km, int grid, hipStream_t st);
 // K2c: one 4-lane quad per chain (few / long chains); threads = workgroup size.
 hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                int threads, hipStream_t st);

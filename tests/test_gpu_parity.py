@@ -383,6 +383,60 @@ def test_short_frames_whole_frame_passes(engine, oracle, keylen, nk, wire):
     assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
 
 
+@pytest.mark.parametrize("keylen,nk", [(16, 1000), (24, 7), (32, 1000), (32, 1)])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_short_frames_decrypt_whole_frames(engine, oracle, keylen, nk, inplace):
+    """D2s (k_cfb_encrypt_frames_db<..., DEC>, round 6): ragged package decrypts whose caller
+    bounds every length by <= 175 bytes, at least one frame per GPU lane: one lane per frame,
+    the next frame loaded while this one is deciphered.  300 000 frames of 0-175 bytes
+    (FPNN's 145, whole blocks, 1-15-byte tails, empty, under 16 B) at unaligned offsets, a
+    few past the bound (block by block), one key or keyed connections, in place and not,
+    against the oracle; and the batch without the bound (K1r) gives the same bytes."""
+    import fpnn_amd
+    rng = np.random.default_rng(9900 + keylen + nk + 5 * inplace)
+    n = 300_000
+    lens = rng.integers(0, 176, n).astype(np.int64)
+    pick = rng.random(n)
+    lens[pick < 0.3] = 145
+    lens[(pick >= 0.3) & (pick < 0.4)] = 16 * rng.integers(0, 11, int(((pick >= 0.3) & (pick < 0.4)).sum()))
+    over = rng.integers(0, n, 40)
+    lens[over] = rng.integers(176, 401, 40)  # (past the caller's bound)
+    gaps = rng.integers(0, 3, n)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1] + gaps[:-1])]).astype(np.int64) + 1
+    keys = rng.integers(0, 256, nk * keylen, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nk * 16, dtype=np.uint8)
+    slots = rng.integers(0, nk, n).astype(np.int32)
+    ks = keyset(engine, keys, keylen, ivs)
+    total = int(offs[-1] + lens[-1])  # (the last frame ends the buffer)
+    inp = rng.integers(0, 256, total, dtype=np.uint8)
+    kw = dict(in_off=to_dev(offs), lens=to_dev(lens.astype(np.int32)))
+    if nk > 1:
+        kw["key_slot"] = to_dev(slots)
+    exp = inp.copy()
+    oracle.package_batch(False, inp, exp, n, in_off=offs.astype(np.uint64), lens=lens.astype(np.uint32),
+                         key_slot=slots.astype(np.uint32) if nk > 1 else None, keys=keys, keylen=keylen, ivs=ivs,
+                         threads=8)
+    src = to_dev(inp)
+    dst = src if inplace else to_dev(rng.integers(0, 256, total, dtype=np.uint8))
+    if not inplace:  # bytes between frames keep the destination's own
+        keep = np.ones(total, bool)
+        for o, ln in zip(offs, lens):
+            keep[o:o + ln] = False
+        exp = np.where(keep, to_host(dst), exp)
+    engine.package_decrypt(src, dst, n, ks, max_len=175, **kw)
+    torch.cuda.synchronize()
+    assert engine.last_kernel(fpnn_amd.K_DECRYPT) == "cfb_decrypt_frames"
+    got = to_host(dst)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, f"{len(bad)} bytes differ, first at {bad[:8]}"
+    if not inplace:
+        dst2 = to_dev(to_host(dst))
+        engine.package_decrypt(src, dst2, n, ks, **kw)  # no bound: K1r
+        torch.cuda.synchronize()
+        assert engine.last_kernel(fpnn_amd.K_DECRYPT) != "cfb_decrypt_frames"
+        assert torch.equal(dst2, dst)
+
+
 @pytest.mark.parametrize("keylen", [16, 32])
 @pytest.mark.parametrize("eng_kind", ["engine", "hybrid_lane_engine", "hybrid_quad_engine"])
 def test_keyset_writes_refresh_first_keystream_block(request, oracle, keylen, eng_kind):
