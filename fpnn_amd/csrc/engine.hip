@@ -693,9 +693,9 @@ int run_encrypt_calls(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint8_t *iv_s
     if (!b->len) k.flags |= F_ALIGN_CHUNKS;
     EventPair *ev;
     if ((rc = timing_begin(e, FPNN_AES_K_ENCRYPT, &ev))) return rc;
-    if (k2_ragged && b->max_len <= kFrameMaxBytes)  // FPNN's quests: whole frames at once (K2s)
-        HIP_TRY(launch_encrypt_frames(k, b->keys->nrounds, km, (b->flags & FPNN_AES_F_WIRE_PREFIX) != 0, grid, threads,
-                                      e->stream));
+    if (k2_ragged && b->max_len <= kFrameMaxBytes)  // FPNN's quests: whole frames at once (K2s-DB)
+        HIP_TRY(launch_encrypt_frames(k, b->keys->nrounds, km, (b->flags & FPNN_AES_F_WIRE_PREFIX) != 0,
+                                      e->num_cus, e->stream));
     else
         HIP_TRY(launch_encrypt_chains(k, b->keys->nrounds, layout, km, stream, grid, threads, e->stream));
     return timing_end(e, ev, FPNN_AES_K_ENCRYPT);

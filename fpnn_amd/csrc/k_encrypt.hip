@@ -179,17 +179,14 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_enc
 // its algorithmic HBM bytes (reads 2.52x, writes 2.16x; profiles/r05/Q1s_final, VERDICT r05
 // item 3).  Here a wave's 64 frames -- one contiguous span for a collector's flush -- are
 // read by back-to-back loads and written by back-to-back stores, so every line is read
-// once and written whole while L2 still holds it.
+// once and written whole while L2 still holds it: 1.01-1.02x.
 
-// One chain of K2s: MAXB-block passes (see k_cfb_encrypt_frames).
+// A frame past the pipeline's slots (past the caller's bound, or under 16 B) in MAXB-block
+// passes: K2s-DB's rare path.
 template <int NR, int KM, bool WIRE, int MAXB>
 __device__ __forceinline__ void frame_passes(const KBatch &b, const Seg &g, const uint4 &eiv, const RoundKeys<NR> &key,
                                              const Tables4<4> &T, const uint8_t *dummy) {
-#ifdef FPNN_AES_K2S_NO_TAILSLOT
-    constexpr bool kTailSlot = false;  // (probe build: tools/probe/build_variant.sh)
-#else
     constexpr bool kTailSlot = true;
-#endif
     constexpr int NT = 4;
     FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len, a_olo = (uintptr_t)g.out,
             a_ohi = (uintptr_t)g.out + g.len + (WIRE ? 4u : 0u));
@@ -255,48 +252,6 @@ __device__ __forceinline__ void frame_passes(const KBatch &b, const Seg &g, cons
     }
 }
 
-template <int NR, int KM, bool WIRE>
-__global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
-    // 10 blocks a pass: a 145-B quest's 9 whole blocks and its partial one.  (Per-lane
-    // AES-256 round keys hold 60 VGPRs, and 10 slots spill 3 VGPRs (12 B/lane) there; 9
-    // slots and a separate round trip for the tail measured 746 against 781-786 GiB/s on
-    // Q1, r06i.)
-    constexpr int NT = 4, MAXB = kFrameMaxBlocks;
-    __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
-    lds_fill_tables<NT>(lds4, b.t0le);
-    __syncthreads();
-    const Tables4<NT> T{reinterpret_cast<const char *>(lds4), LaneBase()};
-
-    RoundKeys<NR> rku;
-    uint4 eiv_u = make_uint4(0, 0, 0, 0);
-    if (KM == KEY_UNIFORM) {
-        rku = load_round_keys<NR>(b.keys);
-        eiv_u = aes_encrypt_block<NR, NT>(*reinterpret_cast<const uint4 *>(b.keys->iv), rku, T);
-    }
-    const uint8_t *const dummy = reinterpret_cast<const uint8_t *>(b.keys);  // 272 readable bytes
-    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-    RoundKeys<NR> rk;  // per-lane keys: kept while the lane's next chain has the same slot
-    if (KM != KEY_UNIFORM) {
-#pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); i++) rk.k[i] = 0u;
-    }
-    uint32_t rk_slot = ~0u;
-    // The IV itself is never needed: block 0's keystream is E_k(IV), every later one comes
-    // from the ciphertext.  (Measured and not kept, tools/ab_frames.py: loading the next
-    // chain's descriptor during this chain, -5 % on Q1s / Q1w (r06g); the second half of a
-    // pass loaded behind block 0, -8 % (r06h); waves of a CU starting one chain-step apart,
-    // +1 % Q1s / -1 % Q1 / -3 % Q1w (r06h, r06i).)
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < b.count; s += nthreads) {
-        const Seg g = get_seg<LAYOUT_GENERAL>(b, s);
-        const uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
-        if (KM != KEY_UNIFORM && g.slot != rk_slot) {
-            rk = load_round_keys<NR>(FA_AT(b, AB_KEYS, b.keys + g.slot, sizeof(DevKey)));
-            rk_slot = g.slot;
-        }
-        frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // K2s-DB: K2s with the next chain's frame in flight while this one is ciphered.  In K2s every
 // chain starts with the same two round trips (descriptor, then frame), and the waves of a CU
@@ -309,7 +264,14 @@ __global__ __launch_bounds__(kThreads, 4) void k_cfb_encrypt_frames(KBatch b) {
 //
 // A frame "fits" when its whole blocks and partial block take at most MAXB slots; its
 // partial block is then loaded as the frame's LAST 16 bytes (inside the frame) and shifted
-// down.  Frames past the caller's bound and frames under 16 B take the K2s passes.
+// down.  Frames past the caller's bound and frames under 16 B take frame_passes (encrypt)
+// or frame_decrypt_blocks (decrypt).
+//
+// Measured and not kept (tools/ab_frames.py over tools/probe/build_variant.sh builds, DESIGN
+// section 4): K2s at 4 waves per SIMD with no frame in flight (Q1s 903-916, Q1w 754 against
+// 960-968 / 891-939); 3 waves per SIMD (spills with AES-256 lane keys); two store bursts
+// per frame, the next frame loading into the first half's registers; the next descriptor
+// alone loaded ahead; waves of a CU started a chain step apart.
 
 struct FrameShape {
     uint32_t nfull, tail;
@@ -324,33 +286,31 @@ __device__ __forceinline__ FrameShape frame_shape(const Seg &g, int maxb) {
     return f;
 }
 
-template <int MAXB, int LO = 0, int HI = MAXB>
+template <int MAXB>
 __device__ __forceinline__ void frame_issue(const KBatch &b, const Seg &g, const FrameShape &f, uint4 (&x)[MAXB],
                                             const uint8_t *dummy) {
     FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len);
 #pragma unroll
-    for (int j = LO; j < HI; j++)
+    for (int j = 0; j < MAXB; j++)
         x[j] = load16(j < (int)f.nfull                   ? FA_SEG(b, AB_IN, g.in + 16 * j, 16, a_ilo, a_ihi)
                       : (f.tail && j == (int)f.nfull) ? FA_SEG(b, AB_IN, g.in + g.len - 16, 16, a_ilo, a_ihi)
                                                       : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
 }
 
-// Store slots [LO, HI) of a fitted frame: its whole blocks there, and its partial block if
-// that block's slot is there.
-template <int LO, int HI, int MAXB>
+// Store a fitted frame's slots in one burst: its whole blocks, then its partial block.
+template <int MAXB>
 __device__ __forceinline__ void frame_store(const KBatch &b, const uint4 (&A)[MAXB], const FrameShape &f, uint8_t *o,
                                             uint64_t a_olo, uint64_t a_ohi) {
     (void)a_olo;
     (void)a_ohi;
-    uint4 t = A[LO];  // the partial block's slot, picked by selects
+    uint4 t = A[0];  // the partial block's slot, picked by selects
 #pragma unroll
-    for (int j = LO + 1; j < HI; j++)
+    for (int j = 1; j < MAXB; j++)
         if (j == (int)f.nfull) t = A[j];
 #pragma unroll
-    for (int j = LO; j < HI; j++)
+    for (int j = 0; j < MAXB; j++)
         if (j < (int)f.nfull) store16(FA_SEG(b, AB_OUT, o + 16 * j, 16, a_olo, a_ohi), A[j]);
-    if (f.tail && (int)f.nfull >= LO && (int)f.nfull < HI)
-        store_bytes(FA_RG(b, AB_OUT, o + 16 * f.nfull, 0, f.tail, a_olo, a_ohi), t, 0, (int)f.tail);
+    if (f.tail) store_bytes(FA_RG(b, AB_OUT, o + 16 * f.nfull, 0, f.tail, a_olo, a_ohi), t, 0, (int)f.tail);
 }
 
 // One chain of a decrypt past the bound (or under 16 B): block by block.  P_i = C_i ^
@@ -377,8 +337,8 @@ __device__ __forceinline__ void frame_decrypt_blocks(const KBatch &b, const Seg 
 
 // DEC: the same pipeline decrypts (D2s): block j's keystream is E(C_{j-1}), the ciphertext
 // just loaded, so a lane's AES passes are independent of each other.
-template <int NR, int KM, bool WIRE, int OCC, int HS, bool RING, bool DEC = false>
-__global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_cfb_encrypt_frames_db(
+template <int NR, int KM, bool WIRE, int OCC, bool DEC>
+__global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void k_cfb_frames_db(
     KBatch b) {
     constexpr int NT = 4, MAXB = kFrameMaxBlocks;
     __shared__ uint4 lds4[Lds<NT>::kBytes / 16];
@@ -426,16 +386,10 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
             uint4 iv = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < MAXB; j++) {
-                if (j == (HS ? HS : 2)) {
-                    // HS: slots [0, HS) are stored first and the next chain's frame loads into
-                    // them (one frame of registers less in flight); else it loads behind block 1
-                    if (HS) frame_store<0, HS, MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));
+                if (j == 2) {  // the next chain's frame and E_k(IV), behind this chain's block 1
                     fb = frame_shape(gn, MAXB);
                     fb.fit = fb.fit && more;
-                    if (fb.fit) {
-                        if (RING) frame_issue<MAXB, 0, HS>(b, gn, fb, A, dummy);  // into the stored slots
-                        else frame_issue<MAXB>(b, gn, fb, B, dummy);
-                    }
+                    if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
                     if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
                 }
                 if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
@@ -450,14 +404,13 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
                     }
                 }
             }
-            frame_store<HS, MAXB, MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));
-            if (RING && fb.fit) frame_issue<MAXB, HS, MAXB>(b, gn, fb, A, dummy);  // the rest of the next frame
+            frame_store<MAXB>(b, A, fa, o, FA_ARGS(a_olo, a_ohi));  // (one burst: two measured slower, r06l)
         } else {
             if (DEC) frame_decrypt_blocks<NR>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T);
             else frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
             fb = frame_shape(gn, MAXB);
             fb.fit = fb.fit && more;
-            if (fb.fit) frame_issue<MAXB>(b, gn, fb, RING ? A : B, dummy);
+            if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
             if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
         }
         if (!more) break;
@@ -465,10 +418,8 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
         g = gn;
         fa = fb;
         eiv = eivn;
-        if (!RING) {
 #pragma unroll
-            for (int j = 0; j < MAXB; j++) A[j] = B[j];
-        }
+        for (int j = 0; j < MAXB; j++) A[j] = B[j];
     }
 }
 
@@ -671,31 +622,20 @@ hipError_t launch_encrypt_coop(const KBatch &b, int nrounds, Layout layout, KeyM
     return hipGetLastError();
 }
 
-// K2s-DB's waves per SIMD (0: K2s; the probe builds of tools/probe/build_variant.sh set it)
+// K2s-DB's and D2s's waves per SIMD (3 spilled with AES-256 lane keys and measured slower,
+// r06k / r06m; probe builds of tools/probe/build_variant.sh may set them)
 #ifndef FPNN_AES_K2S_DB_OCC
 #define FPNN_AES_K2S_DB_OCC 2
 #endif
-#ifndef FPNN_AES_K2S_DB_HS
-#define FPNN_AES_K2S_DB_HS 0
-#endif
-#ifndef FPNN_AES_K2S_DB_RING
-#define FPNN_AES_K2S_DB_RING 0
-#endif
-// D2s's waves per SIMD (probe builds set it)
 #ifndef FPNN_AES_D2S_OCC
 #define FPNN_AES_D2S_OCC 2
 #endif
 
 template <int NR>
-static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int threads, hipStream_t st) {
-#if FPNN_AES_K2S_DB_OCC
-    (void)threads;  // one workgroup of 256 * OCC threads per CU
-#define FPNN_FR(K, W)                                                                                          \
-    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, W, FPNN_AES_K2S_DB_OCC, FPNN_AES_K2S_DB_HS, FPNN_AES_K2S_DB_RING>), dim3(grid), \
+static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, hipStream_t st) {
+#define FPNN_FR(K, W)                                                                                              \
+    hipLaunchKernelGGL((k_cfb_frames_db<NR, K, W, FPNN_AES_K2S_DB_OCC, false>), dim3(grid),                 \
                        dim3(256 * FPNN_AES_K2S_DB_OCC), 0, st, b)
-#else
-#define FPNN_FR(K, W) hipLaunchKernelGGL((k_cfb_encrypt_frames<NR, K, W>), dim3(grid), dim3(threads), 0, st, b)
-#endif
     if (km == KEY_UNIFORM) {
         if (wire) FPNN_FR(KEY_UNIFORM, true); else FPNN_FR(KEY_UNIFORM, false);
     } else {
@@ -706,8 +646,8 @@ static void frames_nr(const KBatch &b, KeyMode km, bool wire, int grid, int thre
 
 template <int NR>
 static void dframes_nr(const KBatch &b, KeyMode km, int grid, hipStream_t st) {
-#define FPNN_DF(K)                                                                                               \
-    hipLaunchKernelGGL((k_cfb_encrypt_frames_db<NR, K, false, FPNN_AES_D2S_OCC, 0, false, true>), dim3(grid),   \
+#define FPNN_DF(K)                                                                                                 \
+    hipLaunchKernelGGL((k_cfb_frames_db<NR, K, false, FPNN_AES_D2S_OCC, true>), dim3(grid),                 \
                        dim3(256 * FPNN_AES_D2S_OCC), 0, st, b)
     if (km == KEY_UNIFORM) FPNN_DF(KEY_UNIFORM);
     else FPNN_DF(KEY_LANE);
@@ -725,13 +665,12 @@ hipError_t launch_decrypt_frames(const KBatch &b, int nrounds, KeyMode km, int g
     return hipGetLastError();
 }
 
-hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, int threads,
-                                 hipStream_t st) {
+hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, hipStream_t st) {
     set_launched("cfb_encrypt_frames");
     switch (nrounds) {
-        case 10: frames_nr<10>(b, km, wire, grid, threads, st); break;
-        case 12: frames_nr<12>(b, km, wire, grid, threads, st); break;
-        case 14: frames_nr<14>(b, km, wire, grid, threads, st); break;
+        case 10: frames_nr<10>(b, km, wire, grid, st); break;
+        case 12: frames_nr<12>(b, km, wire, grid, st); break;
+        case 14: frames_nr<14>(b, km, wire, grid, st); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

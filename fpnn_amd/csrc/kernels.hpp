@@ -117,13 +117,13 @@ struct KScan {
 hipError_t launch_scan_frames(const KScan &s, bool stream, int num_cus, hipStream_t st);
 hipError_t launch_encrypt_chains(const KBatch &b, int nrounds, Layout layout, KeyMode km, bool stream, int grid,
                                  int threads, hipStream_t st);
-// K2s (k_encrypt.hip): ragged package batches of short frames -- every len <= kFrameMaxBytes
-// (the caller's fpnn_aes_batch.max_len) -- one lane per chain, the whole frame loaded,
-// ciphered and stored at once; wire = the 4-byte length prefix (FPNN_AES_F_WIRE_PREFIX).
+// K2s-DB (k_encrypt.hip): ragged package batches of short frames -- every len <=
+// kFrameMaxBytes (the caller's fpnn_aes_batch.max_len) -- one lane per chain, the whole frame
+// loaded, ciphered and stored at once while the lane's next frame loads; wire = the 4-byte
+// length prefix (FPNN_AES_F_WIRE_PREFIX); grid = one workgroup per CU.
 constexpr int kFrameMaxBlocks = 10;
 constexpr uint32_t kFrameMaxBytes = 16u * kFrameMaxBlocks + 15u;  // 175: FPNN's 145-B quests and shorter
-hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, int threads,
-                                 hipStream_t st);
+hipError_t launch_encrypt_frames(const KBatch &b, int nrounds, KeyMode km, bool wire, int grid, hipStream_t st);
 // D2s: the same pipeline for package decrypts of short frames (one lane per frame, its
 // blocks' AES passes independent of each other); grid = one workgroup per CU
 hipError_t launch_decrypt_frames(const KBatch &b, int nrounds, KeyMode km, int grid, hipStream_t st);

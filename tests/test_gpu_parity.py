@@ -335,7 +335,7 @@ def test_many_short_frames_bounded_length_take_lane_chains(engine, oracle, keyle
 @pytest.mark.parametrize("keylen,nk", [(16, 1000), (24, 7), (32, 1000), (32, 1)])
 @pytest.mark.parametrize("wire", [False, True])
 def test_short_frames_whole_frame_passes(engine, oracle, keylen, nk, wire):
-    """K2s (k_cfb_encrypt_frames, round 6): ragged package encrypts whose caller bounds every
+    """K2s-DB (k_cfb_frames_db, round 6): ragged package encrypts whose caller bounds every
     length by <= 175 bytes (fpnn_aes_batch.max_len; FPNN's 145-B quests) with at least one
     chain per GPU lane load each frame whole, cipher it in registers and store it whole.
     300 000 frames of 0-175 bytes (FPNN's 145, whole blocks, 1-15-byte tails, empty) at
@@ -386,7 +386,7 @@ def test_short_frames_whole_frame_passes(engine, oracle, keylen, nk, wire):
 @pytest.mark.parametrize("keylen,nk", [(16, 1000), (24, 7), (32, 1000), (32, 1)])
 @pytest.mark.parametrize("inplace", [False, True])
 def test_short_frames_decrypt_whole_frames(engine, oracle, keylen, nk, inplace):
-    """D2s (k_cfb_encrypt_frames_db<..., DEC>, round 6): ragged package decrypts whose caller
+    """D2s (k_cfb_frames_db<..., DEC>, round 6): ragged package decrypts whose caller
     bounds every length by <= 175 bytes, at least one frame per GPU lane: one lane per frame,
     the next frame loaded while this one is deciphered.  300 000 frames of 0-175 bytes
     (FPNN's 145, whole blocks, 1-15-byte tails, empty, under 16 B) at unaligned offsets, a
