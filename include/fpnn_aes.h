@@ -157,8 +157,10 @@ typedef struct {
                                    Ragged package encrypts of many short frames (max_len <=
                                    2048, count >= 1 chain per GPU lane, i.e. 256 CUs x 1024)
                                    then run one lane per chain in grid-stride order (K2;
-                                   with max_len <= 175, FPNN's quests, K2s: each frame
-                                   loaded, ciphered and stored whole in one pass);
+                                   with max_len <= 175, FPNN's quests, K2s-DB: each frame
+                                   loaded, ciphered and stored whole in one pass, the next
+                                   one loading meanwhile; package decrypts with that bound
+                                   likewise, D2s);
                                    without the bound, or with fewer chains, the
                                    length-ordered hybrid (K2h), whose work queue also balances
                                    Zipf-like lengths.  (Was `reserved`, 0: same layout.) */
