@@ -1340,6 +1340,7 @@ int fpnn_aes_package_recv(fpnn_aes_engine *e, const fpnn_aes_batch *b, uint32_t 
     fb.len = frame_len;
     fb.key_slot = per_key ? e->d_fr_slot : nullptr;
     fb.keys = b->keys;
+    fb.max_len = max_len;  // (every frame the scan accepts is within it: D2s for FPNN's quests)
     return run_decrypt(e, &fb, nullptr, nullptr, false);
 }
 

@@ -1112,6 +1112,53 @@ def test_package_recv_frames(engine, oracle, inplace, scan_mode):
     assert (status == PO.SCAN_FULL).any() and (status == PO.SCAN_TOO_LARGE).any()
 
 
+@pytest.mark.parametrize("inplace", [False, True])
+def test_package_recv_quests_whole_frames(engine, inplace):
+    """fpnn_aes_package_recv with a frame-size cap of 175 B over 16 384 connections x 16
+    frame slots: every accepted frame is within the cap, so the decrypt behind the scan takes
+    D2s (one lane per frame).  FPNN's 145-B quests (and a spread of shorter ones, empty
+    included) as wire frames htole32(len) || C made by the wire encrypt, received and
+    deciphered back to the plaintext."""
+    import fpnn_amd
+    rng = np.random.default_rng(3131 + inplace)
+    nconn, per, cap = 16384, 16, 175
+    keys = rng.integers(0, 256, nconn * 32, dtype=np.uint8)
+    ivs = rng.integers(0, 256, nconn * 16, dtype=np.uint8)
+    ks = fpnn_amd.KeySet(engine, keys.tobytes(), 32, ivs.tobytes())
+    nfr = rng.integers(0, per + 1, nconn)  # frames per connection
+    lens = np.where(rng.random((nconn, per)) < 0.6, 145, rng.integers(0, cap + 1, (nconn, per)))
+    lens[np.arange(per)[None, :] >= nfr[:, None]] = 0
+    flat_len = lens.reshape(-1).astype(np.int64)
+    conn = np.repeat(np.arange(nconn), per)
+    wire_len = np.where(np.arange(per)[None, :] < nfr[:, None], lens + 4, 0)
+    seg_len = wire_len.sum(1)
+    seg_off = np.concatenate([[0], np.cumsum(seg_len[:-1] + 3)]).astype(np.int64)
+    wout = (seg_off[:, None] + np.concatenate([np.zeros((nconn, 1), np.int64), np.cumsum(wire_len, 1)[:, :-1]], 1))
+    plain_off = np.concatenate([[0], np.cumsum(flat_len[:-1])]).astype(np.int64)
+    plain = rng.integers(0, 256, int(flat_len.sum()) + 1, dtype=np.uint8)
+    live = (np.arange(per)[None, :] < nfr[:, None]).reshape(-1)
+    n = int(live.sum())
+    wire = torch.zeros(int(seg_off[-1] + seg_len[-1] + 3), dtype=torch.uint8, device=DEV)
+    engine.package_encrypt(to_dev(plain), wire, n, ks, wire_prefix=True, max_len=cap,
+                           in_off=to_dev(plain_off[live]), out_off=to_dev(wout.reshape(-1)[live]),
+                           lens=to_dev(flat_len[live].astype(np.int32)), key_slot=to_dev(conn[live].astype(np.int32)))
+    out = wire if inplace else torch.zeros_like(wire)
+    foff, flen, scan = engine.package_recv(wire, out, nconn, ks, cap, per, in_off=to_dev(seg_off),
+                                           lens=to_dev(seg_len.astype(np.int32)),
+                                           key_slot=to_dev(np.arange(nconn, dtype=np.int32)))
+    torch.cuda.synchronize()
+    assert engine.last_kernel(fpnn_amd.K_DECRYPT) == "cfb_decrypt_frames"
+    frames, status, consumed = fpnn_amd.Engine.decode_scan(scan)
+    assert (frames == nfr).all() and (consumed == seg_len).all()
+    res, fo, fl = to_host(out), to_host(foff), to_host(flen)
+    got_idx = (seg_off[:, None] + fo.reshape(nconn, per).astype(np.int64)).reshape(-1)[live]
+    assert (fl.reshape(-1)[live] == flat_len[live]).all()
+    for i in np.nonzero(live)[0][rng.permutation(int(live.sum()))[:20000]]:
+        o, ln, po = int(seg_off[conn[i]] + fo[i]), int(flat_len[i]), int(plain_off[i])
+        assert np.array_equal(res[o:o + ln], plain[po:po + ln]), i
+    assert len(got_idx) == n
+
+
 def _fpnn_message(rng, mtype, ss, psize):
     hdr = b"FPNN" + bytes([1, 0x80, mtype, ss]) + psize.to_bytes(4, "little")
     body = {1: psize + ss + 4, 2: psize + 4, 0: psize + ss}[mtype]
