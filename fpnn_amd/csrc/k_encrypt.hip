@@ -273,10 +273,6 @@ __device__ __forceinline__ void frame_passes(const KBatch &b, const Seg &g, cons
 // per frame, the next frame loading into the first half's registers; the next descriptor
 // alone loaded ahead; waves of a CU started a chain step apart.
 
-#ifndef FPNN_AES_FRAMES_NB
-#define FPNN_AES_FRAMES_NB kFrameMaxBlocks
-#endif
-
 struct FrameShape {
     uint32_t nfull, tail;
     bool fit;
@@ -290,13 +286,12 @@ __device__ __forceinline__ FrameShape frame_shape(const Seg &g, int maxb) {
     return f;
 }
 
-// slots [LO, HI) of a frame into x[LO, HI)
-template <int N, int LO = 0, int HI = N>
-__device__ __forceinline__ void frame_issue(const KBatch &b, const Seg &g, const FrameShape &f, uint4 (&x)[N],
+template <int MAXB>
+__device__ __forceinline__ void frame_issue(const KBatch &b, const Seg &g, const FrameShape &f, uint4 (&x)[MAXB],
                                             const uint8_t *dummy) {
     FA_DECL(a_ilo = (uintptr_t)g.in, a_ihi = (uintptr_t)g.in + g.len);
 #pragma unroll
-    for (int j = LO; j < HI; j++)
+    for (int j = 0; j < MAXB; j++)
         x[j] = load16(j < (int)f.nfull                   ? FA_SEG(b, AB_IN, g.in + 16 * j, 16, a_ilo, a_ihi)
                       : (f.tail && j == (int)f.nfull) ? FA_SEG(b, AB_IN, g.in + g.len - 16, 16, a_ilo, a_ihi)
                                                       : FA_AT(b, AB_KEYS, dummy + 16 * j, 16));
@@ -370,10 +365,7 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
     Seg g = get_seg<LAYOUT_GENERAL>(b, s);
     FrameShape fa = frame_shape(g, MAXB);
     uint4 eiv = KM == KEY_UNIFORM ? eiv_u : *FA_AT(b, AB_EIV, b.eiv + g.slot, 16);
-    // NB: slots of the next frame loaded behind block 1 (into B); the rest load into A right
-    // after this frame's store burst, a half chain before they are needed
-    constexpr int NB = FPNN_AES_FRAMES_NB < MAXB ? FPNN_AES_FRAMES_NB : MAXB;
-    uint4 A[MAXB], B[NB];
+    uint4 A[MAXB], B[MAXB];
     if (fa.fit) frame_issue<MAXB>(b, g, fa, A, dummy);
     for (;;) {
         const uint64_t sn = s + nthreads;
@@ -397,7 +389,7 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
                 if (j == 2) {  // the next chain's frame and E_k(IV), behind this chain's block 1
                     fb = frame_shape(gn, MAXB);
                     fb.fit = fb.fit && more;
-                    if (fb.fit) frame_issue<NB>(b, gn, fb, B, dummy);
+                    if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
                     if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
                 }
                 if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
@@ -418,7 +410,7 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
             else frame_passes<NR, KM, WIRE, MAXB>(b, g, eiv, KM == KEY_UNIFORM ? rku : rk, T, dummy);
             fb = frame_shape(gn, MAXB);
             fb.fit = fb.fit && more;
-            if (fb.fit) frame_issue<NB>(b, gn, fb, B, dummy);
+            if (fb.fit) frame_issue<MAXB>(b, gn, fb, B, dummy);
             if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
         }
         if (!more) break;
@@ -427,8 +419,7 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
         fa = fb;
         eiv = eivn;
 #pragma unroll
-        for (int j = 0; j < NB; j++) A[j] = B[j];
-        if (NB < MAXB && fa.fit) frame_issue<MAXB, NB, MAXB>(b, g, fa, A, dummy);
+        for (int j = 0; j < MAXB; j++) A[j] = B[j];
     }
 }
 
