@@ -271,7 +271,11 @@ __device__ __forceinline__ void frame_passes(const KBatch &b, const Seg &g, cons
 // section 4): K2s at 4 waves per SIMD with no frame in flight (Q1s 903-916, Q1w 754 against
 // 960-968 / 891-939); 3 waves per SIMD (spills with AES-256 lane keys); two store bursts
 // per frame, the next frame loading into the first half's registers; the next descriptor
-// alone loaded ahead; waves of a CU started a chain step apart.
+// alone loaded ahead; waves of a CU started a chain step apart; a decrypt's passes run 2 or
+// 3 at a time, round-interleaved (equal); every global access of the steady state issued
+// unconditionally -- buffer stores through an output window, unused slots dropped past it
+// -- so that the compiler's waits count them instead of collapsing to vmcnt(0) at each
+// join (with fenced rounds: encrypt equal, Q1s decrypt 990 -> 972, profiles/r06/ab_fence).
 
 struct FrameShape {
     uint32_t nfull, tail;
@@ -393,7 +397,10 @@ __global__ __launch_bounds__(256 * OCC) __attribute__((amdgpu_waves_per_eu(OCC, 
                     if (KM != KEY_UNIFORM) eivn = *FA_AT(b, AB_EIV, b.eiv + gn.slot, 16);
                 }
                 if (j < (int)fa.nfull || (fa.tail && j == (int)fa.nfull)) {
-                    const uint4 ks = j == 0 ? eiv : aes_encrypt_block<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
+                    // fenced rounds (every lookup of a round issued before any fold): Q1 encrypt /
+                    // decrypt 784-786 / 782-792 -> 811-813 / 815-823 GiB/s, Q1s 961-963 / 963-966
+                    // -> 985-988 / 990-991, Q1w 921 -> 929-931 (profiles/r06/ab_fence)
+                    const uint4 ks = j == 0 ? eiv : aes_encrypt_block_fenced<NR, NT>(iv, KM == KEY_UNIFORM ? rku : rk, T);
                     const uint4 x = j == (int)fa.nfull ? shr_bytes(A[j], 16 - (int)fa.tail) : A[j];
                     if (DEC) {  // P_i = C_i ^ E(C_{i-1}); iv carries the ciphertext
                         A[j] = x ^ ks;
