@@ -330,7 +330,8 @@ __global__ __launch_bounds__(kThreads, 4 * Lds<NT>::kBlocksPerCU) void k_cfb_dec
                          wave_shr1(X.x.w, fill.w));
         if (lane != 0 && bi == 0) kin = ivl;
         if (pref) load(c + nwaves, NX);
-        const uint4 ks = aes_encrypt_block<NR, NT>(kin, rk, T);
+        // fenced rounds: U1 decrypt 1 147-1 149 -> 1 163-1 173 GiB/s (profiles/r06/ab_k1k_fence)
+        const uint4 ks = aes_encrypt_block_fenced<NR, NT>(kin, rk, T);
         if ((c << 6) + lane < total) store16(b.out + 16ull * ((c << 6) + lane), X.x ^ ks);
     };
     uint64_t c = w0;
