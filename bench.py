@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time pinned H2D + kernels + D2H (for DESIGN.md)")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL; default) or gloo (rehearsal)")
+    ap.add_argument("--dist-backend", default="auto",
+                    help="auto (RCCL when every local rank has a GPU of its own, else gloo: RCCL refuses two ranks "
+                         "on one device), nccl or gloo")
     ap.add_argument("--workload", choices=["C2", "C4", "C5"], default="C2",
                     help="C2 = the bench line (default); C4 / C5 = the BASELINE.json sharded configs")
     ap.add_argument("--only", choices=["encrypt", "decrypt"], default=None,
@@ -127,7 +129,12 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
-    dev = local % max(1, torch.cuda.device_count())  # == local on a node with one GPU per rank
+    ndev = max(1, torch.cuda.device_count())  # (counting devices does not initialise the GPU)
+    dev = local % ndev  # == local on a node with one GPU per rank
+    if args.dist_backend == "auto":
+        # the data path has no collective; torch.distributed carries only the barrier and the
+        # reductions of the timing, so ranks that share a device (a rehearsal) take gloo
+        args.dist_backend = "nccl" if int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) <= ndev else "gloo"
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
